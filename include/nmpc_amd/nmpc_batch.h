@@ -1,0 +1,117 @@
+/*
+ * nmpc_batch.h -- batched MI355X SQP-RTI solve path (libnmpc_amd.so), C ABI.
+ *
+ * The batched entry points behind which thousands of NMPCNavControl*::run() calls of the reference
+ * (src/nmpc_nav_control/NMPCNavControl{Diff,Omni4,Tric}.cpp:82/91/88) execute as one device launch.
+ * The per-robot acados-compatible ABI ({name}_acados_*, ocp_nlp_*) lives in acados_solver_{name}.h
+ * and acados_c/ocp_nlp_interface.h and is implemented on top of these functions.
+ *
+ * Conventions
+ *   - All array arguments of nmpc_batch_solve / nmpc_batch_run are DEVICE pointers (hipMalloc or torch
+ *     CUDA tensors), fp32, instance-minor "[field][B]" layout so that lane i of a wave reads element i.
+ *   - `stream` is a hipStream_t (NULL = default stream). Calls are asynchronous on that stream.
+ *   - Return value: 0 on success, < 0 on an API error (see nmpc_last_error()). Per-instance solver
+ *     status codes follow acados (0 success, 1 NaN detected, 4 QP failure) and are written to `status`.
+ *   - Array outputs may be NULL when not wanted.
+ */
+#ifndef NMPC_AMD_NMPC_BATCH_H
+#define NMPC_AMD_NMPC_BATCH_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NMPC_MODEL_DIFF2AMR 0
+#define NMPC_MODEL_OMNI4AMR 1
+#define NMPC_MODEL_TRIC3AMR 2
+
+#define NMPC_OK 0
+#define NMPC_ERR_ARG (-1)
+#define NMPC_ERR_HIP (-2)
+#define NMPC_ERR_UNSUPPORTED (-3)
+
+/* Model + OCP + solver configuration. Mirrors the two parameter surfaces of the reference:
+ *   codegen yaml  config/nmpc_nav_control_acados_models.yaml  (N, dt = 1/freq; bakes the model)
+ *   ROS yaml      config/nmpc_nav_control.yaml                (dt_ctrl = 1/control_freq, p, bounds, W) */
+typedef struct nmpc_model_params {
+    int model; /* NMPC_MODEL_* */
+    int N;     /* horizon (common.py:6: N = ceil(tf_ini / dt)) */
+    double dt;      /* solver time step */
+    double dt_ctrl; /* wrapper time step used for vel_ref integration (NMPCNavControlDiff.cpp:155-157) */
+    double p[3];    /* diff {b, tau_v}; omni4 {l1+l2, tau_v}; tric {d, tau_v, tau_a} */
+    double lbx[4], ubx[4]; /* bounds of the ref states idxbx (stages 1..N) */
+    double lbu[4], ubu[4]; /* bounds of the inputs idxbu (stages 0..N-1) */
+    double W[15];   /* stage weight diagonal [Q_diag; R_diag] (NY entries) */
+    double W_e[11]; /* terminal weight diagonal (NX entries); constructors set it to Q_diag */
+    int terminal_hack; /* diff run(): x100 terminal pose weight when yref[N]==yref[N-1] (default 1 for diff) */
+    int tric_sin_bug;  /* tric_amr_model.py:45 cos_alpha = sin(alpha) (default 1: reproduce) */
+    int qp_iter_max;   /* 50 */
+    double qp_tol_stat, qp_tol_ineq, qp_tol_comp; /* fp32 stopping rule, see DESIGN.md */
+    double qp_mu0, qp_thr0, qp_tau;              /* IPM initial point and fraction-to-boundary */
+} nmpc_model_params;
+
+typedef struct nmpc_batch nmpc_batch;
+
+/* Dimensions of a model: nx, nu, ny (=nx+nu), nbx, nbu, np. Any pointer may be NULL. */
+int nmpc_model_dims(int model, int* nx, int* nu, int* ny, int* nbx, int* nbu, int* np);
+/* Defaults = the reference's shipped runtime configuration. */
+int nmpc_model_params_default(int model, int N, nmpc_model_params* prm);
+/* Bounds from the wrapper-constructor scalars (NMPCNavControlDiff.cpp:18-22, NMPCNavControlOmni4.cpp:18-22,
+ * NMPCNavControlTric.cpp:18-29): ref states in [-v_max, v_max] (tric alpha_ref in [alpha_min, alpha_max]),
+ * inputs in [-a_max, a_max] (tric dalpha_ref in [-dalpha_max, dalpha_max]); angles in radians. */
+int nmpc_model_params_set_limits(nmpc_model_params* prm, double v_max, double a_max, double alpha_min,
+                                 double alpha_max, double dalpha_max);
+
+/* Create a batch engine for up to `capacity` instances on the current HIP device. The iterate is
+ * initialised with {name}_acados_create semantics (x = [0,0,pi,0,...], u = 0) and carried refs = 0. */
+int nmpc_batch_create(const nmpc_model_params* prm, int capacity, nmpc_batch** out);
+int nmpc_batch_destroy(nmpc_batch* b);
+/* Replace weights / bounds / parameters / QP options (model and N must not change). */
+int nmpc_batch_set_params(nmpc_batch* b, const nmpc_model_params* prm);
+int nmpc_batch_get_params(const nmpc_batch* b, nmpc_model_params* prm);
+/* Re-initialise instances [0, B): mode 0 = create semantics, 1 = reset semantics (all zero). Both zero the
+ * carried ref states. */
+int nmpc_batch_init_iterate(nmpc_batch* b, int B, int mode, void* stream);
+
+/* One SQP-RTI iteration ({name}_acados_solve) for instances [0, B) on caller-packed QP data:
+ *   x0    [NX][B]          initial state (stage-0 lbx = ubx)
+ *   yref  [N+1][ny_in][B]  stage references; entries j >= ny_in are 0 (ny_in = 3 pose-only or NY);
+ *                          stage N uses entries 0..NX-1
+ *   We    [NX][B] or NULL  per-instance terminal weight diagonal (NULL: params W_e)
+ *   reset [B] or NULL      nonzero: zero the iterate before solving ({name}_acados_reset)
+ * outputs: u0 [NU][B], x1 [NX][B], xtraj [(N+1)*NX][B], utraj [N*NU][B], status [B], qp_iter [B],
+ *          qp_res [3][B] = {max |stationarity residual|, max |bound residual|, mu} at IPM exit. */
+int nmpc_batch_solve(nmpc_batch* b, int B, const float* x0, const float* yref, int ny_in, const float* We,
+                     const unsigned char* reset, float* u0, float* x1, float* xtraj, float* utraj, int* status,
+                     int* qp_iter, float* qp_res, void* stream);
+
+/* Batched NMPCNavControl*::run(): pre-solve + SQP-RTI + post-solve for B robots.
+ *   pose  [3][B] {x, y, theta}; vel [3][B] {v, vn, w}; steer [B] (tric; NULL = 0)
+ *   traj  [N+1][3][B] reference poses; traj_len [B] poses valid per robot (NULL = N+1; padded with the
+ *         last valid pose, NMPCNavControlDiff.cpp:113-117)
+ * outputs: cmd [3][B] (diff {v, w, 0}, omni4 {v, vn, w}, tric {v, alpha, 0}), u0 [NU][B], status, qp_iter,
+ * qp_res [3][B] (as nmpc_batch_solve). The carried vel-ref states are kept on the device between calls
+ * (NMPCNavControlDiff.cpp:168-172). */
+int nmpc_batch_run(nmpc_batch* b, int B, const float* pose, const float* vel, const float* steer,
+                   const float* traj, const int* traj_len, const unsigned char* reset, float* cmd, float* u0,
+                   int* status, int* qp_iter, float* qp_res, void* stream);
+
+/* Device pointers of the resident state: xbar [(N+1)*NX][stride], ubar [N*NU][stride],
+ * carried [NBX][stride]; stride = capacity. */
+int nmpc_batch_state(nmpc_batch* b, float** xbar, float** ubar, float** carried, int* stride);
+
+/* Bench / test harness: closed-loop plant step and path-reference regeneration for B robots
+ * (see DESIGN.md "Synthetic closed loop"). All device pointers, [field][B]:
+ *   path [6][B] = {x0, y0, th0, kappa, speed, length} circular-arc paths; goal-pose robots have length < 0
+ *   and {x0, y0, th0} is the goal. s [B] arc-length progress (in/out). pose/vel/steer in/out: advanced by
+ *   one RK4 step of the plant with the applied input u0 [NU][B]; traj [N+1][3][B], traj_len [B] out. */
+int nmpc_fleet_sim_step(nmpc_batch* b, int B, const float* path, float* s, float* pose, float* vel, float* steer,
+                        const float* u0, const int* status, float* traj, int* traj_len, int advance, void* stream);
+
+const char* nmpc_last_error(void);
+const char* nmpc_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,128 @@
+"""ctypes binding of libnmpc_amd.so (the HIP solve path). Fails loudly when the library is missing:
+there is no CPU fallback in the product package."""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_DIR = os.path.join(_HERE, "lib")
+LIB_PATH = os.path.join(LIB_DIR, "libnmpc_amd.so")
+
+MODEL_IDS = {"diff": 0, "omni4": 1, "tric": 2}
+MODEL_NAMES = {"diff": "diff2amr", "omni4": "omni4amr", "tric": "tric3amr"}
+
+c_int_p = ctypes.POINTER(ctypes.c_int)
+c_double_p = ctypes.POINTER(ctypes.c_double)
+c_void_p = ctypes.c_void_p
+
+
+class ModelParams(ctypes.Structure):
+    """Mirror of nmpc_model_params (include/nmpc_amd/nmpc_batch.h)."""
+    _fields_ = [
+        ("model", ctypes.c_int), ("N", ctypes.c_int),
+        ("dt", ctypes.c_double), ("dt_ctrl", ctypes.c_double),
+        ("p", ctypes.c_double * 3),
+        ("lbx", ctypes.c_double * 4), ("ubx", ctypes.c_double * 4),
+        ("lbu", ctypes.c_double * 4), ("ubu", ctypes.c_double * 4),
+        ("W", ctypes.c_double * 15), ("W_e", ctypes.c_double * 11),
+        ("terminal_hack", ctypes.c_int), ("tric_sin_bug", ctypes.c_int),
+        ("qp_iter_max", ctypes.c_int),
+        ("qp_tol_stat", ctypes.c_double), ("qp_tol_ineq", ctypes.c_double), ("qp_tol_comp", ctypes.c_double),
+        ("qp_mu0", ctypes.c_double), ("qp_thr0", ctypes.c_double), ("qp_tau", ctypes.c_double),
+    ]
+
+
+class NlpOut(ctypes.Structure):
+    """Mirror of the ocp_nlp_out handle (include/acados_c/ocp_nlp_interface.h)."""
+    _fields_ = [("impl", c_void_p), ("inf_norm_res", ctypes.c_double), ("total_cost", ctypes.c_double),
+                ("sqp_iter", ctypes.c_int)]
+
+
+class SolverCapsule(ctypes.Structure):
+    """Mirror of {name}_solver_capsule (include/acados_solver_{name}.h)."""
+    _fields_ = [("nlp_config", c_void_p), ("nlp_dims", c_void_p), ("nlp_in", c_void_p),
+                ("nlp_out", ctypes.POINTER(NlpOut)), ("nlp_solver", c_void_p), ("nlp_opts", c_void_p),
+                ("impl", c_void_p)]
+
+
+# every symbol the public headers declare (checked by tests/test_abi_symbols.py)
+BATCH_SYMBOLS = [
+    "nmpc_model_dims", "nmpc_model_params_default", "nmpc_model_params_set_limits", "nmpc_batch_create",
+    "nmpc_batch_destroy", "nmpc_batch_set_params", "nmpc_batch_get_params", "nmpc_batch_init_iterate",
+    "nmpc_batch_solve", "nmpc_batch_run", "nmpc_batch_state", "nmpc_fleet_sim_step", "nmpc_last_error",
+    "nmpc_version",
+]
+NLP_SYMBOLS = ["ocp_nlp_constraints_model_set", "ocp_nlp_cost_model_set", "ocp_nlp_out_get", "ocp_nlp_out_set",
+               "ocp_nlp_get", "ocp_nlp_dims_get_from_attr"]
+CAPSULE_SUFFIXES = ["create_capsule", "free_capsule", "create", "create_with_discretization", "reset",
+                    "update_params", "solve", "batch_solve", "free", "print_stats", "get_nlp_in", "get_nlp_out",
+                    "get_nlp_solver", "get_nlp_config", "get_nlp_opts", "get_nlp_dims"]
+
+
+def capsule_symbols():
+    return [f"{n}_acados_{s}" for n in MODEL_NAMES.values() for s in CAPSULE_SUFFIXES]
+
+
+_lib = None
+
+
+def lib():
+    """Load libnmpc_amd.so (raises if it was not built: run __graft_entry__.build())."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"libnmpc_amd.so not found at {LIB_PATH}: build it with "
+                           "`python -c 'import __graft_entry__ as g; g.build()'` (no CPU fallback exists)")
+    L = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+    P = ctypes.POINTER(ModelParams)
+    i, vp = ctypes.c_int, c_void_p
+    L.nmpc_model_dims.argtypes = [i] + [c_int_p] * 6
+    L.nmpc_model_params_default.argtypes = [i, i, P]
+    L.nmpc_model_params_set_limits.argtypes = [P] + [ctypes.c_double] * 5
+    L.nmpc_batch_create.argtypes = [P, i, ctypes.POINTER(vp)]
+    L.nmpc_batch_destroy.argtypes = [vp]
+    L.nmpc_batch_set_params.argtypes = [vp, P]
+    L.nmpc_batch_get_params.argtypes = [vp, P]
+    L.nmpc_batch_init_iterate.argtypes = [vp, i, i, vp]
+    L.nmpc_batch_solve.argtypes = [vp, i, vp, vp, i, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]
+    L.nmpc_batch_run.argtypes = [vp, i, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]
+    L.nmpc_batch_state.argtypes = [vp, ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.POINTER(vp), c_int_p]
+    L.nmpc_fleet_sim_step.argtypes = [vp, i, vp, vp, vp, vp, vp, vp, vp, vp, vp, i, vp]
+    L.nmpc_last_error.restype = ctypes.c_char_p
+    L.nmpc_version.restype = ctypes.c_char_p
+    for name in MODEL_NAMES.values():
+        cp = ctypes.POINTER(SolverCapsule)
+        getattr(L, f"{name}_acados_create_capsule").restype = cp
+        getattr(L, f"{name}_acados_free_capsule").argtypes = [cp]
+        getattr(L, f"{name}_acados_create").argtypes = [cp]
+        getattr(L, f"{name}_acados_create_with_discretization").argtypes = [cp, i, c_double_p]
+        getattr(L, f"{name}_acados_reset").argtypes = [cp, i]
+        getattr(L, f"{name}_acados_update_params").argtypes = [cp, i, c_double_p, i]
+        getattr(L, f"{name}_acados_solve").argtypes = [cp]
+        getattr(L, f"{name}_acados_batch_solve").argtypes = [ctypes.POINTER(cp), c_int_p, i]
+        getattr(L, f"{name}_acados_free").argtypes = [cp]
+    L.ocp_nlp_constraints_model_set.argtypes = [vp, vp, vp, vp, i, ctypes.c_char_p, vp]
+    L.ocp_nlp_cost_model_set.argtypes = [vp, vp, vp, i, ctypes.c_char_p, vp]
+    L.ocp_nlp_out_get.argtypes = [vp, vp, vp, i, ctypes.c_char_p, vp]
+    L.ocp_nlp_out_set.argtypes = [vp, vp, vp, i, ctypes.c_char_p, vp]
+    L.ocp_nlp_get.argtypes = [vp, ctypes.c_char_p, vp]
+    _lib = L
+    return L
+
+
+def check(rc, what="nmpc call"):
+    if rc != 0:
+        raise RuntimeError(f"{what} failed ({rc}): {lib().nmpc_last_error().decode()}")
+    return rc
+
+
+def default_params(model, N):
+    prm = ModelParams()
+    check(lib().nmpc_model_params_default(MODEL_IDS[model], int(N), ctypes.byref(prm)), "params_default")
+    return prm
+
+
+def model_dims(model):
+    vals = [ctypes.c_int() for _ in range(6)]
+    check(lib().nmpc_model_dims(MODEL_IDS[model], *[ctypes.byref(v) for v in vals]), "model_dims")
+    return dict(zip(("nx", "nu", "ny", "nbx", "nbu", "np"), (v.value for v in vals)))

@@ -1,0 +1,151 @@
+"""Batched solve path on the device: a thin Python owner of an ``nmpc_batch`` handle (libnmpc_amd.so).
+
+Device memory and streams come from PyTorch (plumbing only); every array is an fp32 torch CUDA tensor in
+the instance-minor ``[field][B]`` layout of include/nmpc_amd/nmpc_batch.h. All compute runs in the HIP
+kernels of the library; there is no Python or CPU fallback.
+"""
+import ctypes
+
+import torch
+
+from ._lib import MODEL_IDS, ModelParams, check, default_params, lib, model_dims
+
+
+def _ptr(t):
+    if t is None:
+        return None
+    if not t.is_cuda:
+        raise ValueError("expected a device tensor")
+    if not t.is_contiguous():
+        raise ValueError("expected a contiguous tensor")
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def _stream(stream):
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return ctypes.c_void_p(s.cuda_stream)
+
+
+class BatchSolver:
+    """B independent OCP instances of one model, solved in lockstep on one GPU.
+
+    ``solve`` is the batched ``{name}_acados_solve`` on caller-packed x0 / yref; ``run`` is the batched
+    ``NMPCNavControl{Diff,Omni4,Tric}::run`` (pre-solve, SQP-RTI, post-solve) with the warm-start
+    iterate and carried vel-ref states resident on the device between ticks.
+    """
+
+    def __init__(self, model, N, capacity, params=None, device="cuda"):
+        self.model = model
+        self.N = int(N)
+        self.capacity = int(capacity)
+        self.device = torch.device(device)
+        self.params = params if params is not None else default_params(model, N)
+        self.params.model = MODEL_IDS[model]
+        self.params.N = self.N
+        d = model_dims(model)
+        self.nx, self.nu, self.ny, self.nbx, self.nbu = d["nx"], d["nu"], d["ny"], d["nbx"], d["nbu"]
+        self._h = ctypes.c_void_p()
+        with torch.cuda.device(self.device):
+            check(lib().nmpc_batch_create(ctypes.byref(self.params), self.capacity, ctypes.byref(self._h)),
+                  "nmpc_batch_create")
+
+    def close(self):
+        if self._h:
+            lib().nmpc_batch_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_params(self, params):
+        check(lib().nmpc_batch_set_params(self._h, ctypes.byref(params)), "nmpc_batch_set_params")
+        self.params = params
+
+    def init_iterate(self, B=None, mode=0, stream=None):
+        """mode 0: {name}_acados_create semantics; mode 1: {name}_acados_reset (zeros)."""
+        B = self.capacity if B is None else int(B)
+        check(lib().nmpc_batch_init_iterate(self._h, B, int(mode), _stream(stream)), "nmpc_batch_init_iterate")
+
+    def state(self):
+        """Views of the resident device state: xbar [(N+1)*NX][cap], ubar [N*NU][cap], carried [NBX][cap]."""
+        xb, ub, cr = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p()
+        stride = ctypes.c_int()
+        check(lib().nmpc_batch_state(self._h, ctypes.byref(xb), ctypes.byref(ub), ctypes.byref(cr),
+                                     ctypes.byref(stride)), "nmpc_batch_state")
+        S = stride.value
+        return (_DeviceView(xb.value, ((self.N + 1) * self.nx, S), self.device),
+                _DeviceView(ub.value, (self.N * self.nu, S), self.device),
+                _DeviceView(cr.value, (self.nbx, S), self.device))
+
+    def empty(self, *shape, dtype=torch.float32):
+        return torch.empty(*shape, dtype=dtype, device=self.device)
+
+    def solve(self, x0, yref, We=None, reset=None, u0=None, x1=None, xtraj=None, utraj=None, status=None,
+              qp_iter=None, qp_res=None, stream=None):
+        B = x0.shape[1]
+        ny_in = yref.shape[1]
+        assert x0.shape == (self.nx, B) and yref.shape == (self.N + 1, ny_in, B)
+        if We is not None:
+            assert We.shape == (self.nx, B)
+        check(lib().nmpc_batch_solve(self._h, B, _ptr(x0), _ptr(yref), ny_in, _ptr(We), _ptr(reset), _ptr(u0),
+                                     _ptr(x1), _ptr(xtraj), _ptr(utraj), _ptr(status), _ptr(qp_iter),
+                                     _ptr(qp_res), _stream(stream)), "nmpc_batch_solve")
+
+    def run(self, pose, vel, traj, steer=None, traj_len=None, reset=None, cmd=None, u0=None, status=None,
+            qp_iter=None, qp_res=None, stream=None):
+        B = pose.shape[1]
+        assert pose.shape == (3, B) and vel.shape == (3, B) and traj.shape == (self.N + 1, 3, B)
+        check(lib().nmpc_batch_run(self._h, B, _ptr(pose), _ptr(vel), _ptr(steer), _ptr(traj), _ptr(traj_len),
+                                   _ptr(reset), _ptr(cmd), _ptr(u0), _ptr(status), _ptr(qp_iter),
+                                   _ptr(qp_res), _stream(stream)), "nmpc_batch_run")
+
+    def fleet_sim_step(self, path, s, pose, vel, steer, u0, status, traj, traj_len, advance=True, stream=None):
+        B = pose.shape[1]
+        check(lib().nmpc_fleet_sim_step(self._h, B, _ptr(path), _ptr(s), _ptr(pose), _ptr(vel), _ptr(steer),
+                                        _ptr(u0), _ptr(status), _ptr(traj), _ptr(traj_len), int(bool(advance)),
+                                        _stream(stream)), "nmpc_fleet_sim_step")
+
+
+class _DeviceView:
+    """Copy helpers for device memory owned by the library (no torch tensor aliases it)."""
+
+    def __init__(self, addr, shape, device):
+        self.addr, self.shape, self.device = addr, shape, device
+
+    def to_tensor(self):
+        rows, S = self.shape
+        out = torch.empty(rows, S, dtype=torch.float32, device=self.device)
+        _memcpy(out.data_ptr(), self.addr, rows * S * 4)
+        return out
+
+    def copy_from(self, t):
+        rows, S = self.shape
+        t = t.to(device=self.device, dtype=torch.float32).contiguous()
+        assert t.numel() == rows * S
+        _memcpy(self.addr, t.data_ptr(), rows * S * 4)
+
+
+def _memcpy(dst, src, nbytes):
+    torch.cuda.synchronize()
+    hip = _hip()
+    rc = hip.hipMemcpy(ctypes.c_void_p(dst), ctypes.c_void_p(src), ctypes.c_size_t(nbytes), 3)  # DeviceToDevice
+    if rc != 0:
+        raise RuntimeError(f"hipMemcpy failed ({rc})")
+
+
+_hip_lib = None
+
+
+def _hip():
+    global _hip_lib
+    if _hip_lib is None:
+        lib()  # libnmpc_amd pulls in libamdhip64
+        _hip_lib = ctypes.CDLL("libamdhip64.so", mode=ctypes.RTLD_GLOBAL)
+        _hip_lib.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    return _hip_lib
+
+
+__all__ = ["BatchSolver", "ModelParams", "default_params"]

@@ -1,0 +1,616 @@
+// acados_shim.cpp -- the acados-generated per-model solver ABI and the generic ocp_nlp_* setters/getters
+// the reference's wrappers call, implemented on the batched MI355X solve path.
+//
+// Reference call sites (src/nmpc_nav_control/NMPCNavControlDiff.cpp; Omni4/Tric identical in shape):
+//   create_capsule/create :10-12, update_params :44-46, constraints_model_set :49-65/:96-101,
+//   cost_model_set :68-73/:121-124/:138, solve :142, nlp_out->inf_norm_res :146, ocp_nlp_get time_tot :148,
+//   ocp_nlp_out_get u/x :151/:168, reset :179, free/free_capsule :78-79.
+//
+// A capsule keeps the acados "nlp_in" data (per-stage bounds, weights, references, parameters) and the
+// warm-start iterate ("nlp_out") on the host in fp64, as the wrappers set them. solve() packs them into a
+// batch of one (batch_solve() into one batch per parameter group), runs the fp32 SQP-RTI kernel and
+// copies the new iterate back. Device engines are shared per (model, N) and grow on demand.
+#include <hip/hip_runtime.h>
+
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "acados_solver_diff2amr.h"
+#include "acados_solver_omni4amr.h"
+#include "acados_solver_tric3amr.h"
+#include "nmpc_amd/nmpc_batch.h"
+
+struct nmpc_capsule_impl {
+    int model = 0, N = 0;
+    int nx = 0, nu = 0, ny = 0, nbx = 0, nbu = 0, np = 0;
+    bool created = false;
+    nmpc_model_params prm;           // codegen defaults + QP options
+    std::vector<double> W;           // (N+1) * NY*NY col-major (stage N uses the leading NX*NX)
+    std::vector<double> yref;        // (N+1) * NY (stage N uses NX)
+    std::vector<double> lbx, ubx;    // (N+1) * NX: stage 0 all NX (x0 equality), stages 1..N the NBX first
+    std::vector<double> lbu, ubu;    // N * NBU
+    std::vector<double> p;           // (N+1) * NP
+    std::vector<double> xbar, ubar;  // iterate (N+1)*NX, N*NU
+    double time_tot = 0.0, time_lin = 0.0, time_qp = 0.0;
+    int status = 5, qp_iter = 0, sqp_iter = 0;  // ACADOS_READY before the first solve
+    ocp_nlp_config config;
+    ocp_nlp_dims dims;
+    ocp_nlp_in in;
+    ocp_nlp_out out;
+    ocp_nlp_solver solver;
+};
+
+namespace {
+
+std::mutex g_mu;
+
+// Device engine per (model, N): one batch handle plus staging buffers.
+struct Engine {
+    nmpc_batch* batch = nullptr;
+    int cap = 0;
+    float *x0 = nullptr, *yref = nullptr, *We = nullptr, *xtraj = nullptr, *utraj = nullptr;
+    int *status = nullptr, *qp_iter = nullptr;
+    ~Engine() { release(); }
+    void release()
+    {
+        nmpc_batch_destroy(batch);
+        batch = nullptr;
+        (void)hipFree(x0); (void)hipFree(yref); (void)hipFree(We); (void)hipFree(xtraj); (void)hipFree(utraj);
+        (void)hipFree(status); (void)hipFree(qp_iter);
+        x0 = yref = We = xtraj = utraj = nullptr;
+        status = qp_iter = nullptr;
+        cap = 0;
+    }
+};
+std::map<std::pair<int, int>, std::unique_ptr<Engine>> g_engines;
+
+void log_err(const char* what, const std::string& msg) { std::fprintf(stderr, "[nmpc_amd] %s: %s\n", what, msg.c_str()); }
+
+int model_default_N(int model)
+{
+    static const char* env[3] = {"NMPC_AMD_DIFF2AMR_N", "NMPC_AMD_OMNI4AMR_N", "NMPC_AMD_TRIC3AMR_N"};
+    if (const char* e = std::getenv(env[model])) {
+        const int n = std::atoi(e);
+        if (n > 0) return n;
+    }
+    return 80;  // tf_ini 2.0 s at freq 40 Hz (config/nmpc_nav_control_acados_models.yaml:3-4,27-28,51-52)
+}
+
+void stage_W_diag(nmpc_capsule_impl* c, int k, const double* d, int n)
+{
+    double* W = c->W.data() + (size_t)k * c->ny * c->ny;
+    std::fill(W, W + c->ny * c->ny, 0.0);
+    for (int i = 0; i < n; i++) W[i + n * i] = d[i];
+}
+
+// Values baked into the acados-generated code by the shipped codegen yaml
+// (config/nmpc_nav_control_acados_models.yaml) and scripts/*/generate_c_code.py; the wrappers overwrite
+// p, bounds and W at construction time (e.g. NMPCNavControlDiff.cpp:16-73).
+void codegen_defaults(nmpc_capsule_impl* c)
+{
+    nmpc_model_params_default(c->model, c->N, &c->prm);
+    c->prm.terminal_hack = 0;  // the wrappers apply it themselves through cost_model_set(N, "W")
+    const double deg = M_PI / 180.0;
+    double Q[11] = {0}, R[4] = {0}, QN[11] = {0};
+    if (c->model == NMPC_MODEL_DIFF2AMR) {
+        c->prm.p[0] = 0.270; c->prm.p[1] = 0.1;                     // yaml:30-31
+        nmpc_model_params_set_limits(&c->prm, 1.0, 2.0, 0, 0, 0);  // yaml:33-34
+        const double q[7] = {10, 10, 5, 0, 0, 0, 0}, qn[7] = {1000, 1000, 500, 0, 0, 0, 0};  // yaml:37-47
+        std::memcpy(Q, q, sizeof(q));
+        std::memcpy(QN, qn, sizeof(qn));
+        R[0] = R[1] = 1.0;
+    } else if (c->model == NMPC_MODEL_OMNI4AMR) {
+        c->prm.p[0] = 0.535; c->prm.p[1] = 0.1;                     // yaml:6-7
+        nmpc_model_params_set_limits(&c->prm, 1.0, 1.0, 0, 0, 0);  // yaml:9-10
+        const double q[11] = {10, 10, 10, 0, 0, 0, 0, 0, 0, 0, 0};  // yaml:13-23
+        std::memcpy(Q, q, sizeof(q));
+        std::memcpy(QN, q, sizeof(q));
+        R[0] = R[1] = R[2] = R[3] = 1.0;
+    } else {
+        c->prm.p[0] = 0.270; c->prm.p[1] = 0.1; c->prm.p[2] = 0.5;                               // yaml:54-56
+        nmpc_model_params_set_limits(&c->prm, 1.0, 1.0, -30.0 * deg, 30.0 * deg, 120.0 * deg);  // yaml:58-62
+        const double q[7] = {10, 10, 5, 0, 0, 0, 0}, qn[7] = {1000, 1000, 500, 0, 0, 0, 0};     // yaml:65-75
+        std::memcpy(Q, q, sizeof(q));
+        std::memcpy(QN, qn, sizeof(qn));
+        R[0] = R[1] = 1.0;
+    }
+    const int N = c->N, nx = c->nx, nu = c->nu, ny = c->ny;
+    c->W.assign((size_t)(N + 1) * ny * ny, 0.0);
+    double wd[15];
+    for (int i = 0; i < nx; i++) wd[i] = Q[i];
+    for (int i = 0; i < nu; i++) wd[nx + i] = R[i];
+    for (int k = 0; k < N; k++) stage_W_diag(c, k, wd, ny);
+    stage_W_diag(c, N, QN, nx);
+    c->yref.assign((size_t)(N + 1) * ny, 0.0);
+    c->lbx.assign((size_t)(N + 1) * nx, 0.0);
+    c->ubx.assign((size_t)(N + 1) * nx, 0.0);
+    // ocp.constraints.x0 = [0, 0, pi, 0, ...] (generate_c_code.py:58-60)
+    c->lbx[2] = c->ubx[2] = M_PI;
+    for (int k = 1; k <= N; k++)
+        for (int i = 0; i < c->nbx; i++) {
+            c->lbx[(size_t)k * nx + i] = c->prm.lbx[i];
+            c->ubx[(size_t)k * nx + i] = c->prm.ubx[i];
+        }
+    c->lbu.assign((size_t)N * c->nbu, 0.0);
+    c->ubu.assign((size_t)N * c->nbu, 0.0);
+    for (int k = 0; k < N; k++)
+        for (int i = 0; i < c->nbu; i++) {
+            c->lbu[(size_t)k * c->nbu + i] = c->prm.lbu[i];
+            c->ubu[(size_t)k * c->nbu + i] = c->prm.ubu[i];
+        }
+    c->p.assign((size_t)(N + 1) * c->np, 0.0);
+    for (int k = 0; k <= N; k++)
+        for (int i = 0; i < c->np; i++) c->p[(size_t)k * c->np + i] = c->prm.p[i];
+    // iterate after create: x = x0 of the codegen, u = 0
+    c->xbar.assign((size_t)(N + 1) * nx, 0.0);
+    c->ubar.assign((size_t)N * nu, 0.0);
+    for (int k = 0; k <= N; k++) c->xbar[(size_t)k * nx + 2] = M_PI;
+}
+
+nmpc_capsule_impl* new_impl(int model)
+{
+    nmpc_capsule_impl* c = new nmpc_capsule_impl();
+    c->model = model;
+    nmpc_model_dims(model, &c->nx, &c->nu, &c->ny, &c->nbx, &c->nbu, &c->np);
+    c->config.impl = c;
+    c->dims.impl = c;
+    c->in.impl = c;
+    c->out.impl = c;
+    c->out.inf_norm_res = 0.0;
+    c->out.total_cost = 0.0;
+    c->out.sqp_iter = 0;
+    c->solver.impl = c;
+    return c;
+}
+
+int impl_create(nmpc_capsule_impl* c, int N)
+{
+    if (N < 1) return 1;
+    c->N = N;
+    codegen_defaults(c);
+    c->dims.N = N;
+    c->dims.nx = c->nx;
+    c->dims.nu = c->nu;
+    c->dims.ny = c->ny;
+    c->dims.nyn = c->nx;
+    c->dims.nbx = c->nbx;
+    c->dims.nbu = c->nbu;
+    c->dims.np = c->np;
+    c->created = true;
+    c->status = 5;
+    return 0;
+}
+
+// Per-capsule packed solve input; returns false (with a message) if the capsule uses a feature the
+// batched kernel does not implement.
+struct Packed {
+    nmpc_model_params prm;
+    std::vector<double> x0, yref, We;
+};
+
+bool pack(const nmpc_capsule_impl* c, Packed& o, std::string& why)
+{
+    const int N = c->N, nx = c->nx, nu = c->nu, ny = c->ny;
+    o.prm = c->prm;
+    o.x0.resize(nx);
+    for (int i = 0; i < nx; i++) {
+        if (c->lbx[i] != c->ubx[i]) { why = "stage-0 lbx != ubx (x0 must be an equality)"; return false; }
+        o.x0[i] = c->lbx[i];
+    }
+    // stage weights: diagonal, identical on stages 0..N-1
+    const double* W0 = c->W.data();
+    for (int k = 0; k < N; k++) {
+        const double* Wk = c->W.data() + (size_t)k * ny * ny;
+        for (int j = 0; j < ny; j++)
+            for (int i = 0; i < ny; i++) {
+                if (i != j && Wk[i + ny * j] != 0.0) { why = "non-diagonal W"; return false; }
+                if (Wk[i + ny * j] != W0[i + ny * j]) { why = "stage-varying W"; return false; }
+            }
+    }
+    for (int i = 0; i < ny; i++) o.prm.W[i] = W0[i + ny * i];
+    const double* WN = c->W.data() + (size_t)N * ny * ny;
+    o.We.resize(nx);
+    for (int j = 0; j < nx; j++)
+        for (int i = 0; i < nx; i++) {
+            if (i != j && WN[i + nx * j] != 0.0) { why = "non-diagonal W_e"; return false; }
+            if (i == j) o.We[i] = WN[i + nx * i];
+        }
+    for (int i = 0; i < c->nbx; i++) {
+        o.prm.lbx[i] = c->lbx[(size_t)nx + i];
+        o.prm.ubx[i] = c->ubx[(size_t)nx + i];
+        for (int k = 2; k <= N; k++)
+            if (c->lbx[(size_t)k * nx + i] != o.prm.lbx[i] || c->ubx[(size_t)k * nx + i] != o.prm.ubx[i]) {
+                why = "stage-varying state bounds";
+                return false;
+            }
+    }
+    for (int i = 0; i < c->nbu; i++) {
+        o.prm.lbu[i] = c->lbu[i];
+        o.prm.ubu[i] = c->ubu[i];
+        for (int k = 1; k < N; k++)
+            if (c->lbu[(size_t)k * c->nbu + i] != o.prm.lbu[i] || c->ubu[(size_t)k * c->nbu + i] != o.prm.ubu[i]) {
+                why = "stage-varying input bounds";
+                return false;
+            }
+    }
+    for (int i = 0; i < c->np; i++) {
+        o.prm.p[i] = c->p[i];
+        for (int k = 1; k < N; k++)
+            if (c->p[(size_t)k * c->np + i] != o.prm.p[i]) { why = "stage-varying parameters"; return false; }
+    }
+    o.yref.assign(c->yref.begin(), c->yref.end());
+    (void)nu;
+    return true;
+}
+
+bool same_params(const nmpc_model_params& a, const nmpc_model_params& b)
+{
+    return std::memcmp(&a, &b, sizeof(a)) == 0;
+}
+
+int ensure_engine(Engine& e, const nmpc_model_params& prm, int n, std::string& why)
+{
+    if (e.batch && e.cap >= n) {
+        if (nmpc_batch_set_params(e.batch, &prm) != NMPC_OK) { why = nmpc_last_error(); return -1; }
+        return 0;
+    }
+    e.release();
+    int cap = 1;
+    while (cap < n) cap *= 2;
+    int nx, nu, ny;
+    nmpc_model_dims(prm.model, &nx, &nu, &ny, nullptr, nullptr, nullptr);
+    const int N = prm.N;
+    if (nmpc_batch_create(&prm, cap, &e.batch) != NMPC_OK) { why = nmpc_last_error(); return -1; }
+    hipError_t r = hipSuccess;
+    if ((r = hipMalloc(&e.x0, sizeof(float) * nx * cap)) != hipSuccess ||
+        (r = hipMalloc(&e.yref, sizeof(float) * (N + 1) * ny * cap)) != hipSuccess ||
+        (r = hipMalloc(&e.We, sizeof(float) * nx * cap)) != hipSuccess ||
+        (r = hipMalloc(&e.xtraj, sizeof(float) * (N + 1) * nx * cap)) != hipSuccess ||
+        (r = hipMalloc(&e.utraj, sizeof(float) * N * nu * cap)) != hipSuccess ||
+        (r = hipMalloc(&e.status, sizeof(int) * cap)) != hipSuccess ||
+        (r = hipMalloc(&e.qp_iter, sizeof(int) * cap)) != hipSuccess) {
+        why = hipGetErrorString(r);
+        e.release();
+        return -1;
+    }
+    e.cap = cap;
+    return 0;
+}
+
+// Solve one group of capsules that share all uniform parameters.
+void solve_group(std::vector<nmpc_capsule_impl*>& cs, std::vector<Packed>& ps, const std::vector<int>& idx)
+{
+    const auto t0 = std::chrono::steady_clock::now();
+    nmpc_capsule_impl* c0 = cs[idx[0]];
+    const int n = (int)idx.size(), N = c0->N, nx = c0->nx, nu = c0->nu, ny = c0->ny;
+    auto& slot = g_engines[{c0->model, N}];
+    if (!slot) slot.reset(new Engine());
+    Engine& e = *slot;
+    std::string why;
+    auto fail_all = [&](const std::string& msg) {
+        log_err("solve", msg);
+        for (int i : idx) cs[i]->status = 4;
+    };
+    if (ensure_engine(e, ps[idx[0]].prm, n, why)) return fail_all(why);
+    const int S = e.cap;
+    std::vector<float> hx0((size_t)nx * n), hyref((size_t)(N + 1) * ny * n), hWe((size_t)nx * n);
+    std::vector<float> hxb((size_t)(N + 1) * nx * n), hub((size_t)N * nu * n);
+    for (int q = 0; q < n; q++) {
+        const Packed& P = ps[idx[q]];
+        const nmpc_capsule_impl* c = cs[idx[q]];
+        for (int i = 0; i < nx; i++) {
+            hx0[(size_t)i * n + q] = (float)P.x0[i];
+            hWe[(size_t)i * n + q] = (float)P.We[i];
+        }
+        for (int k = 0; k <= N; k++)
+            for (int j = 0; j < ny; j++) hyref[((size_t)k * ny + j) * n + q] = (float)P.yref[(size_t)k * ny + j];
+        for (size_t r = 0; r < (size_t)(N + 1) * nx; r++) hxb[r * n + q] = (float)c->xbar[r];
+        for (size_t r = 0; r < (size_t)N * nu; r++) hub[r * n + q] = (float)c->ubar[r];
+    }
+    float *dxb, *dub;
+    nmpc_batch_state(e.batch, &dxb, &dub, nullptr, nullptr);
+    hipError_t r = hipSuccess;
+    if ((r = hipMemcpy(e.x0, hx0.data(), sizeof(float) * hx0.size(), hipMemcpyHostToDevice)) != hipSuccess ||
+        (r = hipMemcpy(e.yref, hyref.data(), sizeof(float) * hyref.size(), hipMemcpyHostToDevice)) != hipSuccess ||
+        (r = hipMemcpy(e.We, hWe.data(), sizeof(float) * hWe.size(), hipMemcpyHostToDevice)) != hipSuccess ||
+        (r = hipMemcpy2D(dxb, sizeof(float) * S, hxb.data(), sizeof(float) * n, sizeof(float) * n, (size_t)(N + 1) * nx,
+                         hipMemcpyHostToDevice)) != hipSuccess ||
+        (r = hipMemcpy2D(dub, sizeof(float) * S, hub.data(), sizeof(float) * n, sizeof(float) * n, (size_t)N * nu,
+                         hipMemcpyHostToDevice)) != hipSuccess)
+        return fail_all(hipGetErrorString(r));
+    const auto t1 = std::chrono::steady_clock::now();
+    if (nmpc_batch_solve(e.batch, n, e.x0, e.yref, ny, e.We, nullptr, nullptr, nullptr, e.xtraj, e.utraj, e.status,
+                         e.qp_iter, nullptr, nullptr) != NMPC_OK)
+        return fail_all(nmpc_last_error());
+    std::vector<int> hst(n), hit(n);
+    if ((r = hipMemcpy(hxb.data(), e.xtraj, sizeof(float) * hxb.size(), hipMemcpyDeviceToHost)) != hipSuccess ||
+        (r = hipMemcpy(hub.data(), e.utraj, sizeof(float) * hub.size(), hipMemcpyDeviceToHost)) != hipSuccess ||
+        (r = hipMemcpy(hst.data(), e.status, sizeof(int) * n, hipMemcpyDeviceToHost)) != hipSuccess ||
+        (r = hipMemcpy(hit.data(), e.qp_iter, sizeof(int) * n, hipMemcpyDeviceToHost)) != hipSuccess)
+        return fail_all(hipGetErrorString(r));
+    const auto t2 = std::chrono::steady_clock::now();
+    const double tt = std::chrono::duration<double>(t2 - t0).count();
+    const double tq = std::chrono::duration<double>(t2 - t1).count();
+    for (int q = 0; q < n; q++) {
+        nmpc_capsule_impl* c = cs[idx[q]];
+        c->status = hst[q];
+        c->qp_iter = hit[q];
+        c->sqp_iter = 1;
+        c->out.sqp_iter = 1;
+        c->time_tot = tt;
+        c->time_qp = tq;
+        c->time_lin = 0.0;
+        if (hst[q] == 0) {
+            for (size_t rr = 0; rr < (size_t)(N + 1) * nx; rr++) c->xbar[rr] = hxb[rr * n + q];
+            for (size_t rr = 0; rr < (size_t)N * nu; rr++) c->ubar[rr] = hub[rr * n + q];
+        }
+    }
+}
+
+int batch_solve_impl(std::vector<nmpc_capsule_impl*>& cs, int* status_out)
+{
+    std::lock_guard<std::mutex> lock(g_mu);
+    const int n = (int)cs.size();
+    std::vector<Packed> ps(n);
+    std::vector<bool> done(n, false);
+    for (int i = 0; i < n; i++) {
+        std::string why;
+        if (!cs[i] || !cs[i]->created) {
+            if (cs[i]) cs[i]->status = 4;
+            log_err("solve", "capsule not created");
+            done[i] = true;
+            continue;
+        }
+        if (!pack(cs[i], ps[i], why)) {
+            log_err("solve", "unsupported OCP data: " + why);
+            cs[i]->status = 4;
+            done[i] = true;
+        }
+    }
+    // group by (N, uniform parameters)
+    for (int i = 0; i < n; i++) {
+        if (done[i]) continue;
+        std::vector<int> idx;
+        for (int j = i; j < n; j++)
+            if (!done[j] && cs[j]->N == cs[i]->N && same_params(ps[j].prm, ps[i].prm)) {
+                idx.push_back(j);
+                done[j] = true;
+            }
+        solve_group(cs, ps, idx);
+    }
+    int nfail = 0;
+    for (int i = 0; i < n; i++) {
+        const int s = cs[i] ? cs[i]->status : 4;
+        if (status_out) status_out[i] = s;
+        if (s != 0) nfail++;
+    }
+    return nfail;
+}
+
+nmpc_capsule_impl* impl_of(void* p) { return p ? static_cast<nmpc_capsule_impl*>(p) : nullptr; }
+
+}  // namespace
+
+// ------------------------------------------------------------------------------------------------------
+// Generic acados C interface subset
+// ------------------------------------------------------------------------------------------------------
+extern "C" {
+
+int ocp_nlp_constraints_model_set(ocp_nlp_config* config, ocp_nlp_dims* dims, ocp_nlp_in* in, ocp_nlp_out* out,
+                                  int stage, const char* field, void* value)
+{
+    (void)config; (void)dims; (void)out;
+    nmpc_capsule_impl* c = in ? impl_of(in->impl) : nullptr;
+    if (!c || !c->created || !field || !value) return -1;
+    if (stage < 0 || stage > c->N) return -1;
+    const double* v = static_cast<const double*>(value);
+    const int nx = c->nx;
+    if (!std::strcmp(field, "lbx") || !std::strcmp(field, "ubx")) {
+        std::vector<double>& dst = (field[0] == 'l') ? c->lbx : c->ubx;
+        const int n = (stage == 0) ? nx : c->nbx;  // nbx0 = NX (x0), nbx = NBX on idxbx
+        for (int i = 0; i < n; i++) dst[(size_t)stage * nx + i] = v[i];
+        return 0;
+    }
+    if (!std::strcmp(field, "lbu") || !std::strcmp(field, "ubu")) {
+        if (stage >= c->N) return -1;
+        std::vector<double>& dst = (field[0] == 'l') ? c->lbu : c->ubu;
+        for (int i = 0; i < c->nbu; i++) dst[(size_t)stage * c->nbu + i] = v[i];
+        return 0;
+    }
+    log_err("ocp_nlp_constraints_model_set", std::string("unsupported field ") + field);
+    return -1;
+}
+
+int ocp_nlp_cost_model_set(ocp_nlp_config* config, ocp_nlp_dims* dims, ocp_nlp_in* in, int stage,
+                           const char* field, void* value)
+{
+    (void)config; (void)dims;
+    nmpc_capsule_impl* c = in ? impl_of(in->impl) : nullptr;
+    if (!c || !c->created || !field || !value) return -1;
+    if (stage < 0 || stage > c->N) return -1;
+    const double* v = static_cast<const double*>(value);
+    const int n = (stage == c->N) ? c->nx : c->ny;
+    if (!std::strcmp(field, "W")) {
+        double* W = c->W.data() + (size_t)stage * c->ny * c->ny;
+        std::fill(W, W + c->ny * c->ny, 0.0);
+        for (int i = 0; i < n * n; i++) W[i] = v[i];  // col-major n x n
+        return 0;
+    }
+    if (!std::strcmp(field, "yref")) {
+        for (int i = 0; i < n; i++) c->yref[(size_t)stage * c->ny + i] = v[i];
+        return 0;
+    }
+    log_err("ocp_nlp_cost_model_set", std::string("unsupported field ") + field);
+    return -1;
+}
+
+void ocp_nlp_out_get(ocp_nlp_config* config, ocp_nlp_dims* dims, ocp_nlp_out* out, int stage, const char* field,
+                     void* value)
+{
+    (void)config; (void)dims;
+    nmpc_capsule_impl* c = out ? impl_of(out->impl) : nullptr;
+    if (!c || !c->created || !field || !value || stage < 0 || stage > c->N) return;
+    double* v = static_cast<double*>(value);
+    if (!std::strcmp(field, "x")) {
+        for (int i = 0; i < c->nx; i++) v[i] = c->xbar[(size_t)stage * c->nx + i];
+    } else if (!std::strcmp(field, "u") && stage < c->N) {
+        for (int i = 0; i < c->nu; i++) v[i] = c->ubar[(size_t)stage * c->nu + i];
+    } else {
+        log_err("ocp_nlp_out_get", std::string("unsupported field ") + field);
+    }
+}
+
+void ocp_nlp_out_set(ocp_nlp_config* config, ocp_nlp_dims* dims, ocp_nlp_out* out, int stage, const char* field,
+                     void* value)
+{
+    (void)config; (void)dims;
+    nmpc_capsule_impl* c = out ? impl_of(out->impl) : nullptr;
+    if (!c || !c->created || !field || !value || stage < 0 || stage > c->N) return;
+    const double* v = static_cast<const double*>(value);
+    if (!std::strcmp(field, "x")) {
+        for (int i = 0; i < c->nx; i++) c->xbar[(size_t)stage * c->nx + i] = v[i];
+    } else if (!std::strcmp(field, "u") && stage < c->N) {
+        for (int i = 0; i < c->nu; i++) c->ubar[(size_t)stage * c->nu + i] = v[i];
+    } else {
+        log_err("ocp_nlp_out_set", std::string("unsupported field ") + field);
+    }
+}
+
+void ocp_nlp_get(ocp_nlp_solver* solver, const char* field, void* return_value_)
+{
+    nmpc_capsule_impl* c = solver ? impl_of(solver->impl) : nullptr;
+    if (!c || !field || !return_value_) return;
+    if (!std::strcmp(field, "time_tot")) *static_cast<double*>(return_value_) = c->time_tot;
+    else if (!std::strcmp(field, "time_lin")) *static_cast<double*>(return_value_) = c->time_lin;
+    else if (!std::strcmp(field, "time_qp_sol") || !std::strcmp(field, "time_qp"))
+        *static_cast<double*>(return_value_) = c->time_qp;
+    else if (!std::strcmp(field, "sqp_iter")) *static_cast<int*>(return_value_) = c->sqp_iter;
+    else if (!std::strcmp(field, "qp_iter")) *static_cast<int*>(return_value_) = c->qp_iter;
+    else if (!std::strcmp(field, "status")) *static_cast<int*>(return_value_) = c->status;
+    else log_err("ocp_nlp_get", std::string("unsupported field ") + field);
+}
+
+int ocp_nlp_dims_get_from_attr(ocp_nlp_config* config, ocp_nlp_dims* dims, ocp_nlp_out* out, int stage,
+                               const char* field)
+{
+    (void)config; (void)out;
+    nmpc_capsule_impl* c = dims ? impl_of(dims->impl) : nullptr;
+    if (!c || !field) return -1;
+    if (!std::strcmp(field, "x")) return c->nx;
+    if (!std::strcmp(field, "u")) return stage < c->N ? c->nu : 0;
+    if (!std::strcmp(field, "y_ref") || !std::strcmp(field, "yref")) return stage < c->N ? c->ny : c->nx;
+    return -1;
+}
+
+}  // extern "C"
+
+// ------------------------------------------------------------------------------------------------------
+// Per-model generated-solver ABI
+// ------------------------------------------------------------------------------------------------------
+#define NMPC_DEFINE_MODEL_ABI(name, MODEL)                                                                       \
+    extern "C" name##_solver_capsule* name##_acados_create_capsule(void)                                        \
+    {                                                                                                            \
+        name##_solver_capsule* cap = new name##_solver_capsule();                                               \
+        nmpc_capsule_impl* c = new_impl(MODEL);                                                                  \
+        cap->impl = c;                                                                                           \
+        cap->nlp_config = &c->config;                                                                            \
+        cap->nlp_dims = &c->dims;                                                                                \
+        cap->nlp_in = &c->in;                                                                                    \
+        cap->nlp_out = &c->out;                                                                                  \
+        cap->nlp_solver = &c->solver;                                                                            \
+        cap->nlp_opts = nullptr;                                                                                 \
+        return cap;                                                                                              \
+    }                                                                                                            \
+    extern "C" int name##_acados_free_capsule(name##_solver_capsule* capsule)                                   \
+    {                                                                                                            \
+        if (!capsule) return 1;                                                                                  \
+        delete capsule->impl;                                                                                    \
+        delete capsule;                                                                                          \
+        return 0;                                                                                                \
+    }                                                                                                            \
+    extern "C" int name##_acados_create_with_discretization(name##_solver_capsule* capsule, int n_time_steps,    \
+                                                            double* new_time_steps)                              \
+    {                                                                                                            \
+        if (!capsule || !capsule->impl) return 1;                                                                \
+        if (new_time_steps) {                                                                                    \
+            log_err("create", "non-uniform time steps are not supported");                                      \
+            return 1;                                                                                            \
+        }                                                                                                        \
+        return impl_create(capsule->impl, n_time_steps);                                                        \
+    }                                                                                                            \
+    extern "C" int name##_acados_create(name##_solver_capsule* capsule)                                         \
+    {                                                                                                            \
+        return name##_acados_create_with_discretization(capsule, model_default_N(MODEL), nullptr);             \
+    }                                                                                                            \
+    extern "C" int name##_acados_reset(name##_solver_capsule* capsule, int reset_qp_solver_mem)                 \
+    {                                                                                                            \
+        (void)reset_qp_solver_mem; /* the IPM cold-starts every QP: no QP memory to reset */                    \
+        if (!capsule || !capsule->impl || !capsule->impl->created) return 1;                                    \
+        nmpc_capsule_impl* c = capsule->impl;                                                                    \
+        std::fill(c->xbar.begin(), c->xbar.end(), 0.0);                                                          \
+        std::fill(c->ubar.begin(), c->ubar.end(), 0.0);                                                          \
+        return 0;                                                                                                \
+    }                                                                                                            \
+    extern "C" int name##_acados_update_params(name##_solver_capsule* capsule, int stage, double* value, int np) \
+    {                                                                                                            \
+        if (!capsule || !capsule->impl || !capsule->impl->created || !value) return 1;                          \
+        nmpc_capsule_impl* c = capsule->impl;                                                                    \
+        if (np != c->np) {                                                                                       \
+            log_err("update_params", "np does not match the model");                                            \
+            return 1;                                                                                            \
+        }                                                                                                        \
+        if (stage < 0 || stage > c->N) return 1;                                                                 \
+        for (int i = 0; i < np; i++) c->p[(size_t)stage * np + i] = value[i];                                    \
+        return 0;                                                                                                \
+    }                                                                                                            \
+    extern "C" int name##_acados_solve(name##_solver_capsule* capsule)                                          \
+    {                                                                                                            \
+        if (!capsule || !capsule->impl) return 4;                                                                \
+        std::vector<nmpc_capsule_impl*> cs{capsule->impl};                                                       \
+        batch_solve_impl(cs, nullptr);                                                                           \
+        return capsule->impl->status;                                                                            \
+    }                                                                                                            \
+    extern "C" int name##_acados_batch_solve(name##_solver_capsule** capsules, int* status_out, int N_batch)    \
+    {                                                                                                            \
+        if (!capsules || N_batch < 0) return -1;                                                                 \
+        std::vector<nmpc_capsule_impl*> cs(N_batch);                                                             \
+        for (int i = 0; i < N_batch; i++) cs[i] = capsules[i] ? capsules[i]->impl : nullptr;                    \
+        return batch_solve_impl(cs, status_out);                                                                 \
+    }                                                                                                            \
+    extern "C" int name##_acados_free(name##_solver_capsule* capsule)                                           \
+    {                                                                                                            \
+        if (!capsule || !capsule->impl) return 1;                                                                \
+        capsule->impl->created = false;                                                                          \
+        return 0;                                                                                                \
+    }                                                                                                            \
+    extern "C" void name##_acados_print_stats(name##_solver_capsule* capsule)                                   \
+    {                                                                                                            \
+        if (!capsule || !capsule->impl) return;                                                                  \
+        const nmpc_capsule_impl* c = capsule->impl;                                                              \
+        std::printf("%s: status %d, sqp_iter %d, qp_iter %d, time_tot %.3f ms\n", #name, c->status, c->sqp_iter, \
+                    c->qp_iter, c->time_tot * 1e3);                                                              \
+    }                                                                                                            \
+    extern "C" ocp_nlp_in* name##_acados_get_nlp_in(name##_solver_capsule* capsule) { return capsule->nlp_in; }  \
+    extern "C" ocp_nlp_out* name##_acados_get_nlp_out(name##_solver_capsule* capsule) { return capsule->nlp_out; } \
+    extern "C" ocp_nlp_solver* name##_acados_get_nlp_solver(name##_solver_capsule* capsule)                     \
+    {                                                                                                            \
+        return capsule->nlp_solver;                                                                              \
+    }                                                                                                            \
+    extern "C" ocp_nlp_config* name##_acados_get_nlp_config(name##_solver_capsule* capsule)                     \
+    {                                                                                                            \
+        return capsule->nlp_config;                                                                              \
+    }                                                                                                            \
+    extern "C" void* name##_acados_get_nlp_opts(name##_solver_capsule* capsule) { return capsule->nlp_opts; }    \
+    extern "C" ocp_nlp_dims* name##_acados_get_nlp_dims(name##_solver_capsule* capsule) { return capsule->nlp_dims; }
+
+NMPC_DEFINE_MODEL_ABI(diff2amr, NMPC_MODEL_DIFF2AMR)
+NMPC_DEFINE_MODEL_ABI(omni4amr, NMPC_MODEL_OMNI4AMR)
+NMPC_DEFINE_MODEL_ABI(tric3amr, NMPC_MODEL_TRIC3AMR)

@@ -1,0 +1,376 @@
+// nmpc_batch.cpp -- C ABI of the batched solve path (include/nmpc_amd/nmpc_batch.h).
+#include "nmpc_amd/nmpc_batch.h"
+
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+
+#include "nmpc_kernels.hpp"
+
+using namespace nmpc;
+
+struct nmpc_batch {
+    nmpc_model_params prm;
+    KParams kp;
+    int capacity;
+    int nx, nu, nbx, nbu, ny;
+    float* xbar = nullptr;
+    float* ubar = nullptr;
+    float* carried = nullptr;
+    float* scratch = nullptr;
+};
+
+namespace {
+
+thread_local std::string g_err;
+
+int set_err(int code, const std::string& msg)
+{
+    g_err = msg;
+    return code;
+}
+
+int hip_err(hipError_t e, const char* what)
+{
+    if (e == hipSuccess) return NMPC_OK;
+    return set_err(NMPC_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+bool dims_of(int model, int* nx, int* nu, int* nbx, int* nbu, int* np)
+{
+    switch (model) {
+    case NMPC_MODEL_DIFF2AMR: *nx = 7; *nu = 2; *nbx = 2; *nbu = 2; *np = 2; return true;
+    case NMPC_MODEL_OMNI4AMR: *nx = 11; *nu = 4; *nbx = 4; *nbu = 4; *np = 2; return true;
+    case NMPC_MODEL_TRIC3AMR: *nx = 7; *nu = 2; *nbx = 2; *nbu = 2; *np = 3; return true;
+    default: return false;
+    }
+}
+
+KParams to_kparams(const nmpc_model_params& p, int nx, int nu, int nbx, int nbu)
+{
+    KParams k;
+    std::memset(&k, 0, sizeof(k));
+    k.N = p.N;
+    k.dt = (float)p.dt;
+    k.dt_ctrl = (float)p.dt_ctrl;
+    for (int i = 0; i < 3; i++) k.p[i] = (float)p.p[i];
+    for (int i = 0; i < nbx; i++) { k.lbx[i] = (float)p.lbx[i]; k.ubx[i] = (float)p.ubx[i]; }
+    for (int i = 0; i < nbu; i++) { k.lbu[i] = (float)p.lbu[i]; k.ubu[i] = (float)p.ubu[i]; }
+    for (int i = 0; i < nx + nu; i++) k.W[i] = (float)p.W[i];
+    for (int i = 0; i < nx; i++) k.We[i] = (float)p.W_e[i];
+    k.terminal_hack = p.terminal_hack;
+    k.sin_bug = p.tric_sin_bug;
+    k.iter_max = p.qp_iter_max;
+    k.tol_stat = (float)p.qp_tol_stat;
+    k.tol_ineq = (float)p.qp_tol_ineq;
+    k.tol_comp = (float)p.qp_tol_comp;
+    k.mu0 = (float)p.qp_mu0;
+    k.thr0 = (float)p.qp_thr0;
+    k.tau = (float)p.qp_tau;
+    return k;
+}
+
+size_t scratch_floats(int model, int N, int stride)
+{
+    switch (model) {
+    case NMPC_MODEL_DIFF2AMR: return lane_scratch_floats<Diff2>(N, stride);
+    case NMPC_MODEL_OMNI4AMR: return lane_scratch_floats<Omni4>(N, stride);
+    default: return lane_scratch_floats<Tric3>(N, stride);
+    }
+}
+
+hipError_t launch(nmpc_batch* b, const KArgs& a, int mode, hipStream_t s)
+{
+    switch (b->prm.model) {
+    case NMPC_MODEL_DIFF2AMR: return launch_sqp_rti_lane<Diff2>(b->kp, a, mode, s);
+    case NMPC_MODEL_OMNI4AMR: return launch_sqp_rti_lane<Omni4>(b->kp, a, mode, s);
+    default: return launch_sqp_rti_lane<Tric3>(b->kp, a, mode, s);
+    }
+}
+
+__global__ void k_init_iterate(float* xbar, float* ubar, float* carried, int B, int stride, int N, int nx, int nu,
+                               int nbx, int mode)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= B) return;
+    for (int k = 0; k <= N; k++)
+        for (int j = 0; j < nx; j++)
+            xbar[((size_t)k * nx + j) * stride + i] = (mode == 0 && j == 2) ? 3.14159265358979323846f : 0.0f;
+    for (int k = 0; k < N; k++)
+        for (int j = 0; j < nu; j++) ubar[((size_t)k * nu + j) * stride + i] = 0.0f;
+    for (int j = 0; j < nbx; j++) carried[(size_t)j * stride + i] = 0.0f;
+}
+
+int check_params(const nmpc_model_params* prm)
+{
+    int nx, nu, nbx, nbu, np;
+    if (!prm) return set_err(NMPC_ERR_ARG, "params is NULL");
+    if (!dims_of(prm->model, &nx, &nu, &nbx, &nbu, &np)) return set_err(NMPC_ERR_ARG, "unknown model id");
+    if (prm->N < 1 || prm->N > 4096) return set_err(NMPC_ERR_ARG, "horizon N out of range [1, 4096]");
+    if (!(prm->dt > 0.0) || !(prm->dt_ctrl > 0.0)) return set_err(NMPC_ERR_ARG, "dt must be positive");
+    if (prm->qp_iter_max < 1) return set_err(NMPC_ERR_ARG, "qp_iter_max must be >= 1");
+    for (int i = 0; i < nbx; i++)
+        if (!(prm->lbx[i] < prm->ubx[i])) return set_err(NMPC_ERR_ARG, "state bounds need lbx < ubx");
+    for (int i = 0; i < nbu; i++)
+        if (!(prm->lbu[i] < prm->ubu[i])) return set_err(NMPC_ERR_ARG, "input bounds need lbu < ubu");
+    for (int i = 0; i < np; i++)
+        if (!(prm->p[i] > 0.0)) return set_err(NMPC_ERR_ARG, "model parameters must be positive");
+    for (int i = 0; i < nu; i++)
+        if (!(prm->W[nx + i] > 0.0)) return set_err(NMPC_ERR_UNSUPPORTED, "input weights R must be > 0");
+    return NMPC_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* nmpc_last_error(void) { return g_err.c_str(); }
+const char* nmpc_version(void) { return "nmpc_amd 0.1 (lane-per-instance SQP-RTI, gfx950)"; }
+
+int nmpc_model_dims(int model, int* nx, int* nu, int* ny, int* nbx, int* nbu, int* np)
+{
+    int a, b, c, d, e;
+    if (!dims_of(model, &a, &b, &c, &d, &e)) return set_err(NMPC_ERR_ARG, "unknown model id");
+    if (nx) *nx = a;
+    if (nu) *nu = b;
+    if (ny) *ny = a + b;
+    if (nbx) *nbx = c;
+    if (nbu) *nbu = d;
+    if (np) *np = e;
+    return NMPC_OK;
+}
+
+int nmpc_model_params_default(int model, int N, nmpc_model_params* prm)
+{
+    int nx, nu, nbx, nbu, np;
+    if (!prm) return set_err(NMPC_ERR_ARG, "params is NULL");
+    if (!dims_of(model, &nx, &nu, &nbx, &nbu, &np)) return set_err(NMPC_ERR_ARG, "unknown model id");
+    std::memset(prm, 0, sizeof(*prm));
+    prm->model = model;
+    prm->N = N;
+    prm->dt = 1.0 / 40.0;      // config/nmpc_nav_control_acados_models.yaml:28
+    prm->dt_ctrl = 1.0 / 40.0; // config/nmpc_nav_control.yaml:4
+    const double deg = M_PI / 180.0;
+    // rob_wh_max_vel / rob_wh_max_ace 1.0 (nmpc_nav_control.yaml:20-21/31-32/44-45),
+    // steering -45..45 deg, 15 deg/s (nmpc_nav_control.yaml:46-48)
+    nmpc_model_params_set_limits(prm, 1.0, 1.0, -45.0 * deg, 45.0 * deg, 15.0 * deg);
+    if (model == NMPC_MODEL_DIFF2AMR) {
+        prm->p[0] = 0.270; prm->p[1] = 0.1;  // nmpc_nav_control.yaml:29-30
+        const double W[9] = {10, 10, 5, 0, 0, 0, 0, 1, 1};
+        std::memcpy(prm->W, W, sizeof(W));
+        prm->terminal_hack = 1;
+    } else if (model == NMPC_MODEL_OMNI4AMR) {
+        prm->p[0] = 0.265 + 0.270; prm->p[1] = 0.1;  // nmpc_nav_control.yaml:17-19, NMPCNavControlROS.cpp:97-99
+        const double W[15] = {10, 10, 5, 0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1};
+        std::memcpy(prm->W, W, sizeof(W));
+    } else {
+        prm->p[0] = 0.270; prm->p[1] = 0.1; prm->p[2] = 0.5;  // nmpc_nav_control.yaml:41-43
+        const double W[9] = {10, 10, 5, 0, 0, 0, 0, 1, 1};
+        std::memcpy(prm->W, W, sizeof(W));
+        prm->tric_sin_bug = 1;
+    }
+    for (int i = 0; i < nx; i++) prm->W_e[i] = prm->W[i];  // NMPCNavControlDiff.cpp:39-41
+    prm->qp_iter_max = 50;
+    prm->qp_tol_stat = 1e-4;
+    prm->qp_tol_ineq = 1e-5;
+    prm->qp_tol_comp = 1e-10;
+    prm->qp_mu0 = 1.0;
+    prm->qp_thr0 = 0.5;
+    prm->qp_tau = 0.995;
+    return NMPC_OK;
+}
+
+int nmpc_model_params_set_limits(nmpc_model_params* prm, double v_max, double a_max, double alpha_min,
+                                 double alpha_max, double dalpha_max)
+{
+    int nx, nu, nbx, nbu, np;
+    if (!prm) return set_err(NMPC_ERR_ARG, "params is NULL");
+    if (!dims_of(prm->model, &nx, &nu, &nbx, &nbu, &np)) return set_err(NMPC_ERR_ARG, "unknown model id");
+    for (int i = 0; i < 4; i++) prm->lbx[i] = prm->ubx[i] = prm->lbu[i] = prm->ubu[i] = 0.0;
+    for (int i = 0; i < nbx; i++) { prm->lbx[i] = -v_max; prm->ubx[i] = v_max; }
+    for (int i = 0; i < nbu; i++) { prm->lbu[i] = -a_max; prm->ubu[i] = a_max; }
+    if (prm->model == NMPC_MODEL_TRIC3AMR) {
+        prm->lbx[1] = alpha_min;
+        prm->ubx[1] = alpha_max;
+        prm->lbu[1] = -dalpha_max;
+        prm->ubu[1] = dalpha_max;
+    }
+    return NMPC_OK;
+}
+
+int nmpc_batch_create(const nmpc_model_params* prm, int capacity, nmpc_batch** out)
+{
+    if (!out) return set_err(NMPC_ERR_ARG, "out is NULL");
+    *out = nullptr;
+    int rc = check_params(prm);
+    if (rc) return rc;
+    if (capacity < 1) return set_err(NMPC_ERR_ARG, "capacity must be >= 1");
+    nmpc_batch* b = new nmpc_batch();
+    b->prm = *prm;
+    b->capacity = capacity;
+    int np;
+    dims_of(prm->model, &b->nx, &b->nu, &b->nbx, &b->nbu, &np);
+    b->ny = b->nx + b->nu;
+    b->kp = to_kparams(*prm, b->nx, b->nu, b->nbx, b->nbu);
+    const int N = prm->N;
+    const size_t S = (size_t)capacity;
+    hipError_t e;
+    if ((e = hipMalloc(&b->xbar, sizeof(float) * (N + 1) * b->nx * S)) != hipSuccess ||
+        (e = hipMalloc(&b->ubar, sizeof(float) * N * b->nu * S)) != hipSuccess ||
+        (e = hipMalloc(&b->carried, sizeof(float) * b->nbx * S)) != hipSuccess ||
+        (e = hipMalloc(&b->scratch, sizeof(float) * scratch_floats(prm->model, N, capacity))) != hipSuccess) {
+        nmpc_batch_destroy(b);
+        return hip_err(e, "hipMalloc");
+    }
+    rc = nmpc_batch_init_iterate(b, capacity, 0, nullptr);
+    if (rc == NMPC_OK) rc = hip_err(hipStreamSynchronize(nullptr), "hipStreamSynchronize");
+    if (rc) {
+        nmpc_batch_destroy(b);
+        return rc;
+    }
+    *out = b;
+    return NMPC_OK;
+}
+
+int nmpc_batch_destroy(nmpc_batch* b)
+{
+    if (!b) return NMPC_OK;
+    (void)hipFree(b->xbar);
+    (void)hipFree(b->ubar);
+    (void)hipFree(b->carried);
+    (void)hipFree(b->scratch);
+    delete b;
+    return NMPC_OK;
+}
+
+int nmpc_batch_set_params(nmpc_batch* b, const nmpc_model_params* prm)
+{
+    if (!b) return set_err(NMPC_ERR_ARG, "batch is NULL");
+    int rc = check_params(prm);
+    if (rc) return rc;
+    if (prm->model != b->prm.model || prm->N != b->prm.N)
+        return set_err(NMPC_ERR_ARG, "set_params cannot change model or horizon");
+    b->prm = *prm;
+    b->kp = to_kparams(*prm, b->nx, b->nu, b->nbx, b->nbu);
+    return NMPC_OK;
+}
+
+int nmpc_batch_get_params(const nmpc_batch* b, nmpc_model_params* prm)
+{
+    if (!b || !prm) return set_err(NMPC_ERR_ARG, "NULL argument");
+    *prm = b->prm;
+    return NMPC_OK;
+}
+
+int nmpc_batch_init_iterate(nmpc_batch* b, int B, int mode, void* stream)
+{
+    if (!b) return set_err(NMPC_ERR_ARG, "batch is NULL");
+    if (B < 0 || B > b->capacity) return set_err(NMPC_ERR_ARG, "B out of range [0, capacity]");
+    if (mode != 0 && mode != 1) return set_err(NMPC_ERR_ARG, "mode must be 0 (create) or 1 (reset)");
+    if (B == 0) return NMPC_OK;
+    hipLaunchKernelGGL(k_init_iterate, dim3((B + 255) / 256), dim3(256), 0, (hipStream_t)stream, b->xbar, b->ubar,
+                       b->carried, B, b->capacity, b->prm.N, b->nx, b->nu, b->nbx, mode);
+    return hip_err(hipGetLastError(), "init_iterate launch");
+}
+
+int nmpc_batch_solve(nmpc_batch* b, int B, const float* x0, const float* yref, int ny_in, const float* We,
+                     const unsigned char* reset, float* u0, float* x1, float* xtraj, float* utraj, int* status,
+                     int* qp_iter, float* qp_res, void* stream)
+{
+    if (!b) return set_err(NMPC_ERR_ARG, "batch is NULL");
+    if (B < 0 || B > b->capacity) return set_err(NMPC_ERR_ARG, "B out of range [0, capacity]");
+    if (B == 0) return NMPC_OK;
+    if (!x0 || !yref) return set_err(NMPC_ERR_ARG, "x0 and yref are required");
+    if (ny_in < 1 || ny_in > b->ny) return set_err(NMPC_ERR_ARG, "ny_in out of range [1, NY]");
+    KArgs a;
+    std::memset(&a, 0, sizeof(a));
+    a.B = B;
+    a.stride = b->capacity;
+    a.xbar = b->xbar;
+    a.ubar = b->ubar;
+    a.carried = b->carried;
+    a.scratch = b->scratch;
+    a.x0 = x0;
+    a.yref = yref;
+    a.ny_in = ny_in;
+    a.We = We;
+    a.reset = reset;
+    a.u0 = u0;
+    a.x1 = x1;
+    a.xtraj = xtraj;
+    a.utraj = utraj;
+    a.status = status;
+    a.qp_iter = qp_iter;
+    a.qp_res = qp_res;
+    return hip_err(launch(b, a, kModeSolve, (hipStream_t)stream), "solve launch");
+}
+
+int nmpc_batch_run(nmpc_batch* b, int B, const float* pose, const float* vel, const float* steer,
+                   const float* traj, const int* traj_len, const unsigned char* reset, float* cmd, float* u0,
+                   int* status, int* qp_iter, float* qp_res, void* stream)
+{
+    if (!b) return set_err(NMPC_ERR_ARG, "batch is NULL");
+    if (B < 0 || B > b->capacity) return set_err(NMPC_ERR_ARG, "B out of range [0, capacity]");
+    if (B == 0) return NMPC_OK;
+    if (!pose || !vel || !traj) return set_err(NMPC_ERR_ARG, "pose, vel and traj are required");
+    KArgs a;
+    std::memset(&a, 0, sizeof(a));
+    a.B = B;
+    a.stride = b->capacity;
+    a.xbar = b->xbar;
+    a.ubar = b->ubar;
+    a.carried = b->carried;
+    a.scratch = b->scratch;
+    a.pose = pose;
+    a.vel = vel;
+    a.steer = steer;
+    a.traj = traj;
+    a.traj_len = traj_len;
+    a.reset = reset;
+    a.cmd = cmd;
+    a.u0 = u0;
+    a.status = status;
+    a.qp_iter = qp_iter;
+    a.qp_res = qp_res;
+    return hip_err(launch(b, a, kModeRun, (hipStream_t)stream), "run launch");
+}
+
+int nmpc_batch_state(nmpc_batch* b, float** xbar, float** ubar, float** carried, int* stride)
+{
+    if (!b) return set_err(NMPC_ERR_ARG, "batch is NULL");
+    if (xbar) *xbar = b->xbar;
+    if (ubar) *ubar = b->ubar;
+    if (carried) *carried = b->carried;
+    if (stride) *stride = b->capacity;
+    return NMPC_OK;
+}
+
+int nmpc_fleet_sim_step(nmpc_batch* b, int B, const float* path, float* s, float* pose, float* vel, float* steer,
+                        const float* u0, const int* status, float* traj, int* traj_len, int advance, void* stream)
+{
+    if (!b) return set_err(NMPC_ERR_ARG, "batch is NULL");
+    if (B < 0 || B > b->capacity) return set_err(NMPC_ERR_ARG, "B out of range [0, capacity]");
+    if (!path || !s || !pose || !vel || !traj || (advance && !u0)) return set_err(NMPC_ERR_ARG, "NULL argument");
+    hipStream_t st = (hipStream_t)stream;
+    hipError_t e;
+    switch (b->prm.model) {
+    case NMPC_MODEL_DIFF2AMR:
+        e = launch_fleet_sim<Diff2>(b->kp, B, b->capacity, path, s, pose, vel, steer, u0, status, b->carried, traj,
+                                    traj_len, advance, st);
+        break;
+    case NMPC_MODEL_OMNI4AMR:
+        e = launch_fleet_sim<Omni4>(b->kp, B, b->capacity, path, s, pose, vel, steer, u0, status, b->carried, traj,
+                                    traj_len, advance, st);
+        break;
+    default:
+        e = launch_fleet_sim<Tric3>(b->kp, B, b->capacity, path, s, pose, vel, steer, u0, status, b->carried, traj,
+                                    traj_len, advance, st);
+        break;
+    }
+    return hip_err(e, "fleet_sim launch");
+}
+
+}  // extern "C"

@@ -1,0 +1,83 @@
+// nmpc_kernels.hpp -- kernel-side interface shared by the HIP kernels and the C-ABI host code.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+
+#include "nmpc_models.hpp"
+
+namespace nmpc {
+
+constexpr float kPi = 3.14159265358979323846f;
+
+enum KernelMode { kModeSolve = 0, kModeRun = 1 };
+
+// Device pointers of one batched launch. Public inputs/outputs are [field][B] (instance-minor);
+// the device-resident state (iterate, carried refs, scratch) is [field][stride], stride = capacity.
+struct KArgs {
+    int B, stride;
+    float* xbar;     // [(N+1)*NX][stride]   SQP iterate, warm start of the next tick
+    float* ubar;     // [N*NU][stride]
+    float* carried;  // [NBX][stride]        ref states carried between ticks (run mode)
+    float* scratch;  // per-stage workspace
+    // solve mode
+    const float* x0;    // [NX][B]
+    const float* yref;  // [N+1][ny_in][B]
+    int ny_in;
+    const float* We;  // [NX][B] or nullptr
+    // run mode
+    const float* pose;   // [3][B]
+    const float* vel;    // [3][B]  {v, vn, w}
+    const float* steer;  // [B] or nullptr
+    const float* traj;   // [N+1][3][B]
+    const int* traj_len; // [B] or nullptr (= N+1)
+    const unsigned char* reset;  // [B] or nullptr
+    // outputs (each may be nullptr)
+    float* u0;     // [NU][B]
+    float* x1;     // [NX][B]
+    float* cmd;    // [3][B]
+    int* status;   // [B]
+    int* qp_iter;  // [B]
+    float* qp_res; // [3][B] res_stat, res_ineq, mu at IPM exit
+    float* xtraj;  // [(N+1)*NX][B]
+    float* utraj;  // [N*NU][B]
+};
+
+template <int NU>
+__device__ inline void chol_solve_neg(const float (&L)[NU][NU], const float (&r)[NU], float (&y)[NU])
+{
+    // y = -(L L')^{-1} r
+    float w[NU];
+#pragma unroll
+    for (int i = 0; i < NU; i++) {
+        float s = r[i];
+#pragma unroll
+        for (int q = 0; q < i; q++) s -= L[i][q] * w[q];
+        w[i] = s / L[i][i];
+    }
+#pragma unroll
+    for (int i = NU - 1; i >= 0; i--) {
+        float s = w[i];
+#pragma unroll
+        for (int q = i + 1; q < NU; q++) s -= L[q][i] * y[q];
+        y[i] = s / L[i][i];
+    }
+#pragma unroll
+    for (int i = 0; i < NU; i++) y[i] = -y[i];
+}
+
+__device__ inline float step_bound(float amax, float v, float dv)
+{
+    return (dv < 0.0f) ? fminf(amax, -v / dv) : amax;
+}
+
+template <class M>
+size_t lane_scratch_floats(int N, int stride);
+template <class M>
+hipError_t launch_sqp_rti_lane(const KParams& P, const KArgs& a, int mode, hipStream_t stream);
+template <class M>
+hipError_t launch_fleet_sim(const KParams& P, int B, int stride, const float* path, float* s, float* pose, float* vel,
+                            float* steer, const float* u0, const int* status, const float* carried, float* traj,
+                            int* traj_len, int advance, hipStream_t stream);
+
+}  // namespace nmpc

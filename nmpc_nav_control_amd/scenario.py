@@ -1,0 +1,84 @@
+"""Seeded synthetic robot fleets (SURVEY.md 8d "Synthetic inputs").
+
+Every robot starts at x, y ~ U(-1, 1) m, theta ~ U(-pi, pi), wheel / speed / steering states ~ U(-0.5, 0.5)
+and carried vel-ref states ~ U(-0.5, 0.5). Half of the robots follow a circular-arc path (start within
+0.2 m and 0.3 rad of the robot, curvature ~ U(-k, k) 1/m, |v| ~ U(0.2, 0.8) m/s, length ~ U(3, 5) m);
+the other half drive to a goal pose (x, y ~ U(-1.5, 1.5) m, random heading), which repeats one pose
+N+1 times and so triggers the diff terminal-weight hack (NMPCNavControlDiff.cpp:127-139).
+Arrays are float32 in the instance-minor [field][B] layout of include/nmpc_amd/nmpc_batch.h.
+"""
+import numpy as np
+
+from ._lib import model_dims
+
+DEFAULT_SEED = 20250824
+PARAMS = {"diff": (0.270, 0.1, 0.0), "omni4": (0.535, 0.1, 0.0), "tric": (0.270, 0.1, 0.5)}
+
+
+def make_fleet(model, B, seed=DEFAULT_SEED, kappa_max=None, path_frac=0.5, p=None):
+    rng = np.random.default_rng(seed)
+    d = model_dims(model)
+    p = PARAMS[model] if p is None else p
+    if kappa_max is None:
+        kappa_max = 2.5 if model == "tric" else 1.0  # tric: drive alpha_ref into its bounds (BASELINE config 4)
+    pose = np.stack([rng.uniform(-1, 1, B), rng.uniform(-1, 1, B), rng.uniform(-np.pi, np.pi, B)])
+    vel = np.zeros((3, B))
+    steer = np.zeros(B)
+    if model == "diff":
+        vl, vr = rng.uniform(-0.5, 0.5, B), rng.uniform(-0.5, 0.5, B)
+        vel[0] = 0.5 * (vl + vr)
+        vel[2] = (vr - vl) / p[0]
+    elif model == "omni4":
+        w = rng.uniform(-0.5, 0.5, (4, B))
+        vel[0] = 0.25 * (w[0] - w[1] + w[2] - w[3])
+        vel[1] = 0.25 * (-w[0] - w[1] + w[2] + w[3])
+        vel[2] = -(w[0] + w[1] + w[2] + w[3]) / (2.0 * p[0])
+    else:
+        vel[0] = rng.uniform(-0.5, 0.5, B)
+        steer = rng.uniform(-0.5, 0.5, B)
+    carried = rng.uniform(-0.5, 0.5, (d["nbx"], B))
+    is_path = rng.uniform(0, 1, B) < path_frac
+    path = np.zeros((6, B))
+    # arcs
+    r = rng.uniform(0, 0.2, B)
+    a = rng.uniform(-np.pi, np.pi, B)
+    path[0] = pose[0] + r * np.cos(a)
+    path[1] = pose[1] + r * np.sin(a)
+    path[2] = pose[2] + rng.uniform(-0.3, 0.3, B)
+    path[3] = rng.uniform(-kappa_max, kappa_max, B)
+    path[4] = rng.uniform(0.2, 0.8, B)
+    path[5] = rng.uniform(3.0, 5.0, B)
+    # goals
+    goal = np.stack([rng.uniform(-1.5, 1.5, B), rng.uniform(-1.5, 1.5, B), rng.uniform(-np.pi, np.pi, B)])
+    path[:3, ~is_path] = goal[:, ~is_path]
+    path[3:5, ~is_path] = 0.0
+    path[5, ~is_path] = -1.0
+    f32 = lambda x: np.ascontiguousarray(x, dtype=np.float32)  # noqa: E731
+    return dict(pose=f32(pose), vel=f32(vel), steer=f32(steer), carried=f32(carried), path=f32(path),
+                s=np.zeros(B, np.float32), is_path=is_path)
+
+
+def arc_pose(path, i, s):
+    """Pose at arc length s on robot i's path (same formula as fleet_sim.hip)."""
+    x0, y0, th0, kap = (float(path[j, i]) for j in range(4))
+    th = th0 + kap * s
+    if abs(kap) > 1e-4:
+        return np.array([x0 + (np.sin(th) - np.sin(th0)) / kap, y0 - (np.cos(th) - np.cos(th0)) / kap, th])
+    return np.array([x0 + s * np.cos(th0), y0 + s * np.sin(th0), th])
+
+
+def refs_for(path, i, pose, s_prev, N, dt):
+    """Reference poses of robot i (CPU mirror of fleet_sim.hip, for CPU-only tests).
+    Returns (traj [n][3], s_new)."""
+    if path[5, i] < 0:
+        return path[:3, i][None, :].astype(np.float64), s_prev
+    length = float(path[5, i])
+    sc = float(s_prev)
+    for _ in range(3):
+        q = arc_pose(path, i, sc)
+        sc += (pose[0] - q[0]) * np.cos(q[2]) + (pose[1] - q[1]) * np.sin(q[2])
+        sc = min(max(sc, 0.0), length)
+    sc = max(sc, s_prev)
+    spacing = abs(float(path[4, i])) * dt
+    traj = np.stack([arc_pose(path, i, min(sc + (k + 1) * spacing, length)) for k in range(N + 1)])
+    return traj, sc

@@ -1,0 +1,114 @@
+"""GPU parity of the HIP SQP-RTI path against the fp64 CPU oracle (same inputs, same warm iterate).
+
+Tolerance (DESIGN.md "Parity"): |u - u_oracle|_inf <= 1e-3 and the predicted state trajectory
+within 1e-3 (m / rad / m/s), with the GPU IPM stopped by its fp32 rule (tol_stat 1e-4, tol_ineq 1e-5,
+tol_comp 1e-6) and the oracle by its fp64 rule (1e-8 / 1e-8 / 1e-10).
+"""
+import numpy as np
+import pytest
+import torch
+
+from helpers import oracle_closed_loop
+
+from nmpc_nav_control_amd.batch import BatchSolver
+from nmpc_nav_control_amd.scenario import make_fleet
+from oracle.oracle import Oracle
+
+pytestmark = pytest.mark.gpu
+TOL_U = 1e-3
+TOL_X = 1e-3
+DEV = torch.device("cuda:0")
+MODELS = ["diff", "omni4", "tric"]
+
+
+def t(a, dtype=torch.float32):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(device=DEV, dtype=dtype)
+
+
+def upload_iterate(solver, xbars, ubars):
+    """xbars [B][N+1][NX] -> device [(N+1)*NX][cap]."""
+    B = len(xbars)
+    xv, uv, _ = solver.state()
+    X = xv.to_tensor()
+    U = uv.to_tensor()
+    X[:, :B] = t(np.stack(xbars).reshape(B, -1).T)
+    U[:, :B] = t(np.stack(ubars).reshape(B, -1).T)
+    xv.copy_from(X)
+    uv.copy_from(U)
+
+
+@pytest.mark.parametrize("model", MODELS)
+@pytest.mark.parametrize("N,B,ticks", [(20, 48, 8), (40, 5, 4)])
+def test_solve_matches_oracle(built, model, N, B, ticks):
+    o, rec = oracle_closed_loop(model, N, B, ticks)
+    solver = BatchSolver(model, N, 64)
+    nx, nu, ny = o.nx, o.nu, o.ny
+    x0 = np.stack([r[0] for r in rec]).T
+    yref = np.stack([r[1] for r in rec]).transpose(1, 2, 0)
+    We = np.stack([r[2] for r in rec]).T
+    upload_iterate(solver, [r[3] for r in rec], [r[4] for r in rec])
+    xtraj = torch.zeros((N + 1) * nx, B, device=DEV)
+    utraj = torch.zeros(N * nu, B, device=DEV)
+    status = torch.full((B,), -7, dtype=torch.int32, device=DEV)
+    qp_iter = torch.zeros(B, dtype=torch.int32, device=DEV)
+    solver.solve(t(x0), t(yref), We=t(We), xtraj=xtraj, utraj=utraj, status=status, qp_iter=qp_iter)
+    torch.cuda.synchronize()
+    st = status.cpu().numpy()
+    assert (st == 0).all(), st
+    xg = xtraj.cpu().numpy().T.reshape(B, N + 1, nx)
+    ug = utraj.cpu().numpy().T.reshape(B, N, nu)
+    eu, ex = 0.0, 0.0
+    for i, r in enumerate(rec):
+        s, stats, xb, ub = o.sqp_rti(r[3], r[4], r[0], r[1], r[2])
+        assert s == 0
+        eu = max(eu, np.abs(ug[i] - ub).max())
+        ex = max(ex, np.abs(xg[i] - xb).max())
+    assert eu <= TOL_U, eu
+    assert ex <= TOL_X, ex
+    assert qp_iter.cpu().numpy().max() < 50
+
+
+@pytest.mark.parametrize("model", MODELS)
+def test_run_closed_loop_matches_oracle(built, model):
+    """Batched run() + closed-loop plant on the GPU; the oracle replays the same per-tick inputs with its own
+    fp64 warm-start chain (prepare -> sqp_rti -> post, NMPCNavControl*::run)."""
+    N, B, T = 20, 70, 12
+    fl = make_fleet(model, B, seed=11)
+    solver = BatchSolver(model, N, B)
+    o = Oracle(model, N)
+    _, _, cr = solver.state()
+    cr.copy_from(t(fl["carried"]))
+    pose, vel, steer, path, s = t(fl["pose"]), t(fl["vel"]), t(fl["steer"]), t(fl["path"]), t(fl["s"])
+    steer_arg = steer if model == "tric" else None
+    traj = torch.zeros(N + 1, 3, B, device=DEV)
+    tlen = torch.zeros(B, dtype=torch.int32, device=DEV)
+    cmd = torch.zeros(3, B, device=DEV)
+    u0 = torch.zeros(solver.nu, B, device=DEV)
+    status = torch.zeros(B, dtype=torch.int32, device=DEV)
+    xbar = np.zeros((B, N + 1, o.nx))
+    ubar = np.zeros((B, N, o.nu))
+    for i in range(B):
+        xbar[i], ubar[i] = o.iterate_create()
+    carried = np.ascontiguousarray(fl["carried"].T, np.float64)
+    solver.fleet_sim_step(path, s, pose, vel, steer_arg, None, None, traj, tlen, advance=False)
+    worst = 0.0
+    for tick in range(T):
+        torch.cuda.synchronize()
+        pose_h = np.ascontiguousarray(pose.cpu().numpy().T, np.float64)
+        vel_h = np.ascontiguousarray(vel.cpu().numpy().T, np.float64)
+        steer_h = np.ascontiguousarray(steer.cpu().numpy(), np.float64)
+        traj_h = np.ascontiguousarray(traj.cpu().numpy().transpose(2, 0, 1), np.float64)
+        tlen_h = np.ascontiguousarray(tlen.cpu().numpy(), np.int32)
+        solver.run(pose, vel, traj, steer=steer_arg, traj_len=tlen, cmd=cmd, u0=u0, status=status)
+        nf, cmd_o, u0_o, st_o, _ = o.batch_tick(pose_h, vel_h, steer_h if model == "tric" else None, traj_h, tlen_h,
+                                                None, carried, xbar, ubar)
+        torch.cuda.synchronize()
+        assert nf == 0
+        assert (status.cpu().numpy() == 0).all()
+        eu = np.abs(u0.cpu().numpy().T - u0_o).max()
+        ec = np.abs(cmd.cpu().numpy().T - cmd_o).max()
+        worst = max(worst, eu)
+        assert eu <= TOL_U, (tick, eu)
+        assert ec <= TOL_U, (tick, ec)
+        solver.fleet_sim_step(path, s, pose, vel, steer_arg, u0, status, traj, tlen, advance=True)
+    assert np.isfinite(worst)
