@@ -1,0 +1,280 @@
+#!/usr/bin/env python3
+"""Headline benchmark: batched SQP-RTI iterations/s (BASELINE.json metric), diff N=40 B=4096 per GPU.
+
+One step = one control tick of a closed-loop robot fleet resident in HBM: the batched
+NMPCNavControl::run() (x0 packing, reference unwrap/padding, terminal-weight hack, one SQP-RTI
+iteration = RK4 linearisation + Riccati IPM QP + full step, post-solve command) followed by the
+harness kernel that advances the plant one RK4 step and regenerates the path references.
+value = (instances x steps, all ranks) / max-over-ranks wall time of the timed region.
+
+Also reported: the u0 max-abs error against the fp64 CPU oracle on identical inputs,
+the executed IPM iterations, the roofline of the dominant kernel (algorithmic FLOPs from the SURVEY
+formula / HIP-event kernel time; FP32 peak 157.3 TF/s), and the CPU baseline (the oracle, OpenMP on
+the host cores, on a bounded sample of the same workload, rank 0 at N=1 only).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from nmpc_nav_control_amd.batch import BatchSolver  # noqa: E402
+from nmpc_nav_control_amd.scenario import DEFAULT_SEED, make_fleet  # noqa: E402
+
+# BASELINE.json configs (index -> seed offset 20250824 + idx)
+CONFIGS = {
+    "metric": dict(idx=1, models=[("diff", 4096)], N=40, desc="diff2amr N=40 batch=4096 per GPU"),
+    "diff1024": dict(idx=1, models=[("diff", 1024)], N=40, desc="diff2amr N=40 batch=1024"),
+    "omni4": dict(idx=2, models=[("omni4", 4096)], N=40, desc="omni4amr (11x4) N=40 batch=4096"),
+    "tric": dict(idx=3, models=[("tric", 8192)], N=60, desc="tric3amr N=60 batch=8192, alpha bounds active"),
+    # whole fleet: 65536 robots over 8 GPUs -> 8192 per GPU, a third of each model
+    "mixed": dict(idx=4, models=[("diff", 2731), ("omni4", 2731), ("tric", 2730)], N=40,
+                  desc="mixed fleet diff+omni4+tric, 8192 per GPU (65536 on 8 GPUs)"),
+}
+# SURVEY.md 8d algorithmic FLOPs per instance-iteration: F = N*F_lin + K*N*F_ipm
+MODEL_FLOPS = {"diff": dict(nx=7, nu=2, nbx=2, nbu=2, nnz_jx=12, nnz_ju=2, c_f=20),
+               "omni4": dict(nx=11, nu=4, nbx=4, nbu=4, nnz_jx=22, nnz_ju=4, c_f=40),
+               "tric": dict(nx=7, nu=2, nbx=2, nbu=2, nnz_jx=12, nnz_ju=2, c_f=24)}
+FP32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 vector (and FP32-input MFMA) peak
+HBM_PEAK_GBS = 8000.0
+
+
+def flops_per_instance(model, N, K):
+    m = MODEL_FLOPS[model]
+    nx, nu, nv = m["nx"], m["nu"], m["nx"] + m["nu"]
+    f_lin = 4 * (m["c_f"] + 2 * m["nnz_jx"] * nv + m["nnz_ju"]) + 16 * nx * (1 + nv)
+    f_ipm = (2 * nv * nx * nx + nv * (nv + 1) * nx + (nu ** 3) // 3 + nu * nu * nx + nx * nx * nu + 4 * nv * nx
+             + 2 * nu * nx + nu * nu + 2 * nx * nv + 2 * nx * nx
+             + 20 * (m["nbx"] + m["nbu"]) + 4 * nx * nv)
+    return N * f_lin + K * N * f_ipm
+
+
+def bytes_per_instance(model, N):
+    """Compulsory fp32 bytes per instance-iteration: x0, pose refs, iterate in+out, status."""
+    m = MODEL_FLOPS[model]
+    return 4 * (m["nx"] + 3 * (N + 1) + 2 * ((N + 1) * m["nx"] + N * m["nu"]) + 1)
+
+
+class Fleet:
+    """One model's robots on this GPU: solver + closed-loop state, all device-resident."""
+
+    def __init__(self, model, B, N, seed, dev):
+        self.model, self.B, self.N = model, B, N
+        self.solver = BatchSolver(model, N, B, device=dev)
+        fl = make_fleet(model, B, seed=seed)
+        t = lambda a, dt=torch.float32: torch.from_numpy(np.ascontiguousarray(a)).to(dev, dt)  # noqa: E731
+        self.pose, self.vel, self.path, self.s = t(fl["pose"]), t(fl["vel"]), t(fl["path"]), t(fl["s"])
+        self.steer = t(fl["steer"]) if model == "tric" else None
+        _, _, cr = self.solver.state()
+        cr.copy_from(t(fl["carried"]))
+        self.traj = torch.zeros(N + 1, 3, B, device=dev)
+        self.tlen = torch.zeros(B, dtype=torch.int32, device=dev)
+        self.cmd = torch.zeros(3, B, device=dev)
+        self.u0 = torch.zeros(self.solver.nu, B, device=dev)
+        self.status = torch.zeros(B, dtype=torch.int32, device=dev)
+        self.qp_iter = torch.zeros(B, dtype=torch.int32, device=dev)
+        self.solver.fleet_sim_step(self.path, self.s, self.pose, self.vel, self.steer, None, None, self.traj,
+                                   self.tlen, advance=False)
+
+    def solve(self):
+        self.solver.run(self.pose, self.vel, self.traj, steer=self.steer, traj_len=self.tlen, cmd=self.cmd,
+                        u0=self.u0, status=self.status, qp_iter=self.qp_iter)
+
+    def advance(self):
+        self.solver.fleet_sim_step(self.path, self.s, self.pose, self.vel, self.steer, self.u0, self.status,
+                                   self.traj, self.tlen, advance=True)
+
+    def tick(self):
+        self.solve()
+        self.advance()
+
+
+def cpu_baseline(fleets, dev, sample, ticks, nthreads):
+    """Replay `ticks` GPU ticks for the first `sample` robots of each fleet through the fp64 oracle
+    (identical inputs, oracle warm-started from the GPU iterate): CPU it/s and u0 max-abs error."""
+    from oracle.oracle import Oracle
+    total_time, total_solves, err, fails = 0.0, 0, 0.0, 0
+    for f in fleets:
+        S = min(sample, f.B)
+        o = Oracle(f.model, f.N)
+        torch.cuda.synchronize()
+        xv, uv, cv = f.solver.state()
+        X, U, Cr = xv.to_tensor(), uv.to_tensor(), cv.to_tensor()
+        xbar = np.ascontiguousarray(X[:, :S].cpu().numpy().T.reshape(S, f.N + 1, o.nx), np.float64)
+        ubar = np.ascontiguousarray(U[:, :S].cpu().numpy().T.reshape(S, f.N, o.nu), np.float64)
+        carried = np.ascontiguousarray(Cr[:, :S].cpu().numpy().T, np.float64)
+        for _ in range(ticks):
+            torch.cuda.synchronize()
+            pose = np.ascontiguousarray(f.pose[:, :S].cpu().numpy().T, np.float64)
+            vel = np.ascontiguousarray(f.vel[:, :S].cpu().numpy().T, np.float64)
+            steer = np.ascontiguousarray(f.steer[:S].cpu().numpy(), np.float64) if f.steer is not None else None
+            traj = np.ascontiguousarray(f.traj[:, :, :S].cpu().numpy().transpose(2, 0, 1), np.float64)
+            tlen = np.ascontiguousarray(f.tlen[:S].cpu().numpy(), np.int32)
+            f.solve()
+            t0 = time.perf_counter()
+            nf, cmd_o, u0_o, st_o, _ = o.batch_tick(pose, vel, steer, traj, tlen, None, carried, xbar, ubar,
+                                                    nthreads=nthreads)
+            total_time += time.perf_counter() - t0
+            total_solves += S
+            torch.cuda.synchronize()
+            ok = (st_o == 0) & (f.status[:S].cpu().numpy() == 0)
+            fails += int((~ok).sum())
+            if ok.any():
+                err = max(err, float(np.abs(f.u0[:, :S].cpu().numpy().T[ok] - u0_o[ok]).max()))
+            f.advance()
+    return total_solves / total_time, err, fails, total_solves
+
+
+def main():
+    ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--config", default="metric", choices=sorted(CONFIGS))
+    ap.add_argument("--closed-loop-warmup", type=int, default=20, help="ticks before timing (SURVEY 8d: T=20)")
+    ap.add_argument("--cpu-sample", type=int, default=256, help="robots per model replayed on the CPU oracle")
+    ap.add_argument("--cpu-ticks", type=int, default=8)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--gather", action="store_true", help="all-gather u0+status to rank 0 every tick (RCCL)")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    dev = torch.device("cuda", local_rank)
+    torch.cuda.set_device(dev)
+
+    cfg = CONFIGS[args.config]
+    gather = args.gather or (args.config == "mixed" and world > 1)
+    seed = DEFAULT_SEED + cfg["idx"] + 1000 * rank
+    fleets = [Fleet(m, B, cfg["N"], seed + j, dev) for j, (m, B) in enumerate(cfg["models"])]
+    B_rank = sum(f.B for f in fleets)
+    gbuf = None
+    if gather:
+        gsrc = torch.zeros(5, B_rank, device=dev)
+        gbuf = [torch.zeros_like(gsrc) for _ in range(world)]
+
+    def step():
+        for f in fleets:
+            f.tick()
+        if gather:
+            off = 0
+            for f in fleets:
+                gsrc[:f.solver.nu, off:off + f.B] = f.u0
+                gsrc[4, off:off + f.B] = f.status.float()
+                off += f.B
+            dist.all_gather(gbuf, gsrc)
+
+    for _ in range(args.closed_loop_warmup + args.warmup):
+        step()
+    torch.cuda.synchronize()
+
+    # per-kernel timing of the solve launches with HIP events on the launch stream
+    stream = torch.cuda.current_stream()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    iters_sum = torch.zeros((), dtype=torch.float64, device=dev)
+    iters_max = torch.zeros((), dtype=torch.int32, device=dev)
+    fail_cnt = torch.zeros((), dtype=torch.int64, device=dev)
+
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        for f in fleets:
+            ev[k][0].record(stream)
+            f.solve()
+            ev[k][1].record(stream)
+            f.advance()
+        if gather:
+            off = 0
+            for f in fleets:
+                gsrc[:f.solver.nu, off:off + f.B] = f.u0
+                gsrc[4, off:off + f.B] = f.status.float()
+                off += f.B
+            dist.all_gather(gbuf, gsrc)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # stats outside the timed region (one more tick, same state machine)
+    for f in fleets:
+        f.solve()
+        iters_sum += f.qp_iter.double().sum()
+        iters_max = torch.maximum(iters_max, f.qp_iter.max())
+        fail_cnt += (f.status != 0).sum()
+        f.advance()
+    torch.cuda.synchronize()
+    kernel_ms = [ev[k][0].elapsed_time(ev[k][1]) for k in range(args.steps)] if len(fleets) == 1 else None
+    k_mean = float(iters_sum.item()) / B_rank
+    units = args.steps * B_rank * world
+    value = units / elapsed
+
+    result = None
+    if rank == 0:
+        roof = None
+        if kernel_ms:
+            f = fleets[0]
+            t_k = float(np.mean(kernel_ms)) * 1e-3
+            flops = f.B * flops_per_instance(f.model, f.N, k_mean)
+            achieved = flops / t_k / 1e12
+            traffic = None
+            pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+            if os.path.exists(pmc):
+                with open(pmc) as fh:
+                    d = json.load(fh)
+                key = f"{f.model}_N{f.N}_B{f.B}"
+                traffic = d.get(key, {}).get("hbm_bytes_per_launch")
+            roof = {"bound": "mfma", "achieved": round(achieved, 4), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                    "frac": round(achieved / FP32_PEAK_TFLOPS, 6), "traffic": traffic,
+                    "kernel": "k_sqp_rti_lane", "kernel_ms_mean": round(t_k * 1e3, 4),
+                    "algorithmic_flop_per_launch": flops, "qp_iter_mean": round(k_mean, 3),
+                    "compulsory_bytes_per_launch": f.B * bytes_per_instance(f.model, f.N),
+                    "achieved_compulsory_GBs": round(f.B * bytes_per_instance(f.model, f.N) / t_k / 1e9, 2),
+                    "note": "FP32 VALU-bound (no GEMM-sized blocks); peak = MI355X FP32 vector = FP32 MFMA rate"}
+        cpu = None
+        u0_err = None
+        if not args.no_cpu_baseline and world == 1:
+            nthreads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+            cpu_rate, u0_err, nf, ns = cpu_baseline(fleets, dev, args.cpu_sample, args.cpu_ticks, nthreads)
+            cpu = {"value": round(cpu_rate, 1), "unit": "SQP-RTI iterations/sec", "cores": nthreads, "kind": "port",
+                   "sample": f"{ns} instance-iterations: first {args.cpu_sample} robots of each model x "
+                             f"{args.cpu_ticks} closed-loop ticks after the timed region, fp64 oracle/nmpc_oracle.c, "
+                             f"OpenMP {nthreads} threads, identical inputs", "failed": nf}
+        result = {
+            "metric": "SQP-RTI iterations/sec (whole node), diff N=40 batch=4096; u0 max-abs err",
+            "value": round(value, 1), "unit": "SQP-RTI iterations/sec", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+            "data": "synthetic seeded closed-loop fleet (SURVEY 8d), random-arc paths + goal poses",
+            "config": {"workload": cfg["desc"], "config": args.config, "N": cfg["N"],
+                       "batch_per_gpu": B_rank, "global_batch": B_rank * world,
+                       "models": [m for m, _ in cfg["models"]], "parallelism": f"instance-sharded x{world}",
+                       "closed_loop_warmup_ticks": args.closed_loop_warmup, "rccl_gather": gather},
+            "u0_max_abs_err": u0_err, "qp_iter_mean": round(k_mean, 3), "qp_iter_max": int(iters_max.item()),
+            "failed_instances": int(fail_cnt.item()), "roofline": roof, "cpu_baseline": cpu,
+        }
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    return result
+
+
+if __name__ == "__main__":
+    main()

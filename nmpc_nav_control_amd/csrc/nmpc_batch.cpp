@@ -175,7 +175,7 @@ int nmpc_model_params_default(int model, int N, nmpc_model_params* prm)
     for (int i = 0; i < nx; i++) prm->W_e[i] = prm->W[i];  // NMPCNavControlDiff.cpp:39-41
     prm->qp_iter_max = 50;
     prm->qp_tol_stat = 1e-4;
-    prm->qp_tol_ineq = 1e-5;
+    prm->qp_tol_ineq = 1e-6;
     prm->qp_tol_comp = 1e-10;
     prm->qp_mu0 = 1.0;
     prm->qp_thr0 = 0.5;

@@ -55,6 +55,10 @@ size_t lane_scratch_floats(int N, int stride)
 namespace {
 
 constexpr float kBreakdownMu = 1e-6f;
+constexpr float kStatRel = 1e-5f;  // ~100 ulp of fp32
+
+// max that propagates NaN (fmaxf drops it)
+__device__ inline float nan_max(float a, float b) { return (b > a || b != b) ? b : a; }
 
 // Per-comp variable of stage k: comps [0, NBU) are u[idxbu], [NBU, NB) are x[idxbx].
 template <class M>
@@ -252,7 +256,7 @@ __global__ __launch_bounds__(64, 1) void k_sqp_rti_lane(KParams P, KArgs a, int 
     for (it = 0;; it++) {
         // P1 (backward): apply previous update, residuals, adjoint pi, factorisation + predictor rhs.
         float Lp[NX][NX], pv[NX], pin[NX];
-        float res_stat = 0.0f, res_ineq = 0.0f, sum_c = 0.0f;
+        float res_stat = 0.0f, res_ineq = 0.0f, sum_c = 0.0f, stat_scale = 1.0f;
         bool fail = false;
         for (int k = N; k >= 0; k--) {
             float du[NU], dx[NX];
@@ -304,7 +308,7 @@ __global__ __launch_bounds__(64, 1) void k_sqp_rti_lane(KParams P, KArgs a, int 
                     FLD(k, Lay::LU + c) = lu;
                 }
                 const float rl = z - lb - tl, rr = ubd - z - tu;
-                res_ineq = fmaxf(res_ineq, fmaxf(fabsf(rl), fabsf(rr)));
+                res_ineq = nan_max(res_ineq, fmaxf(fabsf(rl), fabsf(rr)));
                 sum_c += ll * tl + lu * tu;
                 // predictor rhs (target 0) and barrier Hessian
                 const float gh = (ll * rl) / tl + ll - (lu * rr) / tu - lu;
@@ -355,12 +359,16 @@ __global__ __launch_bounds__(64, 1) void k_sqp_rti_lane(KParams P, KArgs a, int 
             if (k < N) {
 #pragma unroll
                 for (int i = 0; i < NU; i++) {
-                    float s = sc * P.W[NX + i] * du[i] + FLD(k, Lay::GU + i) - lamdiff_u[i];
+                    const float gu = FLD(k, Lay::GU + i);
+                    float s = sc * P.W[NX + i] * du[i] + gu - lamdiff_u[i];
+                    float bp = 0.0f;
 #pragma unroll
-                    for (int l = 0; l < NX; l++) s += Bm[l][i] * pin[l];
+                    for (int l = 0; l < NX; l++) bp += Bm[l][i] * pin[l];
+                    s += bp;
                     ru[i] = s;
                     FLD(k, Lay::RU + i) = s;
-                    res_stat = fmaxf(res_stat, fabsf(s));
+                    res_stat = nan_max(res_stat, fabsf(s));
+                    stat_scale = fmaxf(stat_scale, fmaxf(fabsf(bp), fmaxf(fabsf(gu), fabsf(lamdiff_u[i]))));
                     gh_u[i] += s;
                 }
             }
@@ -482,7 +490,10 @@ __global__ __launch_bounds__(64, 1) void k_sqp_rti_lane(KParams P, KArgs a, int 
             break;
         }
         if (!(res_stat == res_stat) || !(mu == mu)) { status = 1; break; }
-        if (res_stat <= P.tol_stat && res_ineq <= P.tol_ineq && mu <= P.tol_comp) break;
+        // fp32 stopping rule: the u-stationarity residual is a sum of terms of size stat_scale, so it cannot
+        // fall below ~kStatRel * stat_scale; and once mu is 100x below its target the iterate is final.
+        const bool stat_ok = res_stat <= P.tol_stat || res_stat <= kStatRel * stat_scale;
+        if (res_ineq <= P.tol_ineq && ((stat_ok && mu <= P.tol_comp) || mu <= 1e-2f * P.tol_comp)) break;
         if (it >= P.iter_max) break;
 
         // P2 (forward): affine direction, its maximal step and the mu_aff polynomial.

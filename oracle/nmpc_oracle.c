@@ -218,6 +218,9 @@ void oc_rk4(const oc_params* prm, const double* x, const double* u, double h, do
 /* residual. Same optimum as HPIPM (strictly convex QP, SURVEY Appendix B "Uniqueness").              */
 /* ------------------------------------------------------------------------------------------------ */
 
+/* max that propagates NaN (fmax drops it) */
+static inline double nan_max(double a, double b) { return (b > a || b != b) ? b : a; }
+
 typedef struct {
     int nb;               /* bounded comps at this stage */
     int var[OC_NBMAX];    /* variable index: < nu -> u[idx], else x[idx - nu] */
@@ -463,7 +466,7 @@ int oc_qp_ipm(const oc_params* prm, const oc_qp* qp, oc_qp_sol* sol, oc_stats* s
                 const double z = stage_var(du + k * nu, dx + k * nx, nu, sb[k].var[c]);
                 const double rl = z - sb[k].lb[c] - tl[k * NB + c];
                 const double rr = sb[k].ub[c] - z - tu[k * NB + c];
-                res_ineq = fmax(res_ineq, fmax(fabs(rl), fabs(rr)));
+                res_ineq = nan_max(res_ineq, fmax(fabs(rl), fabs(rr)));
                 sum_c += ll[k * NB + c] * tl[k * NB + c] + lu[k * NB + c] * tu[k * NB + c];
             }
         mu = (m > 0) ? sum_c / m2 : 0.0;
@@ -486,10 +489,13 @@ int oc_qp_ipm(const oc_params* prm, const oc_qp* qp, oc_qp_sol* sol, oc_stats* s
             }
             for (int c = 0; c < sb[k].nb; c++)
                 if (sb[k].var[c] < nu) ru[k * nu + sb[k].var[c]] -= ll[k * NB + c] - lu[k * NB + c];
-            for (int i = 0; i < nu; i++) res_stat = fmax(res_stat, fabs(ru[k * nu + i]));
+            for (int i = 0; i < nu; i++) res_stat = nan_max(res_stat, fabs(ru[k * nu + i]));
         }
         if (!(res_stat == res_stat) || !(mu == mu)) { status = 1; break; }
-        if (res_stat <= prm->tol_stat && res_ineq <= prm->tol_ineq && mu <= prm->tol_comp) { status = 0; break; }
+        if (res_ineq <= prm->tol_ineq && ((res_stat <= prm->tol_stat && mu <= prm->tol_comp) || mu <= 1e-2 * prm->tol_comp)) {
+            status = 0;
+            break;
+        }
         if (it >= prm->iter_max) { status = 0; break; } /* max-iter tolerated in RTI */
 
         /* Newton solves sharing one factorisation: pass 0 predictor (affine, target 0); pass 1 Mehrotra
