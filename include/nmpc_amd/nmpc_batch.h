@@ -96,6 +96,13 @@ int nmpc_batch_run(nmpc_batch* b, int B, const float* pose, const float* vel, co
                    const float* traj, const int* traj_len, const unsigned char* reset, float* cmd, float* u0,
                    int* status, int* qp_iter, float* qp_res, void* stream);
 
+/* Kernel variant: NMPC_KERNEL_TEAM (default: 16-lane team per robot, DPP row exchange) or NMPC_KERNEL_LANE
+ * (one lane per robot; best when B >= 64k per GPU). The environment variable NMPC_AMD_KERNEL=lane|team
+ * sets the default at nmpc_batch_create. */
+#define NMPC_KERNEL_TEAM 0
+#define NMPC_KERNEL_LANE 1
+int nmpc_batch_set_kernel(nmpc_batch* b, int kernel);
+
 /* Device pointers of the resident state: xbar [(N+1)*NX][stride], ubar [N*NU][stride],
  * carried [NBX][stride]; stride = capacity. */
 int nmpc_batch_state(nmpc_batch* b, float** xbar, float** ubar, float** carried, int* stride);

@@ -48,9 +48,10 @@ class SolverCapsule(ctypes.Structure):
 BATCH_SYMBOLS = [
     "nmpc_model_dims", "nmpc_model_params_default", "nmpc_model_params_set_limits", "nmpc_batch_create",
     "nmpc_batch_destroy", "nmpc_batch_set_params", "nmpc_batch_get_params", "nmpc_batch_init_iterate",
-    "nmpc_batch_solve", "nmpc_batch_run", "nmpc_batch_state", "nmpc_fleet_sim_step", "nmpc_last_error",
-    "nmpc_version",
+    "nmpc_batch_solve", "nmpc_batch_run", "nmpc_batch_state", "nmpc_batch_set_kernel", "nmpc_fleet_sim_step",
+    "nmpc_last_error", "nmpc_version",
 ]
+KERNELS = {"team": 0, "lane": 1}
 NLP_SYMBOLS = ["ocp_nlp_constraints_model_set", "ocp_nlp_cost_model_set", "ocp_nlp_out_get", "ocp_nlp_out_set",
                "ocp_nlp_get", "ocp_nlp_dims_get_from_attr"]
 CAPSULE_SUFFIXES = ["create_capsule", "free_capsule", "create", "create_with_discretization", "reset",
@@ -86,6 +87,7 @@ def lib():
     L.nmpc_batch_init_iterate.argtypes = [vp, i, i, vp]
     L.nmpc_batch_solve.argtypes = [vp, i, vp, vp, i, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]
     L.nmpc_batch_run.argtypes = [vp, i, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]
+    L.nmpc_batch_set_kernel.argtypes = [vp, i]
     L.nmpc_batch_state.argtypes = [vp, ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.POINTER(vp), c_int_p]
     L.nmpc_fleet_sim_step.argtypes = [vp, i, vp, vp, vp, vp, vp, vp, vp, vp, vp, i, vp]
     L.nmpc_last_error.restype = ctypes.c_char_p

@@ -8,7 +8,7 @@ import ctypes
 
 import torch
 
-from ._lib import MODEL_IDS, ModelParams, check, default_params, lib, model_dims
+from ._lib import KERNELS, MODEL_IDS, ModelParams, check, default_params, lib, model_dims
 
 
 def _ptr(t):
@@ -34,7 +34,7 @@ class BatchSolver:
     iterate and carried vel-ref states resident on the device between ticks.
     """
 
-    def __init__(self, model, N, capacity, params=None, device="cuda"):
+    def __init__(self, model, N, capacity, params=None, device="cuda", kernel=None):
         self.model = model
         self.N = int(N)
         self.capacity = int(capacity)
@@ -48,6 +48,13 @@ class BatchSolver:
         with torch.cuda.device(self.device):
             check(lib().nmpc_batch_create(ctypes.byref(self.params), self.capacity, ctypes.byref(self._h)),
                   "nmpc_batch_create")
+        if kernel is not None:
+            self.set_kernel(kernel)
+
+    def set_kernel(self, kernel):
+        """'team' (16-lane team per robot, default) or 'lane' (one lane per robot)."""
+        check(lib().nmpc_batch_set_kernel(self._h, KERNELS[kernel]), "nmpc_batch_set_kernel")
+        self.kernel = kernel
 
     def close(self):
         if self._h:

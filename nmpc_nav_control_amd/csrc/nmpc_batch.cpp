@@ -5,6 +5,7 @@
 
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 
@@ -21,6 +22,7 @@ struct nmpc_batch {
     float* ubar = nullptr;
     float* carried = nullptr;
     float* scratch = nullptr;
+    int kernel = 0;  // 0: team-per-instance (default), 1: lane-per-instance
 };
 
 namespace {
@@ -73,21 +75,35 @@ KParams to_kparams(const nmpc_model_params& p, int nx, int nu, int nbx, int nbu)
     return k;
 }
 
+template <class M>
+size_t scratch_floats_m(int N, int stride)
+{
+    const size_t a = lane_scratch_floats<M>(N, stride), b = team_scratch_floats<M>(N, stride);
+    return a > b ? a : b;
+}
+
 size_t scratch_floats(int model, int N, int stride)
 {
     switch (model) {
-    case NMPC_MODEL_DIFF2AMR: return lane_scratch_floats<Diff2>(N, stride);
-    case NMPC_MODEL_OMNI4AMR: return lane_scratch_floats<Omni4>(N, stride);
-    default: return lane_scratch_floats<Tric3>(N, stride);
+    case NMPC_MODEL_DIFF2AMR: return scratch_floats_m<Diff2>(N, stride);
+    case NMPC_MODEL_OMNI4AMR: return scratch_floats_m<Omni4>(N, stride);
+    default: return scratch_floats_m<Tric3>(N, stride);
     }
+}
+
+template <class M>
+hipError_t launch_m(nmpc_batch* b, const KArgs& a, int mode, hipStream_t s)
+{
+    return b->kernel == NMPC_KERNEL_LANE ? launch_sqp_rti_lane<M>(b->kp, a, mode, s)
+                                         : launch_sqp_rti_team<M>(b->kp, a, mode, s);
 }
 
 hipError_t launch(nmpc_batch* b, const KArgs& a, int mode, hipStream_t s)
 {
     switch (b->prm.model) {
-    case NMPC_MODEL_DIFF2AMR: return launch_sqp_rti_lane<Diff2>(b->kp, a, mode, s);
-    case NMPC_MODEL_OMNI4AMR: return launch_sqp_rti_lane<Omni4>(b->kp, a, mode, s);
-    default: return launch_sqp_rti_lane<Tric3>(b->kp, a, mode, s);
+    case NMPC_MODEL_DIFF2AMR: return launch_m<Diff2>(b, a, mode, s);
+    case NMPC_MODEL_OMNI4AMR: return launch_m<Omni4>(b, a, mode, s);
+    default: return launch_m<Tric3>(b, a, mode, s);
     }
 }
 
@@ -128,7 +144,7 @@ int check_params(const nmpc_model_params* prm)
 extern "C" {
 
 const char* nmpc_last_error(void) { return g_err.c_str(); }
-const char* nmpc_version(void) { return "nmpc_amd 0.1 (lane-per-instance SQP-RTI, gfx950)"; }
+const char* nmpc_version(void) { return "nmpc_amd 0.2 (team-per-instance DPP SQP-RTI, gfx950)"; }
 
 int nmpc_model_dims(int model, int* nx, int* nu, int* ny, int* nbx, int* nbu, int* np)
 {
@@ -215,6 +231,7 @@ int nmpc_batch_create(const nmpc_model_params* prm, int capacity, nmpc_batch** o
     dims_of(prm->model, &b->nx, &b->nu, &b->nbx, &b->nbu, &np);
     b->ny = b->nx + b->nu;
     b->kp = to_kparams(*prm, b->nx, b->nu, b->nbx, b->nbu);
+    if (const char* kv = std::getenv("NMPC_AMD_KERNEL")) b->kernel = (std::strcmp(kv, "lane") == 0) ? 1 : 0;
     const int N = prm->N;
     const size_t S = (size_t)capacity;
     hipError_t e;
@@ -336,6 +353,14 @@ int nmpc_batch_run(nmpc_batch* b, int B, const float* pose, const float* vel, co
     a.qp_iter = qp_iter;
     a.qp_res = qp_res;
     return hip_err(launch(b, a, kModeRun, (hipStream_t)stream), "run launch");
+}
+
+int nmpc_batch_set_kernel(nmpc_batch* b, int kernel)
+{
+    if (!b) return set_err(NMPC_ERR_ARG, "batch is NULL");
+    if (kernel != NMPC_KERNEL_TEAM && kernel != NMPC_KERNEL_LANE) return set_err(NMPC_ERR_ARG, "unknown kernel");
+    b->kernel = kernel;
+    return NMPC_OK;
 }
 
 int nmpc_batch_state(nmpc_batch* b, float** xbar, float** ubar, float** carried, int* stride)

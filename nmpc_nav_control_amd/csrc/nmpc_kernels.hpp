@@ -76,6 +76,10 @@ size_t lane_scratch_floats(int N, int stride);
 template <class M>
 hipError_t launch_sqp_rti_lane(const KParams& P, const KArgs& a, int mode, hipStream_t stream);
 template <class M>
+size_t team_scratch_floats(int N, int stride);
+template <class M>
+hipError_t launch_sqp_rti_team(const KParams& P, const KArgs& a, int mode, hipStream_t stream);
+template <class M>
 hipError_t launch_fleet_sim(const KParams& P, int B, int stride, const float* path, float* s, float* pose, float* vel,
                             float* steer, const float* u0, const int* status, const float* carried, float* traj,
                             int* traj_len, int advance, hipStream_t stream);

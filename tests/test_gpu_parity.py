@@ -40,11 +40,15 @@ def upload_iterate(solver, xbars, ubars):
     uv.copy_from(U)
 
 
+KERNELS = ["team", "lane"]
+
+
+@pytest.mark.parametrize("kernel", KERNELS)
 @pytest.mark.parametrize("model", MODELS)
 @pytest.mark.parametrize("N,B,ticks", [(20, 48, 8), (40, 5, 4)])
-def test_solve_matches_oracle(built, model, N, B, ticks):
+def test_solve_matches_oracle(built, kernel, model, N, B, ticks):
     o, rec = oracle_closed_loop(model, N, B, ticks)
-    solver = BatchSolver(model, N, 64)
+    solver = BatchSolver(model, N, 64, kernel=kernel)
     nx, nu, ny = o.nx, o.nu, o.ny
     x0 = np.stack([r[0] for r in rec]).T
     yref = np.stack([r[1] for r in rec]).transpose(1, 2, 0)
@@ -73,13 +77,14 @@ def test_solve_matches_oracle(built, model, N, B, ticks):
     assert qp_iter.cpu().numpy().max() < 50
 
 
+@pytest.mark.parametrize("kernel", KERNELS)
 @pytest.mark.parametrize("model", MODELS)
-def test_run_closed_loop_matches_oracle(built, model):
+def test_run_closed_loop_matches_oracle(built, kernel, model):
     """Batched run() + closed-loop plant on the GPU; the oracle replays the same per-tick inputs with its own
     fp64 warm-start chain (prepare -> sqp_rti -> post, NMPCNavControl*::run)."""
     N, B, T = 20, 70, 12
     fl = make_fleet(model, B, seed=11)
-    solver = BatchSolver(model, N, B)
+    solver = BatchSolver(model, N, B, kernel=kernel)
     o = Oracle(model, N)
     _, _, cr = solver.state()
     cr.copy_from(t(fl["carried"]))
