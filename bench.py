@@ -27,6 +27,7 @@ sys.path.insert(0, ROOT)
 
 from nmpc_nav_control_amd.batch import BatchSolver  # noqa: E402
 from nmpc_nav_control_amd.scenario import DEFAULT_SEED, make_fleet  # noqa: E402
+from nmpc_nav_control_amd.sharding import CommandGather, TimedRegion, shard_range, world_info  # noqa: E402
 
 # BASELINE.json configs (index -> seed offset 20250824 + idx)
 CONFIGS = {
@@ -65,10 +66,10 @@ def bytes_per_instance(model, N):
 class Fleet:
     """One model's robots on this GPU: solver + closed-loop state, all device-resident."""
 
-    def __init__(self, model, B, N, seed, dev):
+    def __init__(self, model, B, N, seed, dev, start=0):
         self.model, self.B, self.N = model, B, N
         self.solver = BatchSolver(model, N, B, device=dev)
-        fl = make_fleet(model, B, seed=seed)
+        fl = make_fleet(model, B, seed=seed, start=start)
         t = lambda a, dt=torch.float32: torch.from_numpy(np.ascontiguousarray(a)).to(dev, dt)  # noqa: E731
         self.pose, self.vel, self.path, self.s = t(fl["pose"]), t(fl["vel"]), t(fl["path"]), t(fl["s"])
         self.steer = t(fl["steer"]) if model == "tric" else None
@@ -97,25 +98,27 @@ class Fleet:
 
 
 def cpu_baseline(fleets, dev, sample, ticks, nthreads):
-    """Replay `ticks` GPU ticks for the first `sample` robots of each fleet through the fp64 oracle
-    (identical inputs, oracle warm-started from the GPU iterate): CPU it/s and u0 max-abs error."""
+    """Replay `ticks` closed-loop GPU ticks for the first `sample` robots of each fleet through the fp64
+    oracle. Every tick the oracle starts from exactly the GPU's pre-tick state (iterate, carried refs,
+    measurements, references), so the u0 error is the per-solve fp32-vs-fp64 error, not the divergence of
+    two closed loops. Returns (CPU instance-iterations/s, u0 max-abs err, failed, solves)."""
     from oracle.oracle import Oracle
     total_time, total_solves, err, fails = 0.0, 0, 0.0, 0
+    host = lambda a: np.ascontiguousarray(a.cpu().numpy(), np.float64)  # noqa: E731
     for f in fleets:
         S = min(sample, f.B)
         o = Oracle(f.model, f.N)
-        torch.cuda.synchronize()
         xv, uv, cv = f.solver.state()
-        X, U, Cr = xv.to_tensor(), uv.to_tensor(), cv.to_tensor()
-        xbar = np.ascontiguousarray(X[:, :S].cpu().numpy().T.reshape(S, f.N + 1, o.nx), np.float64)
-        ubar = np.ascontiguousarray(U[:, :S].cpu().numpy().T.reshape(S, f.N, o.nu), np.float64)
-        carried = np.ascontiguousarray(Cr[:, :S].cpu().numpy().T, np.float64)
         for _ in range(ticks):
             torch.cuda.synchronize()
-            pose = np.ascontiguousarray(f.pose[:, :S].cpu().numpy().T, np.float64)
-            vel = np.ascontiguousarray(f.vel[:, :S].cpu().numpy().T, np.float64)
-            steer = np.ascontiguousarray(f.steer[:S].cpu().numpy(), np.float64) if f.steer is not None else None
-            traj = np.ascontiguousarray(f.traj[:, :, :S].cpu().numpy().transpose(2, 0, 1), np.float64)
+            X, U, Cr = xv.to_tensor(), uv.to_tensor(), cv.to_tensor()
+            xbar = np.ascontiguousarray(host(X[:, :S]).T.reshape(S, f.N + 1, o.nx))
+            ubar = np.ascontiguousarray(host(U[:, :S]).T.reshape(S, f.N, o.nu))
+            carried = np.ascontiguousarray(host(Cr[:, :S]).T)
+            pose = np.ascontiguousarray(host(f.pose[:, :S]).T)
+            vel = np.ascontiguousarray(host(f.vel[:, :S]).T)
+            steer = host(f.steer[:S]) if f.steer is not None else None
+            traj = np.ascontiguousarray(host(f.traj[:, :, :S]).transpose(2, 0, 1))
             tlen = np.ascontiguousarray(f.tlen[:S].cpu().numpy(), np.int32)
             f.solve()
             t0 = time.perf_counter()
@@ -145,83 +148,60 @@ def main():
     ap.add_argument("--gather", action="store_true", help="all-gather u0+status to rank 0 every tick (RCCL)")
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    rank, world, local_rank = world_info()
     dev = torch.device("cuda", local_rank)
     torch.cuda.set_device(dev)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
 
     cfg = CONFIGS[args.config]
     gather = args.gather or (args.config == "mixed" and world > 1)
-    seed = DEFAULT_SEED + cfg["idx"] + 1000 * rank
-    fleets = [Fleet(m, B, cfg["N"], seed + j, dev) for j, (m, B) in enumerate(cfg["models"])]
+    # weak scaling: the global fleet holds B x world robots of each model; this rank owns the contiguous
+    # shard [rank*B, (rank+1)*B) of it (sharding.shard_range), no collective on the solve path
+    fleets = []
+    for j, (m, B) in enumerate(cfg["models"]):
+        lo, hi = shard_range(B * world, rank, world)
+        fleets.append(Fleet(m, hi - lo, cfg["N"], DEFAULT_SEED + cfg["idx"] + 100 * j, dev, start=lo))
     B_rank = sum(f.B for f in fleets)
-    gbuf = None
-    if gather:
-        gsrc = torch.zeros(5, B_rank, device=dev)
-        gbuf = [torch.zeros_like(gsrc) for _ in range(world)]
+    cmd_gather = CommandGather(5, [B_rank] * world, dev) if gather else None
 
-    def step():
+    def gather_commands():
+        cmd_gather([torch.cat([f.u0, f.status.float()[None]]) for f in fleets])
+
+    for _ in range(args.closed_loop_warmup + args.warmup):
         for f in fleets:
             f.tick()
         if gather:
-            off = 0
-            for f in fleets:
-                gsrc[:f.solver.nu, off:off + f.B] = f.u0
-                gsrc[4, off:off + f.B] = f.status.float()
-                off += f.B
-            dist.all_gather(gbuf, gsrc)
-
-    for _ in range(args.closed_loop_warmup + args.warmup):
-        step()
+            gather_commands()
     torch.cuda.synchronize()
 
     # per-kernel timing of the solve launches with HIP events on the launch stream
     stream = torch.cuda.current_stream()
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    iters_sum = torch.zeros((), dtype=torch.float64, device=dev)
-    iters_max = torch.zeros((), dtype=torch.int32, device=dev)
-    fail_cnt = torch.zeros((), dtype=torch.int64, device=dev)
+    # executed IPM iterations and failures, accumulated on the device over the timed ticks
+    iters_sum = torch.zeros(B_rank, dtype=torch.int64, device=dev)
+    iters_max = torch.zeros(B_rank, dtype=torch.int32, device=dev)
+    fail_cnt = torch.zeros(B_rank, dtype=torch.int64, device=dev)
+    offs = np.cumsum([0] + [f.B for f in fleets])
 
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for k in range(args.steps):
-        for f in fleets:
-            ev[k][0].record(stream)
-            f.solve()
-            ev[k][1].record(stream)
-            f.advance()
-        if gather:
-            off = 0
+    with TimedRegion(dev) as region:
+        for k in range(args.steps):
             for f in fleets:
-                gsrc[:f.solver.nu, off:off + f.B] = f.u0
-                gsrc[4, off:off + f.B] = f.status.float()
-                off += f.B
-            dist.all_gather(gbuf, gsrc)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+                ev[k][0].record(stream)
+                f.solve()
+                ev[k][1].record(stream)
+                f.advance()
+            for j, f in enumerate(fleets):
+                sl = slice(offs[j], offs[j + 1])
+                iters_sum[sl] += f.qp_iter
+                torch.maximum(iters_max[sl], f.qp_iter, out=iters_max[sl])
+                fail_cnt[sl] += f.status != 0
+            if gather:
+                gather_commands()
+    elapsed = region.elapsed
 
-    # stats outside the timed region (one more tick, same state machine)
-    for f in fleets:
-        f.solve()
-        iters_sum += f.qp_iter.double().sum()
-        iters_max = torch.maximum(iters_max, f.qp_iter.max())
-        fail_cnt += (f.status != 0).sum()
-        f.advance()
-    torch.cuda.synchronize()
     kernel_ms = [ev[k][0].elapsed_time(ev[k][1]) for k in range(args.steps)] if len(fleets) == 1 else None
-    k_mean = float(iters_sum.item()) / B_rank
+    k_mean = float(iters_sum.sum().item()) / (B_rank * args.steps)
     units = args.steps * B_rank * world
     value = units / elapsed
 
@@ -242,7 +222,7 @@ def main():
                 traffic = d.get(key, {}).get("hbm_bytes_per_launch")
             roof = {"bound": "mfma", "achieved": round(achieved, 4), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
                     "frac": round(achieved / FP32_PEAK_TFLOPS, 6), "traffic": traffic,
-                    "kernel": "k_sqp_rti_lane", "kernel_ms_mean": round(t_k * 1e3, 4),
+                    "kernel": f"k_sqp_rti_{f.solver.kernel}", "kernel_ms_mean": round(t_k * 1e3, 4),
                     "algorithmic_flop_per_launch": flops, "qp_iter_mean": round(k_mean, 3),
                     "compulsory_bytes_per_launch": f.B * bytes_per_instance(f.model, f.N),
                     "achieved_compulsory_GBs": round(f.B * bytes_per_instance(f.model, f.N) / t_k / 1e9, 2),
@@ -266,8 +246,8 @@ def main():
                        "batch_per_gpu": B_rank, "global_batch": B_rank * world,
                        "models": [m for m, _ in cfg["models"]], "parallelism": f"instance-sharded x{world}",
                        "closed_loop_warmup_ticks": args.closed_loop_warmup, "rccl_gather": gather},
-            "u0_max_abs_err": u0_err, "qp_iter_mean": round(k_mean, 3), "qp_iter_max": int(iters_max.item()),
-            "failed_instances": int(fail_cnt.item()), "roofline": roof, "cpu_baseline": cpu,
+            "u0_max_abs_err": u0_err, "qp_iter_mean": round(k_mean, 3), "qp_iter_max": int(iters_max.max().item()),
+            "failed_solves": int(fail_cnt.sum().item()), "roofline": roof, "cpu_baseline": cpu,
         }
         print(json.dumps(result), flush=True)
     if world > 1:

@@ -5,6 +5,7 @@ the instance-minor ``[field][B]`` layout of include/nmpc_amd/nmpc_batch.h. All c
 kernels of the library; there is no Python or CPU fallback.
 """
 import ctypes
+import os
 
 import torch
 
@@ -48,6 +49,7 @@ class BatchSolver:
         with torch.cuda.device(self.device):
             check(lib().nmpc_batch_create(ctypes.byref(self.params), self.capacity, ctypes.byref(self._h)),
                   "nmpc_batch_create")
+        self.kernel = os.environ.get("NMPC_AMD_KERNEL", "team")  # the library's own default selection
         if kernel is not None:
             self.set_kernel(kernel)
 

@@ -15,12 +15,14 @@ DEFAULT_SEED = 20250824
 PARAMS = {"diff": (0.270, 0.1, 0.0), "omni4": (0.535, 0.1, 0.0), "tric": (0.270, 0.1, 0.5)}
 
 
-def make_fleet(model, B, seed=DEFAULT_SEED, kappa_max=None, path_frac=0.5, p=None):
-    rng = np.random.default_rng(seed)
-    d = model_dims(model)
-    p = PARAMS[model] if p is None else p
-    if kappa_max is None:
-        kappa_max = 2.5 if model == "tric" else 1.0  # tric: drive alpha_ref into its bounds (BASELINE config 4)
+BLOCK = 64  # robots per independently seeded block: a robot's data depends only on (seed, global index)
+
+
+def _block(model, seed, blk, kappa_max, path_frac, p):
+    """Robots [blk*BLOCK, (blk+1)*BLOCK) of the global fleet, float64 [field][BLOCK]."""
+    rng = np.random.default_rng([seed, blk])
+    B = BLOCK
+    nbx = model_dims(model)["nbx"]
     pose = np.stack([rng.uniform(-1, 1, B), rng.uniform(-1, 1, B), rng.uniform(-np.pi, np.pi, B)])
     vel = np.zeros((3, B))
     steer = np.zeros(B)
@@ -36,7 +38,7 @@ def make_fleet(model, B, seed=DEFAULT_SEED, kappa_max=None, path_frac=0.5, p=Non
     else:
         vel[0] = rng.uniform(-0.5, 0.5, B)
         steer = rng.uniform(-0.5, 0.5, B)
-    carried = rng.uniform(-0.5, 0.5, (d["nbx"], B))
+    carried = rng.uniform(-0.5, 0.5, (nbx, B))
     is_path = rng.uniform(0, 1, B) < path_frac
     path = np.zeros((6, B))
     # arcs
@@ -53,9 +55,27 @@ def make_fleet(model, B, seed=DEFAULT_SEED, kappa_max=None, path_frac=0.5, p=Non
     path[:3, ~is_path] = goal[:, ~is_path]
     path[3:5, ~is_path] = 0.0
     path[5, ~is_path] = -1.0
+    return dict(pose=pose, vel=vel, steer=steer, carried=carried, path=path, is_path=is_path)
+
+
+def make_fleet(model, B, seed=DEFAULT_SEED, kappa_max=None, path_frac=0.5, p=None, start=0):
+    """Robots [start, start + B) of the seeded global fleet (so an instance shard of a multi-GPU run holds
+    exactly the robots a single-GPU run of the whole fleet would give those indices)."""
+    p = PARAMS[model] if p is None else p
+    if kappa_max is None:
+        kappa_max = 2.5 if model == "tric" else 1.0  # tric: drive alpha_ref into its bounds (BASELINE config 4)
+    b0, b1 = start // BLOCK, (start + B + BLOCK - 1) // BLOCK
+    blocks = [_block(model, seed, k, kappa_max, path_frac, p) for k in range(b0, b1)]
+    lo = start - b0 * BLOCK
+    cat = {k: np.concatenate([bl[k] for bl in blocks], axis=-1)[..., lo:lo + B] for k in blocks[0]} if blocks else \
+        _block(model, seed, 0, kappa_max, path_frac, p)
     f32 = lambda x: np.ascontiguousarray(x, dtype=np.float32)  # noqa: E731
-    return dict(pose=f32(pose), vel=f32(vel), steer=f32(steer), carried=f32(carried), path=f32(path),
-                s=np.zeros(B, np.float32), is_path=is_path)
+    out = {k: f32(v) for k, v in cat.items() if k != "is_path"}
+    if not blocks:
+        out = {k: v[..., :0] for k, v in out.items()}
+    out["s"] = np.zeros(B, np.float32)
+    out["is_path"] = cat["is_path"][..., :B]
+    return out
 
 
 def arc_pose(path, i, s):

@@ -1,0 +1,69 @@
+"""Multi-process instance sharding on CPU (gloo, world_size 2): the contract bench.py uses on RCCL.
+
+Each rank owns a contiguous shard of the seeded fleet (sharding.shard_range + make_fleet(start=...)), steps
+its robots in closed loop, and the per-tick commands are all-gathered to every rank; the result must equal
+the single-process run of the whole fleet exactly (instances are independent: no data-path collective).
+The per-rank solver here is the CPU oracle, since the test runs without a GPU; the GPU path is the same code
+with BatchSolver in place of the oracle (bench.py).
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from nmpc_nav_control_amd.sharding import CommandGather, TimedRegion, mixed_counts, shard_range
+
+MODEL, N, TOTAL, TICKS = "diff", 10, 11, 3
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from helpers import oracle_closed_loop
+        lo, hi = shard_range(TOTAL, rank, world)
+        counts = [b - a for a, b in (shard_range(TOTAL, r, world) for r in range(world))]
+        log = []
+        with TimedRegion() as tr:
+            oracle_closed_loop(MODEL, N, hi - lo, TICKS, start=lo, u0_log=log)
+        gather = CommandGather(2, counts, torch.device("cpu"))
+        fleet = [gather([torch.from_numpy(u.T.astype(np.float32))]).numpy() for u in log]
+        if rank == 0:
+            np.savez(out, u0=np.stack(fleet), elapsed=tr.elapsed)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_shard_range_covers_fleet():
+    for total in (0, 1, 7, 4096, 65536):
+        for world in (1, 2, 3, 8):
+            rs = [shard_range(total, r, world) for r in range(world)]
+            assert rs[0][0] == 0 and rs[-1][1] == total
+            assert all(a[1] == b[0] for a, b in zip(rs, rs[1:]))
+            assert max(b - a for a, b in rs) - min(b - a for a, b in rs) <= 1
+    with pytest.raises(ValueError):
+        shard_range(10, 2, 2)
+    assert mixed_counts(8192, ["diff", "omni4", "tric"]) == [("diff", 2731), ("omni4", 2731), ("tric", 2730)]
+
+
+def test_gloo_world2_sharded_equals_single(tmp_path):
+    from helpers import oracle_closed_loop
+    out = str(tmp_path / "r0.npz")
+    mp.spawn(_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    got = np.load(out)
+    log = []
+    oracle_closed_loop(MODEL, N, TOTAL, TICKS, u0_log=log)
+    ref = np.stack([u.T.astype(np.float32) for u in log])
+    assert got["u0"].shape == ref.shape
+    assert np.array_equal(got["u0"], ref)
+    assert float(got["elapsed"]) > 0
