@@ -30,6 +30,9 @@ enum ModelId { kDiff = 0, kOmni4 = 1, kTric = 2 };
 
 struct Diff2 {
     static constexpr int ID = kDiff, NX = 7, NU = 2, NBX = 2, NBU = 2, NP = 2, NY = 9;
+    // rows >= NGV of the discrete Jacobian [B A] do not depend on the state or input (theta, wheel and
+    // ref rows are linear): they are computed once per launch (checked by tests/test_oracle.py)
+    static constexpr int NGV = 2;
     __host__ __device__ static constexpr int idxbx(int i) { return 5 + i; }
     __host__ __device__ static constexpr int idxbu(int i) { return i; }
 
@@ -84,6 +87,7 @@ struct Diff2 {
 
 struct Omni4 {
     static constexpr int ID = kOmni4, NX = 11, NU = 4, NBX = 4, NBU = 4, NP = 2, NY = 15;
+    static constexpr int NGV = 2;  // x, y rows vary; theta / wheel / ref rows are linear
     __host__ __device__ static constexpr int idxbx(int i) { return 7 + i; }
     __host__ __device__ static constexpr int idxbu(int i) { return i; }
 
@@ -144,6 +148,7 @@ struct Omni4 {
 
 struct Tric3 {
     static constexpr int ID = kTric, NX = 7, NU = 2, NBX = 2, NBU = 2, NP = 3, NY = 9;
+    static constexpr int NGV = 3;  // x, y, theta rows vary; v / alpha / ref rows are linear
     __host__ __device__ static constexpr int idxbx(int i) { return 5 + i; }
     __host__ __device__ static constexpr int idxbu(int i) { return i; }
 

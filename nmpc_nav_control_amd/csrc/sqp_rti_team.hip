@@ -1,48 +1,47 @@
 // sqp_rti_team.hip -- batched SQP-RTI step, one 16-lane team (one DPP row) per robot instance.
 //
-// Same algorithm as sqp_rti_lane.hip and oracle/nmpc_oracle.c (RK4 + forward sensitivities, Gauss-Newton
-// cost, box bounds, Mehrotra IPM with damped corrector and centring safeguard, square-root Riccati),
+// Same algorithm as oracle/nmpc_oracle.c (RK4 + forward sensitivities, Gauss-Newton cost, box bounds,
+// Mehrotra IPM with damped corrector and centring safeguard, Riccati recursion),
 // mapped MI355X-first:
 //   * four robots per wavefront; inside a team lane v owns QP variable v of every stage (v < NU: input,
-//     NU <= v < NU+NX: state), so the stage matrix M = diag(H+Sigma) + (L'[B A])'(L'[B A]) and its Cholesky
-//     factor are distributed one row per lane, and every cross-lane operand is a DPP row_newbcast
-//     (no LDS, no shuffles through memory);
-//   * vector reductions over the team (G * dz for the forward dynamics, mu, step bounds) are 4-step DPP
-//     butterflies;
-//   * the per-stage record of a team (stage matrix columns, iterate, slacks, multipliers, Riccati factor
-//     columns) lives in an instance-interleaved scratch array [stage][field][team][NV], so the four teams
-//     of a wave touch 4*NV*4 contiguous bytes per field; the whole working set of B=4096 diff robots at
-//     N=40 is ~140 MB and stays in the 256 MB Infinity Cache between passes;
-//   * the linearisation is stage-parallel: lane r integrates stages r, r+16, r+32, ...
-// The IPM iteration count is per team; a wave iterates until its four teams have converged (finished
-// teams take no further steps).
+//     NU <= v < NU+NX: state); cross-lane operands are DPP row_newbcast broadcasts, fused into the
+//     multiply-accumulates (v_fmac_f32_dpp / v_fmac_f64_dpp);
+//   * the stage factor is a square-root Riccati step, M = D + (L'[B A])'(L'[B A]) = chol, formed and factored
+//     in fp64 (MI355X runs fp64 FMAs at half the fp32 rate): near the solution the barrier weights of active
+//     bounds reach 1e12 and fp32 Schur complements cancel catastrophically. The factor is stored in fp32 and
+//     every solve with it runs in fp32 (u0 error <1e-5 against the fp64 oracle, DESIGN.md "Precision");
+//   * rows of [B A] that do not depend on the state (model trait NGV) live in registers for the whole launch;
+//     only the NGV varying rows are stored per stage;
+//   * each lane's per-stage record (slacks, multipliers, iterate, directions, factor row, Jacobian column) is
+//     RS contiguous floats at [team][stage][slot][RS]: one record = RS/4 dwordx4 loads, and every sweep
+//     prefetches the next stage's record while the current stage computes (the ~170 MB working set of 4096
+//     robots stays in the 256 MB Infinity Cache);
+//   * the linearisation is column-parallel: lane v integrates the nominal RK4 step and propagates column v of
+//     its sensitivity, and the initial (dynamics-feasible) iterate is simulated in the same forward pass.
+// The IPM iteration count is per team; a wave iterates until its four teams have converged (finished teams
+// skip their loads and stores).
 #include "nmpc_kernels.hpp"
 #include "team_dpp.hpp"
 
 namespace nmpc {
 
 template <class M>
-struct TeamLayout {
-    static constexpr int NX = M::NX, NU = M::NU, NV = NX + NU;
-    static constexpr int G = 0;  // NX fields: G[i][v] = (v < NU ? B : A)[i][v'] (column v of [B A])
-    static constexpr int BV = G + NX;  // b_k[i] in slot i
-    static constexpr int Z = BV + 1;   // QP iterate dz (du / dx)
-    static constexpr int GR = Z + 1;   // cost gradient
-    static constexpr int DZ = GR + 1;  // combined Newton direction
-    static constexpr int TL = DZ + 1, TU = TL + 1, LL = TU + 1, LU = LL + 1, LB = LU + 1, UB = LB + 1;
-    static constexpr int DZA = UB + 1;  // affine direction of the bounded variable
-    static constexpr int LR = DZA + 1;  // Luu^{-1} (g^u + B'p) (u lanes)
-    static constexpr int RU = LR + 1;   // u-stationarity residual (u lanes)
-    static constexpr int YR = RU + 1;   // unwrapped pose reference (slots 0..2, run mode)
-    static constexpr int LM = YR + 1;   // NU fields: row v of the stage factor, columns 0..NU-1
-    static constexpr int NF = LM + NU;
+struct TeamRec {
+    static constexpr int NX = M::NX, NU = M::NU, NV = NX + NU, NGV = M::NGV;
+    static constexpr int TL = 0, TU = 1, LL = 2, LU = 3;  // slacks / multipliers of the box bound (bounded slots)
+    static constexpr int Z = 4, LB = 5, UB = 6, DZA = 7;   // QP iterate, bounds relative to the SQP iterate, affine dir
+    static constexpr int DZ = 8, GR = 9, RU = 10, LR = 11; // combined dir, cost gradient, u-residual, Luu^-1 rhs
+    static constexpr int LM = 12;                          // NU floats: row v of the stage factor, input columns
+    static constexpr int GV = LM + NU;                     // NGV floats: varying rows of column v of [B A]
+    static constexpr int RS = (GV + NGV + 3) / 4 * 4;      // record floats (dwordx4 aligned)
+    static constexpr int NQ = RS / 4;
+    static_assert(NV <= 16, "a team holds at most 16 variables");
 };
 
 template <class M>
 size_t team_scratch_floats(int N, int stride)
 {
-    using Lay = TeamLayout<M>;
-    return (size_t)(N + 1) * Lay::NF * stride * Lay::NV + 64;
+    return (size_t)stride * (N + 1) * 16 * TeamRec<M>::RS + 64;
 }
 
 namespace {
@@ -59,12 +58,105 @@ __device__ __forceinline__ int xcomp(int xi)
     return -1;
 }
 
+// Column `col` (slot convention: col < NU input col, else state col - NU) of the RK4 map's sensitivity at
+// (x, u), propagated by one lane through the four stages, together with the nominal step xn.
+template <class M>
+__device__ __forceinline__ void rk4_column(const float* x, const float* u, const KParams& P, int col, float* xn,
+                                           float* g)
+{
+    constexpr int NX = M::NX, NU = M::NU;
+    const float h = P.dt;
+    float xs[NX], k[NX], acc[NX], s0[NX], s[NX], dacc[NX];
+#pragma unroll
+    for (int i = 0; i < NX; i++) {
+        xs[i] = x[i];
+        s0[i] = (col == NU + i) ? 1.0f : 0.0f;
+        s[i] = s0[i];
+    }
+    const float cst[3] = {0.5f, 0.5f, 1.0f};
+    const float wgt[4] = {1.0f, 2.0f, 2.0f, 1.0f};
+#pragma unroll
+    for (int st = 0; st < 4; st++) {
+        M::f(xs, u, P, k);
+        float S1[NX][1], D1[NX][1];
+#pragma unroll
+        for (int i = 0; i < NX; i++) S1[i][0] = s[i];
+        M::template jvp<1>(xs, S1, P, D1);  // Jx s (the input block of the models is [0; I] on the last NU rows)
+        float dk[NX];
+#pragma unroll
+        for (int i = 0; i < NX; i++) dk[i] = D1[i][0];
+#pragma unroll
+        for (int q = 0; q < NU; q++) dk[NX - NU + q] += (col == q) ? 1.0f : 0.0f;
+#pragma unroll
+        for (int i = 0; i < NX; i++) {
+            acc[i] = (st == 0) ? k[i] : acc[i] + wgt[st] * k[i];
+            dacc[i] = (st == 0) ? dk[i] : dacc[i] + wgt[st] * dk[i];
+        }
+        if (st < 3) {
+            const float ch = cst[st] * h;
+#pragma unroll
+            for (int i = 0; i < NX; i++) {
+                xs[i] = x[i] + ch * k[i];
+                s[i] = s0[i] + ch * dk[i];
+            }
+        }
+    }
+    const float h6 = h * (1.0f / 6.0f);
+#pragma unroll
+    for (int i = 0; i < NX; i++) {
+        xn[i] = x[i] + h6 * acc[i];
+        g[i] = s0[i] + h6 * dacc[i];
+    }
+}
+
+template <int NQ>
+__device__ __forceinline__ void rec_load(const float* p, float (&v)[NQ * 4])
+{
+    const float4* q = reinterpret_cast<const float4*>(p);
+#pragma unroll
+    for (int i = 0; i < NQ; i++) {
+        const float4 t = q[i];
+        v[4 * i + 0] = t.x;
+        v[4 * i + 1] = t.y;
+        v[4 * i + 2] = t.z;
+        v[4 * i + 3] = t.w;
+    }
+}
+
+template <int NQ>
+__device__ __forceinline__ void rec_store(float* p, const float (&v)[NQ * 4])
+{
+    float4* q = reinterpret_cast<float4*>(p);
+#pragma unroll
+    for (int i = 0; i < NQ; i++) q[i] = make_float4(v[4 * i + 0], v[4 * i + 1], v[4 * i + 2], v[4 * i + 3]);
+}
+
+// Newton directions of one bounded variable (lower slack tl / multiplier ll, upper tu / lu) for a step dz with
+// complementarity targets tgl, tgu:  dt = dz + r (primal),  l*dt + t*dl = tg - l*t  (linearised complementarity).
+struct BoundDir {
+    float dtl, dtu, dll, dlu;
+};
+__device__ __forceinline__ BoundDir bound_dir(float dz, float rl, float rr, float tl, float tu, float ll, float lu,
+                                              float itl, float itu, float tgl, float tgu)
+{
+    BoundDir d;
+    d.dtl = dz + rl;
+    d.dtu = -dz + rr;
+    d.dll = (tgl - ll * (tl + rl) - ll * dz) * itl;
+    d.dlu = (tgu - lu * (tu + rr) + lu * dz) * itu;
+    return d;
+}
+
+__device__ __forceinline__ float step_bound_r(float amax, float v, float dv)
+{
+    return (dv < 0.0f) ? fminf(amax, -v * frcp(dv)) : amax;
+}
+
 template <class M>
 __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int mode)
 {
-    using Lay = TeamLayout<M>;
-    constexpr int NX = M::NX, NU = M::NU, NV = Lay::NV, NF = Lay::NF;
-    static_assert(NV <= 16, "a team holds at most 16 variables");
+    using R = TeamRec<M>;
+    constexpr int NX = M::NX, NU = M::NU, NV = R::NV, NGV = R::NGV, RS = R::RS, NQ = R::NQ;
     const int gt = blockIdx.x * blockDim.x + threadIdx.x;
     const int team = gt >> 4;
     const int r = gt & 15;
@@ -72,23 +164,26 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
     const int N = P.N;
     const size_t S = (size_t)a.stride;  // resident state stride (capacity)
     const size_t Bn = (size_t)a.B;
-    const size_t T = (size_t)a.stride;  // teams in the scratch layout
     const int inst = team;
-    float* __restrict__ scr = a.scratch;
     const bool lv = r < NV;
     const bool is_u = r < NU;
     const bool is_x = lv && !is_u;
     const int xi = is_x ? r - NU : 0;
-    // bound of this lane's variable (every input is bounded; states on idxbx)
     const int cx = is_x ? xcomp<M>(xi) : -1;
-    const bool has_c_u = is_u;  // idxbu = all inputs in the three models
-    const bool has_c_x = cx >= 0;
-    const float c_lo = is_u ? P.lbu[r < 4 ? r : 0] : (has_c_x ? P.lbx[cx] : 0.0f);
-    const float c_hi = is_u ? P.ubu[r < 4 ? r : 0] : (has_c_x ? P.ubx[cx] : 0.0f);
+    const bool has_b = is_u || cx >= 0;  // bounded slot: every input (idxbu = all), states on idxbx
     const float sc = P.dt;
     const float h_stage = is_u ? sc * P.W[NX + r] : (is_x ? sc * P.W[xi] : 0.0f);
+    float lo_b = 0.0f, hi_b = 0.0f;
+#pragma unroll
+    for (int q = 0; q < NU; q++)
+        if (r == q) { lo_b = P.lbu[q]; hi_b = P.ubu[q]; }
+#pragma unroll
+    for (int c = 0; c < M::NBX; c++)
+        if (cx == c) { lo_b = P.lbx[c]; hi_b = P.ubx[c]; }
+    // this lane's record of stage k: tbase + k * 16 * RS
+    float* const tbase = a.scratch + ((size_t)team * (N + 1) * 16 + r) * RS;
+    constexpr int KS = 16 * RS;
 
-#define REC(k, f) scr[(((size_t)(k) * NF + (f)) * T + team) * NV + r]
 #define XB(k, j) a.xbar[((size_t)(k) * NX + (j)) * S + inst]
 #define UBAR(k, j) a.ubar[((size_t)(k) * NU + (j)) * S + inst]
 
@@ -98,8 +193,8 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
             for (int j = 0; j < NX; j++) XB(k, j) = 0.0f;
         for (int k = r; k < N; k += 16)
             for (int j = 0; j < NU; j++) UBAR(k, j) = 0.0f;
+        __threadfence_block();
     }
-    __threadfence_block();
 
     // ---- x0 (every lane keeps the full vector) ----------------------------------------------------------
     float x0[NX];
@@ -119,194 +214,223 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
 #pragma unroll
         for (int j = 0; j < NX; j++) x0[j] = a.x0[(size_t)j * Bn + inst];
     }
-
-    // ---- references: unwrap + pad (run mode, NMPCNavControlDiff.cpp:104-118), terminal weight ----------
-    bool hack_eq = false;
-    if (mode == kModeRun) {
-        const int len = a.traj_len ? a.traj_len[inst] : N + 1;
-        float prev = pose_th, px = 0.0f, py = 0.0f, pxo = 0.0f, pyo = 0.0f, pto = 0.0f;
-        for (int k = 0; k <= N; k++) {
-            if (k < len) {
-                px = a.traj[((size_t)k * 3 + 0) * Bn + inst];
-                py = a.traj[((size_t)k * 3 + 1) * Bn + inst];
-                float th = a.traj[((size_t)k * 3 + 2) * Bn + inst];
-                const float d = th - prev;
-                if (d > kPi) th -= 2.0f * kPi;
-                else if (d < -kPi) th += 2.0f * kPi;
-                prev = th;
-            }
-            if (r < 3) REC(k, Lay::YR) = (r == 0) ? px : (r == 1 ? py : prev);
-            if (k == N - 1) { pxo = px; pyo = py; pto = prev; }
-        }
-        hack_eq = (px == pxo) && (py == pyo) && (prev == pto);  // NMPCNavControlDiff.cpp:127-139
-    }
-    // per-lane terminal weight of this lane's state
-    float we_lane = 0.0f;
-    if (is_x) {
-        we_lane = a.We ? a.We[(size_t)xi * Bn + inst] : P.We[xi];
-        if (mode == kModeRun && P.terminal_hack && xi < 3) we_lane = (hack_eq ? 100.0f : 1.0f) * P.W[xi];
-    }
-    // yref(k, j) for the stage-parallel linearisation
-    auto yref = [&](int k, int j) -> float {
-        if (mode == kModeRun) {
-            if (j >= 3) return 0.0f;
-            return scr[(((size_t)k * NF + Lay::YR) * T + team) * NV + j];
-        }
-        return (j < a.ny_in) ? a.yref[((size_t)k * a.ny_in + j) * Bn + inst] : 0.0f;
-    };
-    // every lane needs the terminal weights of all states for the stage-parallel gradient
-    float we_all[NX];
+    float x0_lane = 0.0f;
 #pragma unroll
-    for (int i = 0; i < NX; i++) we_all[i] = bc16(we_lane, NU + i);
-    __threadfence_block();  // YR slots written above are read by other lanes of the team (same wave) below
+    for (int j = 0; j < NX; j++)
+        if (xi == j) x0_lane = x0[j];
 
-    // ---- P0a: stage-parallel linearisation, gradient, bounds -------------------------------------------
-    for (int k = r; k <= N; k += 16) {
+    // terminal weight of this lane's state (solve mode: caller's W_e; run mode: constructor W_e + diff hack)
+    float we_lane = 0.0f;
+    if (is_x) we_lane = (mode != kModeRun && a.We) ? a.We[(size_t)xi * Bn + inst] : P.We[xi];
+
+    // ---- P0: linearisation (lane v: nominal step + column v), gradient, bounds, feasible initial iterate --
+    const int len = (mode == kModeRun) ? (a.traj_len ? a.traj_len[inst] : N + 1) : 0;
+    float ref_x = 0.0f, ref_y = 0.0f, ref_t = pose_th, prv_x = 0.0f, prv_y = 0.0f, prv_t = 0.0f;
+    float gcol[NX];  // column v of [B A]; rows >= NGV are constant for the launch
+#pragma unroll
+    for (int i = 0; i < NX; i++) gcol[i] = 0.0f;
+    float dx = is_x ? x0_lane - XB(0, xi) : 0.0f;  // this lane's state delta at the current stage
+    for (int k = 0; k <= N; k++) {
         float xb[NX], ub[NU];
 #pragma unroll
         for (int j = 0; j < NX; j++) xb[j] = XB(k, j);
 #pragma unroll
         for (int j = 0; j < NU; j++) ub[j] = (k < N) ? UBAR(k, j) : 0.0f;
-        float* rec = scr + ((size_t)k * NF * T + team) * NV;  // slot base of stage k
-        auto put = [&](int f, int slot, float v) { rec[(size_t)f * T * NV + slot] = v; };
-        if (k < N) {
-            float xn[NX], A[NX][NX], Bm[NX][NU];
-            rk4_sens<M>(xb, ub, P, xn, A, Bm);
-#pragma unroll
-            for (int i = 0; i < NX; i++) {
-#pragma unroll
-                for (int v = 0; v < NU; v++) put(Lay::G + i, v, Bm[i][v]);
-#pragma unroll
-                for (int j = 0; j < NX; j++) put(Lay::G + i, NU + j, A[i][j]);
-                put(Lay::BV, i, xn[i] - XB(k + 1, i));
+        // stage reference of this lane: run mode unwraps + pads the pose refs (NMPCNavControlDiff.cpp:104-118),
+        // entries >= 3 of yref are left at zero
+        float yr = 0.0f;
+        if (mode == kModeRun) {
+            if (k < len) {
+                ref_x = a.traj[((size_t)k * 3 + 0) * Bn + inst];
+                ref_y = a.traj[((size_t)k * 3 + 1) * Bn + inst];
+                float th = a.traj[((size_t)k * 3 + 2) * Bn + inst];
+                const float d = th - ref_t;
+                if (d > kPi) th -= 2.0f * kPi;
+                else if (d < -kPi) th += 2.0f * kPi;
+                ref_t = th;
             }
-#pragma unroll
-            for (int v = 0; v < NU; v++) {
-                put(Lay::GR, v, sc * P.W[NX + v] * (ub[v] - yref(k, NX + v)));
-                put(Lay::LB, v, P.lbu[v] - ub[M::idxbu(v)]);
-                put(Lay::UB, v, P.ubu[v] - ub[M::idxbu(v)]);
-            }
+            if (k == N - 1) { prv_x = ref_x; prv_y = ref_y; prv_t = ref_t; }
+            yr = (is_x && xi == 0) ? ref_x : ((is_x && xi == 1) ? ref_y : ((is_x && xi == 2) ? ref_t : 0.0f));
+        } else {
+            const int j = is_u ? NX + r : xi;
+            yr = (lv && j < a.ny_in) ? a.yref[((size_t)k * a.ny_in + j) * Bn + inst] : 0.0f;
         }
-        if (k >= 1) {
+        float rec[RS];
 #pragma unroll
-            for (int j = 0; j < NX; j++) {
-                const float w = (k < N) ? sc * P.W[j] : we_all[j];
-                put(Lay::GR, NU + j, w * (xb[j] - yref(k, j)));
-            }
+        for (int f = 0; f < RS; f++) rec[f] = 0.0f;
+        float xn[NX], g[NX];
 #pragma unroll
-            for (int c = 0; c < M::NBX; c++) {
-                const int j = M::idxbx(c);
-                put(Lay::LB, NU + j, P.lbx[c] - xb[j]);
-                put(Lay::UB, NU + j, P.ubx[c] - xb[j]);
-            }
+        for (int i = 0; i < NX; i++) { xn[i] = 0.0f; g[i] = 0.0f; }
+        if (k < N) rk4_column<M>(xb, ub, P, lv ? r : NU, xn, g);
+        if (k == 0) {
+#pragma unroll
+            for (int i = NGV; i < NX; i++) gcol[i] = lv ? g[i] : 0.0f;
         }
-    }
-    __threadfence_block();  // stage records written by other lanes of the team (same wave)
-
-    // ---- P0b: dynamics-feasible initial iterate, slacks and multipliers (forward) -----------------------
-    float dxv = is_x ? x0[xi] - XB(0, xi) : 0.0f;  // this lane's state delta at the current stage
-    for (int k = 0; k <= N; k++) {
-        const bool valid = is_u ? (k < N) : (is_x && k >= 1);
-        const float z = is_u ? 0.0f : dxv;
-        if (lv) REC(k, Lay::Z) = z;
-        if (valid && (has_c_u || has_c_x)) {
-            const float lb = REC(k, Lay::LB), ubd = REC(k, Lay::UB);
+        const bool vu = is_u && k < N, vx = is_x && k >= 1;
+        const bool valid = vu || vx;
+        float zbar = 0.0f;
+#pragma unroll
+        for (int j = 0; j < NU; j++)
+            if (r == j) zbar = ub[j];
+#pragma unroll
+        for (int j = 0; j < NX; j++)
+            if (is_x && xi == j) zbar = xb[j];
+        // gradient of the Gauss-Newton cost (stage weights scaled by dt, terminal weight unscaled)
+        if (vu) rec[R::GR] = sc * P.W[NX + r] * (zbar - yr);
+        if (vx) {
+            float w = sc * P.W[xi];
+            if (k == N) {
+                w = we_lane;
+                if (mode == kModeRun && P.terminal_hack && xi < 3) {  // NMPCNavControlDiff.cpp:127-139
+                    const bool eq = (ref_x == prv_x) && (ref_y == prv_y) && (ref_t == prv_t);
+                    w = (eq ? 100.0f : 1.0f) * P.W[xi];
+                    we_lane = w;
+                }
+            }
+            rec[R::GR] = w * (zbar - yr);
+        }
+        // iterate, bounds, slacks, multipliers
+        const float z = vx ? dx : 0.0f;
+        rec[R::Z] = z;
+        rec[R::TL] = 1.0f;
+        rec[R::TU] = 1.0f;
+        if (valid && has_b) {
+            const float lb = lo_b - zbar, ubd = hi_b - zbar;
             const float tl = fmaxf(z - lb, P.thr0), tu = fmaxf(ubd - z, P.thr0);
-            REC(k, Lay::TL) = tl;
-            REC(k, Lay::TU) = tu;
-            REC(k, Lay::LL) = P.mu0 / tl;
-            REC(k, Lay::LU) = P.mu0 / tu;
+            rec[R::LB] = lb;
+            rec[R::UB] = ubd;
+            rec[R::TL] = tl;
+            rec[R::TU] = tu;
+            rec[R::LL] = P.mu0 / tl;
+            rec[R::LU] = P.mu0 / tu;
         }
+#pragma unroll
+        for (int i = 0; i < NGV; i++) rec[R::GV + i] = (k < N && lv) ? g[i] : 0.0f;
+        if (lv) rec_store<NQ>(tbase + (size_t)k * KS, rec);
+        // dynamics-feasible initial states: dx_{k+1} = A dx_k + b_k (inputs start at du = 0, dx_0 = x0 - xbar_0)
         if (k < N) {
-            // dx_{k+1} = A dx_k + b_k = sum over state lanes of column(A) * dx + b
-            float nxt = 0.0f;
+            const float dzd = is_x ? dx : 0.0f;
+            float nxt = 0.0f, bk = 0.0f;
 #pragma unroll
             for (int i = 0; i < NX; i++) {
-                const float g = lv ? REC(k, Lay::G + i) : 0.0f;
-                const float s = row_sum16(is_x ? g * z : 0.0f);
-                if (i == xi) nxt = s;
+                const float s = row_sum16(lv ? g[i] * dzd : 0.0f);
+                if (xi == i) {
+                    nxt = s;
+                    bk = xn[i] - XB(k + 1, i);
+                }
             }
-            const float b = is_x ? scr[(((size_t)k * NF + Lay::BV) * T + team) * NV + xi] : 0.0f;
-            dxv = nxt + b;
+            dx = is_x ? nxt + bk : 0.0f;
         }
     }
-    int m = 0;
+    // row xi of the constant rows of [B A] (lane NU+xi, xi >= NGV): grow[v] = G[xi][v], from lane v's column
+    float grow[NV];
 #pragma unroll
-    for (int c = 0; c < NU; c++) m += N;
-    m += N * M::NBX;
+    for (int v = 0; v < NV; v++) {
+        float s = 0.0f;
+#pragma unroll
+        for (int i = NGV; i < NX; i++) {
+            const float t = bc16(gcol[i], v);
+            if (is_x && xi == i) s = t;
+        }
+        grow[v] = s;
+    }
+    double gcol64[NX];
+#pragma unroll
+    for (int i = 0; i < NX; i++) gcol64[i] = (double)gcol[i];
+
+    const int m = N * NU + N * M::NBX;
     const float inv_m2 = 0.5f / (float)m;
+
+    // dx_{k+1} (lane NU+i) = sum_v G_k[i][v] dz_v: NGV row sums over the stored columns + the constant rows
+    auto dyn = [&](const float (&rc)[RS], float dzv) -> float {
+        float nxt = 0.0f;
+#pragma unroll
+        for (int i = 0; i < NGV; i++) {
+            const float s = row_sum16(lv ? rc[R::GV + i] * dzv : 0.0f);
+            if (xi == i) nxt = s;
+        }
+        float cr = 0.0f;
+#pragma unroll
+        for (int v = 0; v < NV; v++) cr = fmac_bc(cr, dzv, grow[v], v);
+        return (xi >= NGV) ? cr : nxt;
+    };
 
     // ---- interior-point iterations ----------------------------------------------------------------------
     int status = 0, it_done = 0;
     bool done = false;
     float exit_res[3] = {0.0f, 0.0f, 0.0f};
     float alpha = 0.0f, sigma_mu = 0.0f, eta = 0.0f;
-    const bool has_c_any = has_c_u || has_c_x;
     for (int it = 0;; it++) {
-        // P1 (backward): update, residuals, adjoint, square-root Riccati factorisation, predictor rhs
-        float Lrow[NV];  // this lane's row of the previous stage factor (state lanes carry L_{k+1})
+        // P1 (backward): apply the previous step, residuals, adjoint, fp64 square-root Riccati factorisation,
+        // predictor rhs
+        double Lrow[NV];  // row r of the factor of stage k+1 (state lanes carry the rows of L_{k+1})
         float pv = 0.0f, piv = 0.0f;
         float res_stat = 0.0f, res_ineq = 0.0f, sum_c = 0.0f, stat_scale = 1.0f, nanf_ = 0.0f;
         bool fail = false;
-#pragma unroll
-        for (int j = 0; j < NV; j++) Lrow[j] = 0.0f;
+        const bool act = lv && !done;
         const float a_upd = (it > 0 && !done) ? alpha : 0.0f;
+        float nx_rec[RS];
+#pragma unroll
+        for (int f = 0; f < RS; f++) nx_rec[f] = 0.0f;
+        if (act) rec_load<NQ>(tbase + (size_t)N * KS, nx_rec);
         for (int k = N; k >= 0; k--) {
+            float rc[RS];
+#pragma unroll
+            for (int f = 0; f < RS; f++) rc[f] = nx_rec[f];
+            if (act && k > 0) rec_load<NQ>(tbase + (size_t)(k - 1) * KS, nx_rec);
             const bool vu = is_u && k < N;
             const bool vx = is_x && k >= 1;
             const bool valid = vu || vx;
-            float z = lv ? REC(k, Lay::Z) : 0.0f;
-            const float g = valid ? REC(k, Lay::GR) : 0.0f;
-            float lamdiff = 0.0f, sig = 0.0f, gh = 0.0f;
-            if (valid && has_c_any) {
-                const float lb = REC(k, Lay::LB), ubd = REC(k, Lay::UB);
-                float tl = REC(k, Lay::TL), tu = REC(k, Lay::TU), ll = REC(k, Lay::LL), lu = REC(k, Lay::LU);
-                if (a_upd > 0.0f) {
-                    const float dz = REC(k, Lay::DZ), dza = REC(k, Lay::DZA);
+            const bool bnd = valid && has_b;
+            float z = rc[R::Z];
+            float tl = rc[R::TL], tu = rc[R::TU], ll = rc[R::LL], lu = rc[R::LU];
+            const float lb = rc[R::LB], ubd = rc[R::UB];
+            if (a_upd > 0.0f) {
+                const float dz = rc[R::DZ];
+                if (bnd) {
                     const float rl = z - lb - tl, rr = ubd - z - tu;
-                    const float dtla = dza + rl, dtua = -dza + rr;
-                    const float dlla = (-ll * (tl + rl) - ll * dza) / tl;
-                    const float dlua = (-lu * (tu + rr) + lu * dza) / tu;
-                    const float tgl = sigma_mu - eta * dlla * dtla, tgu = sigma_mu - eta * dlua * dtua;
-                    const float dtl = dz + rl, dtu = -dz + rr;
-                    const float dll = (tgl - ll * (tl + rl) - ll * dz) / tl;
-                    const float dlu = (tgu - lu * (tu + rr) + lu * dz) / tu;
-                    tl += a_upd * dtl;
-                    tu += a_upd * dtu;
-                    ll += a_upd * dll;
-                    lu += a_upd * dlu;
-                    REC(k, Lay::TL) = tl;
-                    REC(k, Lay::TU) = tu;
-                    REC(k, Lay::LL) = ll;
-                    REC(k, Lay::LU) = lu;
+                    const float itl = frcp(tl), itu = frcp(tu);
+                    const BoundDir da = bound_dir(rc[R::DZA], rl, rr, tl, tu, ll, lu, itl, itu, 0.0f, 0.0f);
+                    const float tgl = sigma_mu - eta * da.dll * da.dtl, tgu = sigma_mu - eta * da.dlu * da.dtu;
+                    const BoundDir d = bound_dir(dz, rl, rr, tl, tu, ll, lu, itl, itu, tgl, tgu);
+                    tl += a_upd * d.dtl;
+                    tu += a_upd * d.dtu;
+                    ll += a_upd * d.dll;
+                    lu += a_upd * d.dlu;
                 }
-                const float zn = (a_upd > 0.0f) ? z + a_upd * REC(k, Lay::DZ) : z;
-                const float rl = zn - lb - tl, rr = ubd - zn - tu;
+                if (valid) z += a_upd * dz;
+                rc[R::Z] = z;
+                rc[R::TL] = tl;
+                rc[R::TU] = tu;
+                rc[R::LL] = ll;
+                rc[R::LU] = lu;
+            }
+            float lamdiff = 0.0f, sig = 0.0f, gh = 0.0f;
+            if (bnd) {
+                const float rl = z - lb - tl, rr = ubd - z - tu;
+                const float itl = frcp(tl), itu = frcp(tu);
                 res_ineq = nan_max(res_ineq, fmaxf(fabsf(rl), fabsf(rr)));
                 sum_c += ll * tl + lu * tu;
                 lamdiff = ll - lu;
-                sig = ll / tl + lu / tu;
-                gh = (ll * rl) / tl + ll - (lu * rr) / tu - lu;
+                sig = ll * itl + lu * itu;
+                gh = ll * rl * itl + ll - lu * rr * itu - lu;
             }
-            if (a_upd > 0.0f && valid) {
-                z += a_upd * REC(k, Lay::DZ);
-                REC(k, Lay::Z) = z;
-            }
-            // column of [B A] of this lane (stage k < N)
+            // column v of [B A] of this lane (stage k < N)
             float Gc[NX];
 #pragma unroll
-            for (int i = 0; i < NX; i++) Gc[i] = (k < N && lv) ? REC(k, Lay::G + i) : 0.0f;
+            for (int i = 0; i < NX; i++) Gc[i] = (i < NGV) ? rc[R::GV + (i < NGV ? i : 0)] : gcol[i];
             // adjoint: c_v = sum_l G[l][v] pi_{k+1}[l]
             float cpi = 0.0f;
             if (k < N) {
 #pragma unroll
-                for (int l = 0; l < NX; l++) cpi += Gc[l] * bc16(piv, NU + l);
+                for (int l = 0; l < NX; l++) cpi = fmac_bc(cpi, piv, Gc[l], NU + l);
             }
             const float hz = ((k < N) ? h_stage : we_lane) * z;
+            const float g = rc[R::GR];
             const float base = hz + g - lamdiff + cpi;
             float ghat = gh;
             if (vu) {
-                REC(k, Lay::RU) = base;
+                rc[R::RU] = base;
                 res_stat = nan_max(res_stat, fabsf(base));
                 stat_scale = fmaxf(stat_scale, fmaxf(fabsf(cpi), fmaxf(fabsf(g), fabsf(lamdiff))));
                 ghat += base;
@@ -315,80 +439,70 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
             if (!valid) ghat = 0.0f;
             if (ghat != ghat || sig != sig) nanf_ = 1.0f;
             if (k == N) {
+                // terminal: P_N = diag(W_e + Sigma) on the state lanes
+                const double d = is_x ? sqrt((double)fmaxf(we_lane + sig, 0.0f)) : 0.0;
 #pragma unroll
-                for (int j = 0; j < NV; j++) Lrow[j] = 0.0f;
-                if (is_x) {
-#pragma unroll
-                    for (int j = 0; j < NX; j++)
-                        if (j == xi) Lrow[NU + j] = sqrtf(fmaxf(we_lane + sig, 0.0f));
-                }
+                for (int j = 0; j < NV; j++) Lrow[j] = (is_x && j == r) ? d : 0.0;
                 pv = is_x ? ghat : 0.0f;
             } else {
-                const bool full = k >= 1;  // stage 0 has no state variables (x0 fixed)
-                // LBA column v = L_{k+1}' G[:, v]; L[l][i] lives in lane NU+l at Lrow[NU+i]
-                float lba[NX];
+                double Gd[NX];
+#pragma unroll
+                for (int l = 0; l < NX; l++) Gd[l] = (l < NGV) ? (double)Gc[l] : gcol64[l];
+                // LBA column v = L_{k+1}' G[:, v]; L[l][i] sits in lane NU+l at Lrow[NU+i]
+                double lba[NX];
 #pragma unroll
                 for (int i = 0; i < NX; i++) {
-                    float s = 0.0f;
+                    double s = 0.0;
 #pragma unroll
-                    for (int l = i; l < NX; l++) s += bc16(Lrow[NU + i], NU + l) * Gc[l];
+                    for (int l = i; l < NX; l++) s = fmac_bc64(s, Lrow[NU + i], Gd[l], NU + l);
                     lba[i] = s;
                 }
-                // this lane's row of M = D + LBA' LBA
-                const float dg = (valid ? h_stage + sig : 1.0f);
-                float Mr[NV];
-#pragma unroll
-                for (int b = 0; b < NV; b++) {
-                    float s = (b == r) ? dg : 0.0f;
-#pragma unroll
-                    for (int i = 0; i < NX; i++) s += lba[i] * bc16(lba[i], b);
-                    Mr[b] = s;
-                }
-                // Cholesky, row-distributed: Lr[j] = row r of the factor
-                float Lr[NV];
-#pragma unroll
-                for (int j = 0; j < NV; j++) Lr[j] = 0.0f;
+                // row r of M = D + LBA' LBA, factored column by column (row-distributed Cholesky, fp64)
+                const double dg = valid ? (double)h_stage + (double)sig : 1.0;
+                double Lr[NV];
 #pragma unroll
                 for (int j = 0; j < NV; j++) {
-                    if (!full && j >= NU) break;
-                    float s = Mr[j];
+                    double mj = (r == j) ? dg : 0.0;
 #pragma unroll
-                    for (int q = 0; q < j; q++) s -= Lr[q] * bc16(Lr[q], j);
-                    const float pivot = bc16(s, j);
-                    float d;
-                    bool zero_col = false;
+                    for (int i = 0; i < NX; i++) mj = fmac_bc64(mj, lba[i], lba[i], j);
+                    double s = mj;
+#pragma unroll
+                    for (int q = 0; q < j; q++) s = fnmac_bc64(s, Lr[q], Lr[q], j);
+                    const double pivot = bc64(s, j);
+                    double rd;
                     if (j < NU) {
-                        if (!(pivot > 0.0f)) fail = true;
-                        d = sqrtf(fmaxf(pivot, 1e-30f));
+                        if (!(pivot > 0.0)) fail = true;
+                        rd = drsq(fmax(pivot, 1e-300));
                     } else {
-                        const float mjj = bc16(Mr[j], j);
-                        zero_col = !(pivot > 1e-10f * (1.0f + fabsf(mjj)));
-                        d = zero_col ? 0.0f : sqrtf(pivot);
+                        const double mjj = bc64(mj, j);
+                        rd = (pivot > 1e-10 * (1.0 + fabs(mjj))) ? drsq(pivot) : 0.0;  // PSD state block
                     }
-                    if (r == j) Lr[j] = d;
-                    else if (r > j) Lr[j] = zero_col ? 0.0f : s / d;
+                    Lr[j] = (r == j) ? pivot * rd : ((r > j) ? s * rd : 0.0);
                 }
-                if (lv) {
+                float Lm[NU];
 #pragma unroll
-                    for (int q = 0; q < NU; q++) REC(k, Lay::LM + q) = Lr[q];
+                for (int q = 0; q < NU; q++) {
+                    Lm[q] = (float)Lr[q];
+                    rc[R::LM + q] = Lm[q];
                 }
-                // rhs: w = g^ + G' p_{k+1}; forward substitution over the input block
+                // rhs: w = g^ + G' p_{k+1}; forward substitution over the input block (fp32)
                 float y = ghat;
 #pragma unroll
-                for (int l = 0; l < NX; l++) y += Gc[l] * bc16(pv, NU + l);
+                for (int l = 0; l < NX; l++) y = fmac_bc(y, pv, Gc[l], NU + l);
                 float my_lr = 0.0f;
 #pragma unroll
                 for (int j = 0; j < NU; j++) {
-                    const float lrj = bc16(y / Lr[j], j);  // valid in lane j (diagonal)
+                    const float lrj = bc16(y * frcp(Lm[j]), j);  // (y_j / L_jj) from lane j
                     if (r == j) my_lr = lrj;
-                    if (r > j) y -= Lr[j] * lrj;
+                    y -= Lm[j] * lrj;
                 }
-                if (is_u) REC(k, Lay::LR) = my_lr;
+                rc[R::LR] = my_lr;
                 pv = is_x ? y : 0.0f;
 #pragma unroll
                 for (int j = 0; j < NV; j++) Lrow[j] = Lr[j];
             }
             piv = pi_new;
+            if (act) rec_store<NQ>(tbase + (size_t)k * KS, rc);
         }
         // team reductions
         sum_c = row_sum16(lv ? sum_c : 0.0f);
@@ -396,6 +510,7 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
         res_stat = row_max16(lv ? res_stat : 0.0f);
         stat_scale = row_max16(stat_scale);
         nanf_ = row_max16(nanf_);
+        const float failf = row_max16(fail ? 1.0f : 0.0f);
         const float mu = sum_c * inv_m2;
         if (!done) {
             exit_res[0] = res_stat;
@@ -405,7 +520,7 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
             if (nanf_ > 0.0f || mu != mu) {
                 status = 1;
                 stop = true;
-            } else if (fail) {
+            } else if (failf > 0.0f) {
                 status = (mu <= kBreakdownMuT && res_ineq <= P.tol_ineq * 10.0f) ? 0 : 4;
                 stop = true;
             } else {
@@ -419,31 +534,42 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
             }
         }
         if (__all(done)) break;
+        const bool act2 = lv && !done;
 
-        // P2 (forward): affine direction, maximal step, mu_aff polynomial
-        float s1 = 0.0f, s2 = 0.0f, amax = 1e30f;
-        {
-            float dx = 0.0f;
+        // forward sweep: du from the stored factor, dz, bounded-variable directions, next-stage dx.
+        // pass 0: affine direction (stores DZA; s1, s2 of the mu_aff polynomial); pass > 0: combined (stores DZ)
+        auto forward = [&](int pass, float& amax, float& s1, float& s2) {
+            float dxs = 0.0f;
+            amax = 1e30f;
+            s1 = 0.0f;
+            s2 = 0.0f;
+            float nr[RS];
+#pragma unroll
+            for (int f = 0; f < RS; f++) nr[f] = 0.0f;
+            if (act2) rec_load<NQ>(tbase, nr);
             for (int k = 0; k <= N; k++) {
+                float rc[RS];
+#pragma unroll
+                for (int f = 0; f < RS; f++) rc[f] = nr[f];
+                if (act2 && k < N) rec_load<NQ>(tbase + (size_t)(k + 1) * KS, nr);
                 const bool vu = is_u && k < N;
                 const bool vx = is_x && k >= 1;
                 const bool valid = vu || vx;
-                float Lr[NU];
-#pragma unroll
-                for (int q = 0; q < NU; q++) Lr[q] = (k < N && lv) ? REC(k, Lay::LM + q) : 0.0f;
                 float du_all[NU];
+#pragma unroll
+                for (int q = 0; q < NU; q++) du_all[q] = 0.0f;
                 if (k < N) {
-                    const float lr = is_u ? REC(k, Lay::LR) : 0.0f;
                     float w[NU];
 #pragma unroll
-                    for (int q = 0; q < NU; q++) w[q] = bc16(lr, q) + row_sum16(is_x ? Lr[q] * dx : 0.0f);
+                    for (int q = 0; q < NU; q++)
+                        w[q] = bc16(rc[R::LR], q) + ((k > 0) ? row_sum16(is_x ? rc[R::LM + q] * dxs : 0.0f) : 0.0f);
 #pragma unroll
                     for (int qq = 0; qq < NU; qq++) {
                         const int q = NU - 1 - qq;
                         float s = w[q];
 #pragma unroll
-                        for (int j = q + 1; j < NU; j++) s -= bc16(Lr[q], j) * du_all[j];
-                        du_all[q] = s / bc16(Lr[q], q);
+                        for (int j = q + 1; j < NU; j++) s -= bc16(rc[R::LM + q], j) * du_all[j];
+                        du_all[q] = s * frcp(bc16(rc[R::LM + q], q));
                     }
 #pragma unroll
                     for (int q = 0; q < NU; q++) du_all[q] = -du_all[q];
@@ -452,35 +578,84 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
 #pragma unroll
                 for (int q = 0; q < NU; q++)
                     if (r == q) dz = du_all[q];
-                if (is_x) dz = (k >= 1) ? dx : 0.0f;
-                if (valid && has_c_any) {
-                    const float z = REC(k, Lay::Z);
-                    const float lb = REC(k, Lay::LB), ubd = REC(k, Lay::UB);
-                    const float tl = REC(k, Lay::TL), tu = REC(k, Lay::TU), ll = REC(k, Lay::LL), lu = REC(k, Lay::LU);
-                    const float rl = z - lb - tl, rr = ubd - z - tu;
-                    const float dtl = dz + rl, dtu = -dz + rr;
-                    const float dll = (-ll * (tl + rl) - ll * dz) / tl;
-                    const float dlu = (-lu * (tu + rr) + lu * dz) / tu;
-                    amax = step_bound(amax, tl, dtl);
-                    amax = step_bound(amax, tu, dtu);
-                    amax = step_bound(amax, ll, dll);
-                    amax = step_bound(amax, lu, dlu);
-                    s1 += ll * dtl + tl * dll + lu * dtu + tu * dlu;
-                    s2 += dll * dtl + dlu * dtu;
-                    REC(k, Lay::DZA) = dz;
-                }
-                if (k < N) {
-                    float nxt = 0.0f;
-#pragma unroll
-                    for (int i = 0; i < NX; i++) {
-                        const float g = lv ? REC(k, Lay::G + i) : 0.0f;
-                        const float s = row_sum16(lv ? g * dz : 0.0f);
-                        if (i == xi) nxt = s;
+                if (is_x) dz = (k >= 1) ? dxs : 0.0f;
+                if (valid && has_b) {
+                    const float z = rc[R::Z];
+                    const float tl = rc[R::TL], tu = rc[R::TU], ll = rc[R::LL], lu = rc[R::LU];
+                    const float rl = z - rc[R::LB] - tl, rr = rc[R::UB] - z - tu;
+                    const float itl = frcp(tl), itu = frcp(tu);
+                    float tgl = 0.0f, tgu = 0.0f;
+                    if (pass > 0) {
+                        const BoundDir da = bound_dir(rc[R::DZA], rl, rr, tl, tu, ll, lu, itl, itu, 0.0f, 0.0f);
+                        tgl = sigma_mu - eta * da.dll * da.dtl;
+                        tgu = sigma_mu - eta * da.dlu * da.dtu;
                     }
-                    dx = nxt;
+                    const BoundDir d = bound_dir(dz, rl, rr, tl, tu, ll, lu, itl, itu, tgl, tgu);
+                    amax = step_bound_r(amax, tl, d.dtl);
+                    amax = step_bound_r(amax, tu, d.dtu);
+                    amax = step_bound_r(amax, ll, d.dll);
+                    amax = step_bound_r(amax, lu, d.dlu);
+                    if (pass == 0) {
+                        s1 += ll * d.dtl + tl * d.dll + lu * d.dtu + tu * d.dlu;
+                        s2 += d.dll * d.dtl + d.dlu * d.dtu;
+                    }
+                }
+                if (act2 && valid) tbase[(size_t)k * KS + (pass == 0 ? R::DZA : R::DZ)] = dz;
+                if (k < N) dxs = dyn(rc, valid ? dz : 0.0f);
+            }
+        };
+
+        // corrector rhs through the stored factorisation (backward)
+        auto corrector_rhs = [&]() {
+            float pvc = 0.0f;
+            float nr[RS];
+#pragma unroll
+            for (int f = 0; f < RS; f++) nr[f] = 0.0f;
+            if (act2) rec_load<NQ>(tbase + (size_t)N * KS, nr);
+            for (int k = N; k >= 0; k--) {
+                float rc[RS];
+#pragma unroll
+                for (int f = 0; f < RS; f++) rc[f] = nr[f];
+                if (act2 && k > 0) rec_load<NQ>(tbase + (size_t)(k - 1) * KS, nr);
+                const bool vu = is_u && k < N;
+                const bool vx = is_x && k >= 1;
+                const bool valid = vu || vx;
+                float ghat = 0.0f;
+                if (valid && has_b) {
+                    const float z = rc[R::Z];
+                    const float tl = rc[R::TL], tu = rc[R::TU], ll = rc[R::LL], lu = rc[R::LU];
+                    const float rl = z - rc[R::LB] - tl, rr = rc[R::UB] - z - tu;
+                    const float itl = frcp(tl), itu = frcp(tu);
+                    const BoundDir da = bound_dir(rc[R::DZA], rl, rr, tl, tu, ll, lu, itl, itu, 0.0f, 0.0f);
+                    const float tgl = sigma_mu - eta * da.dll * da.dtl, tgu = sigma_mu - eta * da.dlu * da.dtu;
+                    ghat = -(tgl - ll * rl) * itl + ll + (tgu - lu * rr) * itu - lu;
+                }
+                if (vu) ghat += rc[R::RU];
+                if (k == N) {
+                    pvc = is_x ? ghat : 0.0f;
+                } else {
+                    float y = ghat;
+#pragma unroll
+                    for (int l = 0; l < NX; l++) {
+                        const float gl = (l < NGV) ? rc[R::GV + (l < NGV ? l : 0)] : gcol[l];
+                        y = fmac_bc(y, pvc, gl, NU + l);
+                    }
+                    float my_lr = 0.0f;
+#pragma unroll
+                    for (int j = 0; j < NU; j++) {
+                        const float Lmj = rc[R::LM + j];
+                        const float lrj = bc16(y * frcp(Lmj), j);
+                        if (r == j) my_lr = lrj;
+                        y -= Lmj * lrj;
+                    }
+                    if (act2 && is_u) tbase[(size_t)k * KS + R::LR] = my_lr;
+                    pvc = is_x ? y : 0.0f;
                 }
             }
-        }
+        };
+
+        float amax, s1, s2;
+        forward(0, amax, s1, s2);
         s1 = row_sum16(lv ? s1 : 0.0f);
         s2 = row_sum16(lv ? s2 : 0.0f);
         amax = row_min16(lv ? amax : 1e30f);
@@ -492,128 +667,25 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
             sg = fmaxf(sg, 0.0f);
             sigma = fminf(sg * sg * sg, 1.0f);
         }
-
-        for (int pass = 1; pass <= 2; pass++) {
-            if (pass == 1) {
-                sigma_mu = sigma * mu;
-                eta = alpha_aff;
-            } else {
-                if (alpha >= 0.1f) break;
+        // pass 1: Mehrotra corrector; pass 2 (teams whose step stayed below 0.1): pure centring safeguard
+        sigma_mu = sigma * mu;
+        eta = alpha_aff;
+        corrector_rhs();
+        {
+            float am, t1, t2;
+            forward(1, am, t1, t2);
+            am = row_min16(lv ? am : 1e30f);
+            alpha = fminf(1.0f, P.tau * am);
+        }
+        if (!__all(done || alpha >= 0.1f)) {
+            if (!done && alpha < 0.1f) {
                 sigma_mu = fmaxf(sigma, 0.3f) * mu;
                 eta = 0.0f;
-            }
-            // P3 (backward): corrector rhs through the stored factorisation
-            {
-                float pvc = 0.0f;
-                for (int k = N; k >= 0; k--) {
-                    const bool vu = is_u && k < N;
-                    const bool vx = is_x && k >= 1;
-                    const bool valid = vu || vx;
-                    float ghat = 0.0f;
-                    if (valid && has_c_any) {
-                        const float z = REC(k, Lay::Z);
-                        const float lb = REC(k, Lay::LB), ubd = REC(k, Lay::UB);
-                        const float tl = REC(k, Lay::TL), tu = REC(k, Lay::TU), ll = REC(k, Lay::LL),
-                                    lu = REC(k, Lay::LU);
-                        const float dza = REC(k, Lay::DZA);
-                        const float rl = z - lb - tl, rr = ubd - z - tu;
-                        const float dtla = dza + rl, dtua = -dza + rr;
-                        const float dlla = (-ll * (tl + rl) - ll * dza) / tl;
-                        const float dlua = (-lu * (tu + rr) + lu * dza) / tu;
-                        const float tgl = sigma_mu - eta * dlla * dtla, tgu = sigma_mu - eta * dlua * dtua;
-                        ghat = -(tgl - ll * rl) / tl + ll + (tgu - lu * rr) / tu - lu;
-                    }
-                    if (vu) ghat += REC(k, Lay::RU);
-                    if (k == N) {
-                        pvc = is_x ? ghat : 0.0f;
-                    } else {
-                        float y = ghat;
-#pragma unroll
-                        for (int l = 0; l < NX; l++) {
-                            const float g = lv ? REC(k, Lay::G + l) : 0.0f;
-                            y += g * bc16(pvc, NU + l);
-                        }
-                        float Lr[NU];
-#pragma unroll
-                        for (int q = 0; q < NU; q++) Lr[q] = lv ? REC(k, Lay::LM + q) : 0.0f;
-                        float my_lr = 0.0f;
-#pragma unroll
-                        for (int j = 0; j < NU; j++) {
-                            const float lrj = bc16(y / Lr[j], j);
-                            if (r == j) my_lr = lrj;
-                            if (r > j) y -= Lr[j] * lrj;
-                        }
-                        if (is_u) REC(k, Lay::LR) = my_lr;
-                        pvc = is_x ? y : 0.0f;
-                    }
-                }
-            }
-            // P4 (forward): combined direction and its step length
-            {
-                float dx = 0.0f;
-                amax = 1e30f;
-                for (int k = 0; k <= N; k++) {
-                    const bool vu = is_u && k < N;
-                    const bool vx = is_x && k >= 1;
-                    const bool valid = vu || vx;
-                    float Lr[NU];
-#pragma unroll
-                    for (int q = 0; q < NU; q++) Lr[q] = (k < N && lv) ? REC(k, Lay::LM + q) : 0.0f;
-                    float du_all[NU];
-                    if (k < N) {
-                        const float lr = is_u ? REC(k, Lay::LR) : 0.0f;
-                        float w[NU];
-#pragma unroll
-                        for (int q = 0; q < NU; q++) w[q] = bc16(lr, q) + row_sum16(is_x ? Lr[q] * dx : 0.0f);
-#pragma unroll
-                        for (int qq = 0; qq < NU; qq++) {
-                            const int q = NU - 1 - qq;
-                            float s = w[q];
-#pragma unroll
-                            for (int j = q + 1; j < NU; j++) s -= bc16(Lr[q], j) * du_all[j];
-                            du_all[q] = s / bc16(Lr[q], q);
-                        }
-#pragma unroll
-                        for (int q = 0; q < NU; q++) du_all[q] = -du_all[q];
-                    }
-                    float dz = 0.0f;
-#pragma unroll
-                    for (int q = 0; q < NU; q++)
-                        if (r == q) dz = du_all[q];
-                    if (is_x) dz = (k >= 1) ? dx : 0.0f;
-                    if (valid) REC(k, Lay::DZ) = dz;
-                    if (valid && has_c_any) {
-                        const float z = REC(k, Lay::Z);
-                        const float lb = REC(k, Lay::LB), ubd = REC(k, Lay::UB);
-                        const float tl = REC(k, Lay::TL), tu = REC(k, Lay::TU), ll = REC(k, Lay::LL),
-                                    lu = REC(k, Lay::LU);
-                        const float dza = REC(k, Lay::DZA);
-                        const float rl = z - lb - tl, rr = ubd - z - tu;
-                        const float dtla = dza + rl, dtua = -dza + rr;
-                        const float dlla = (-ll * (tl + rl) - ll * dza) / tl;
-                        const float dlua = (-lu * (tu + rr) + lu * dza) / tu;
-                        const float tgl = sigma_mu - eta * dlla * dtla, tgu = sigma_mu - eta * dlua * dtua;
-                        const float dtl = dz + rl, dtu = -dz + rr;
-                        const float dll = (tgl - ll * (tl + rl) - ll * dz) / tl;
-                        const float dlu = (tgu - lu * (tu + rr) + lu * dz) / tu;
-                        amax = step_bound(amax, tl, dtl);
-                        amax = step_bound(amax, tu, dtu);
-                        amax = step_bound(amax, ll, dll);
-                        amax = step_bound(amax, lu, dlu);
-                    }
-                    if (k < N) {
-                        float nxt = 0.0f;
-#pragma unroll
-                        for (int i = 0; i < NX; i++) {
-                            const float g = lv ? REC(k, Lay::G + i) : 0.0f;
-                            const float s = row_sum16(lv ? g * dz : 0.0f);
-                            if (i == xi) nxt = s;
-                        }
-                        dx = nxt;
-                    }
-                }
-                amax = row_min16(lv ? amax : 1e30f);
-                alpha = fminf(1.0f, P.tau * amax);
+                corrector_rhs();
+                float am, t1, t2;
+                forward(2, am, t1, t2);
+                am = row_min16(lv ? am : 1e30f);
+                alpha = fminf(1.0f, P.tau * am);
             }
         }
     }
@@ -621,13 +693,14 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
     // ---- full SQP step + outputs ----------------------------------------------------------------------
     if (status == 0) {
         for (int k = 0; k <= N; k++) {
+            const float z = lv ? tbase[(size_t)k * KS + R::Z] : 0.0f;
             if (is_x) {
-                const float nv = (k == 0) ? x0[xi] : XB(k, xi) + REC(k, Lay::Z);
+                const float nv = (k == 0) ? x0_lane : XB(k, xi) + z;
                 XB(k, xi) = nv;
                 if (a.xtraj) a.xtraj[((size_t)k * NX + xi) * Bn + inst] = nv;
             }
             if (is_u && k < N) {
-                const float nv = UBAR(k, r) + REC(k, Lay::Z);
+                const float nv = UBAR(k, r) + z;
                 UBAR(k, r) = nv;
                 if (a.utraj) a.utraj[((size_t)k * NU + r) * Bn + inst] = nv;
             }
@@ -665,7 +738,6 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
             }
         }
     }
-#undef REC
 #undef XB
 #undef UBAR
 }

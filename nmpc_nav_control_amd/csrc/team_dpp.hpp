@@ -3,6 +3,11 @@
 // A team is one DPP row: lanes 16t..16t+15. row_newbcast:j broadcasts lane j of each row to the whole row
 // (gfx90a+), so four independent teams in a wave exchange data without LDS. Row reductions use the
 // quad_perm / row_half_mirror / row_mirror butterfly, which hipcc fuses into v_add_f32_dpp.
+//
+// The broadcast-multiply-accumulate chains of the Riccati recursion use the fused DPP forms
+// v_fmac_f32_dpp / v_fmac_f64_dpp (one VALU op per term instead of a v_mov_dpp + FMA pair). hipcc does not
+// form these for row_newbcast, so they are emitted as inline asm; the compiler's hazard recognizer does not
+// see inside asm, so every block starts with the two wait states a VALU write -> DPP read needs (s_nop 1).
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -38,6 +43,100 @@ __device__ __forceinline__ float bc16(float v, int j)
     }
 }
 
+// ---- fused broadcast FMA (inline asm) ----------------------------------------------------------------------
+// acc + bcast_J(a) * b   (S = -1: acc - bcast_J(a) * b)
+template <int J, int S>
+__device__ __forceinline__ float fmac_bc_t(float acc, float a, float b)
+{
+    if constexpr (S > 0)
+        asm volatile("s_nop 1\n\tv_fmac_f32_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
+                     : "+v"(acc) : "v"(a), "v"(b), "i"(J));
+    else
+        asm volatile("s_nop 1\n\tv_fmac_f32_dpp %0, -%1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
+                     : "+v"(acc) : "v"(a), "v"(b), "i"(J));
+    return acc;
+}
+
+template <int J, int S>
+__device__ __forceinline__ double fmac_bc64_t(double acc, double a, double b)
+{
+    if constexpr (S > 0)
+        asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
+                     : "+v"(acc) : "v"(a), "v"(b), "i"(J));
+    else
+        asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, -%1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
+                     : "+v"(acc) : "v"(a), "v"(b), "i"(J));
+    return acc;
+}
+
+template <int J>
+__device__ __forceinline__ double bc64_t(double v)
+{
+    double r;
+    asm volatile("s_nop 1\n\tv_mov_b64_dpp %0, %1 row_newbcast:%2 row_mask:0xf bank_mask:0xf" : "=v"(r) : "v"(v), "i"(J));
+    return r;
+}
+
+#define NMPC_SWITCH16(EXPR)                                                                                     \
+    switch (j & 15) {                                                                                          \
+    case 0: return EXPR(0);                                                                                    \
+    case 1: return EXPR(1);                                                                                    \
+    case 2: return EXPR(2);                                                                                    \
+    case 3: return EXPR(3);                                                                                    \
+    case 4: return EXPR(4);                                                                                    \
+    case 5: return EXPR(5);                                                                                    \
+    case 6: return EXPR(6);                                                                                    \
+    case 7: return EXPR(7);                                                                                    \
+    case 8: return EXPR(8);                                                                                    \
+    case 9: return EXPR(9);                                                                                    \
+    case 10: return EXPR(10);                                                                                  \
+    case 11: return EXPR(11);                                                                                  \
+    case 12: return EXPR(12);                                                                                  \
+    case 13: return EXPR(13);                                                                                  \
+    case 14: return EXPR(14);                                                                                  \
+    default: return EXPR(15);                                                                                  \
+    }
+
+// j must fold to a constant after unrolling (the switch then disappears)
+__device__ __forceinline__ float fmac_bc(float acc, float a, float b, int j)
+{
+#define E_(J) fmac_bc_t<J, 1>(acc, a, b)
+    NMPC_SWITCH16(E_)
+#undef E_
+}
+__device__ __forceinline__ float fnmac_bc(float acc, float a, float b, int j)
+{
+#define E_(J) fmac_bc_t<J, -1>(acc, a, b)
+    NMPC_SWITCH16(E_)
+#undef E_
+}
+__device__ __forceinline__ double fmac_bc64(double acc, double a, double b, int j)
+{
+#define E_(J) fmac_bc64_t<J, 1>(acc, a, b)
+    NMPC_SWITCH16(E_)
+#undef E_
+}
+__device__ __forceinline__ double fnmac_bc64(double acc, double a, double b, int j)
+{
+#define E_(J) fmac_bc64_t<J, -1>(acc, a, b)
+    NMPC_SWITCH16(E_)
+#undef E_
+}
+__device__ __forceinline__ double bc64(double v, int j)
+{
+#define E_(J) bc64_t<J>(v)
+    NMPC_SWITCH16(E_)
+#undef E_
+}
+#undef NMPC_SWITCH16
+
+// fp64 broadcast through two 32-bit row_newbcast moves (compiler-scheduled, no asm)
+__device__ __forceinline__ double bc16d(double v, int j)
+{
+    return __hiloint2double(__float_as_int(bc16(__int_as_float(__double2hiint(v)), j)),
+                            __float_as_int(bc16(__int_as_float(__double2loint(v)), j)));
+}
+
 // Sum over the 16 lanes of the row, result in every lane.
 __device__ __forceinline__ float row_sum16(float v)
 {
@@ -68,5 +167,15 @@ __device__ __forceinline__ float row_min16(float v)
 
 // max that propagates NaN (fmaxf drops it)
 __device__ __forceinline__ float nan_max(float a, float b) { return (b > a || b != b) ? b : a; }
+
+// hardware reciprocal (1 ulp), used for the IPM's elementwise divisions
+__device__ __forceinline__ float frcp(float x) { return __builtin_amdgcn_rcpf(x); }
+
+// full-precision fp64 reciprocal square root: v_rsq_f64 seed + one Newton step
+__device__ __forceinline__ double drsq(double x)
+{
+    double y = __builtin_amdgcn_rsq(x);
+    return y * (1.5 - 0.5 * x * y * y);
+}
 
 }  // namespace nmpc
