@@ -5,7 +5,7 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_DIR = os.path.join(_HERE, "lib")
-LIB_PATH = os.path.join(LIB_DIR, "libnmpc_amd.so")
+LIB_PATH = os.environ.get("NMPC_AMD_LIB") or os.path.join(LIB_DIR, "libnmpc_amd.so")
 
 MODEL_IDS = {"diff": 0, "omni4": 1, "tric": 2}
 MODEL_NAMES = {"diff": "diff2amr", "omni4": "omni4amr", "tric": "tric3amr"}

@@ -252,7 +252,7 @@ __global__ __launch_bounds__(64, 1) void k_sqp_rti_lane(KParams P, KArgs a, int 
     int status = 0, it = 0;
     float exit_res[3] = {0.0f, 0.0f, 0.0f};
     // step length, centring target and second-order weight of the previous iteration's direction
-    float alpha = 0.0f, sigma_mu = 0.0f, eta = 0.0f;
+    float alpha = 0.0f, sigma_mu = 0.0f, eta = 0.0f, mu_prev = 3.0e38f;
     for (it = 0;; it++) {
         // P1 (backward): apply previous update, residuals, adjoint pi, factorisation + predictor rhs.
         float Lp[NX][NX], pv[NX], pin[NX];
@@ -493,8 +493,10 @@ __global__ __launch_bounds__(64, 1) void k_sqp_rti_lane(KParams P, KArgs a, int 
         // fp32 stopping rule: the u-stationarity residual is a sum of terms of size stat_scale, so it cannot
         // fall below ~kStatRel * stat_scale; and once mu is 100x below its target the iterate is final.
         const bool stat_ok = res_stat <= P.tol_stat || res_stat <= kStatRel * stat_scale;
-        if (res_ineq <= P.tol_ineq && ((stat_ok && mu <= P.tol_comp) || mu <= 1e-2f * P.tol_comp)) break;
+        const bool stalled = mu <= P.tol_comp && mu > 0.5f * mu_prev;  // fp32 floor (see sqp_rti_team.hip)
+        if (res_ineq <= P.tol_ineq && ((stat_ok && mu <= P.tol_comp) || mu <= 1e-2f * P.tol_comp || stalled)) break;
         if (it >= P.iter_max) break;
+        mu_prev = mu;
 
         // P2 (forward): affine direction, its maximal step and the mu_aff polynomial.
         float s1 = 0.0f, s2 = 0.0f, amax = 1e30f;

@@ -25,6 +25,18 @@
 
 namespace nmpc {
 
+#ifdef NMPC_STAMPS
+// diagnostic build only: s_memtime at phase boundaries for the first team of the first 256 waves
+constexpr int kStampIts = 64;
+__device__ unsigned long long g_stamps[256][2 + 4 * kStampIts];
+#define STAMP(slot)                                                                                              \
+    do {                                                                                                         \
+        if (r == 0 && (team & 3) == 0 && (team >> 2) < 256) g_stamps[team >> 2][(slot)] = __builtin_amdgcn_s_memtime(); \
+    } while (0)
+#else
+#define STAMP(slot) ((void)0)
+#endif
+
 template <class M>
 struct TeamRec {
     static constexpr int NX = M::NX, NU = M::NU, NV = NX + NU, NGV = M::NGV;
@@ -48,6 +60,11 @@ namespace {
 
 constexpr float kBreakdownMuT = 1e-6f;
 constexpr float kStatRelT = 1e-5f;
+#ifdef NMPC_STAMPS
+constexpr int kStampItsC = kStampIts;
+#else
+constexpr int kStampItsC = 0;
+#endif
 
 template <class M>
 __device__ __forceinline__ int xcomp(int xi)
@@ -187,6 +204,7 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
 #define XB(k, j) a.xbar[((size_t)(k) * NX + (j)) * S + inst]
 #define UBAR(k, j) a.ubar[((size_t)(k) * NU + (j)) * S + inst]
 
+    STAMP(0);
     // ---- reset -----------------------------------------------------------------------------------------
     if (a.reset && a.reset[inst]) {
         for (int k = r; k <= N; k += 16)
@@ -324,20 +342,21 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
     }
     // row xi of the constant rows of [B A] (lane NU+xi, xi >= NGV): grow[v] = G[xi][v], from lane v's column
     float grow[NV];
-#pragma unroll
-    for (int v = 0; v < NV; v++) {
+    sfor<0, NV>([&](auto vc) {
+        constexpr int v = decltype(vc)::value;
         float s = 0.0f;
 #pragma unroll
         for (int i = NGV; i < NX; i++) {
-            const float t = bc16(gcol[i], v);
+            const float t = bc<v>(gcol[i]);
             if (is_x && xi == i) s = t;
         }
         grow[v] = s;
-    }
+    });
     double gcol64[NX];
 #pragma unroll
     for (int i = 0; i < NX; i++) gcol64[i] = (double)gcol[i];
 
+    STAMP(1);
     const int m = N * NU + N * M::NBX;
     const float inv_m2 = 0.5f / (float)m;
 
@@ -350,8 +369,10 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
             if (xi == i) nxt = s;
         }
         float cr = 0.0f;
-#pragma unroll
-        for (int v = 0; v < NV; v++) cr = fmac_bc(cr, dzv, grow[v], v);
+        sfor<0, NV>([&](auto vc) {
+            constexpr int v = decltype(vc)::value;
+            cr = fmac_bc<v>(cr, dzv, grow[v]);
+        });
         return (xi >= NGV) ? cr : nxt;
     };
 
@@ -359,7 +380,7 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
     int status = 0, it_done = 0;
     bool done = false;
     float exit_res[3] = {0.0f, 0.0f, 0.0f};
-    float alpha = 0.0f, sigma_mu = 0.0f, eta = 0.0f;
+    float alpha = 0.0f, sigma_mu = 0.0f, eta = 0.0f, mu_prev = 3.0e38f;
     for (int it = 0;; it++) {
         // P1 (backward): apply the previous step, residuals, adjoint, fp64 square-root Riccati factorisation,
         // predictor rhs
@@ -422,8 +443,10 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
             // adjoint: c_v = sum_l G[l][v] pi_{k+1}[l]
             float cpi = 0.0f;
             if (k < N) {
-#pragma unroll
-                for (int l = 0; l < NX; l++) cpi = fmac_bc(cpi, piv, Gc[l], NU + l);
+                sfor<0, NX>([&](auto lc) {
+                    constexpr int l = decltype(lc)::value;
+                    cpi = fmac_bc<NU + l>(cpi, piv, Gc[l]);
+                });
             }
             const float hz = ((k < N) ? h_stage : we_lane) * z;
             const float g = rc[R::GR];
@@ -450,35 +473,41 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
                 for (int l = 0; l < NX; l++) Gd[l] = (l < NGV) ? (double)Gc[l] : gcol64[l];
                 // LBA column v = L_{k+1}' G[:, v]; L[l][i] sits in lane NU+l at Lrow[NU+i]
                 double lba[NX];
-#pragma unroll
-                for (int i = 0; i < NX; i++) {
+                sfor<0, NX>([&](auto ic) {
+                    constexpr int i = decltype(ic)::value;
                     double s = 0.0;
-#pragma unroll
-                    for (int l = i; l < NX; l++) s = fmac_bc64(s, Lrow[NU + i], Gd[l], NU + l);
+                    sfor<i, NX>([&](auto lc) {
+                        constexpr int l = decltype(lc)::value;
+                        s = fmac_bc64<NU + l>(s, Lrow[NU + i], Gd[l]);
+                    });
                     lba[i] = s;
-                }
+                });
                 // row r of M = D + LBA' LBA, factored column by column (row-distributed Cholesky, fp64)
                 const double dg = valid ? (double)h_stage + (double)sig : 1.0;
                 double Lr[NV];
-#pragma unroll
-                for (int j = 0; j < NV; j++) {
+                sfor<0, NV>([&](auto jc) {
+                    constexpr int j = decltype(jc)::value;
                     double mj = (r == j) ? dg : 0.0;
-#pragma unroll
-                    for (int i = 0; i < NX; i++) mj = fmac_bc64(mj, lba[i], lba[i], j);
+                    sfor<0, NX>([&](auto ic) {
+                        constexpr int i = decltype(ic)::value;
+                        mj = fmac_bc64<j>(mj, lba[i], lba[i]);
+                    });
                     double s = mj;
-#pragma unroll
-                    for (int q = 0; q < j; q++) s = fnmac_bc64(s, Lr[q], Lr[q], j);
-                    const double pivot = bc64(s, j);
+                    sfor<0, j>([&](auto qc) {
+                        constexpr int q = decltype(qc)::value;
+                        s = fnmac_bc64<j>(s, Lr[q], Lr[q]);
+                    });
+                    const double pivot = bc64<j>(s);
                     double rd;
-                    if (j < NU) {
+                    if constexpr (j < NU) {
                         if (!(pivot > 0.0)) fail = true;
                         rd = drsq(fmax(pivot, 1e-300));
                     } else {
-                        const double mjj = bc64(mj, j);
+                        const double mjj = bc64<j>(mj);
                         rd = (pivot > 1e-10 * (1.0 + fabs(mjj))) ? drsq(pivot) : 0.0;  // PSD state block
                     }
                     Lr[j] = (r == j) ? pivot * rd : ((r > j) ? s * rd : 0.0);
-                }
+                });
                 float Lm[NU];
 #pragma unroll
                 for (int q = 0; q < NU; q++) {
@@ -487,15 +516,17 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
                 }
                 // rhs: w = g^ + G' p_{k+1}; forward substitution over the input block (fp32)
                 float y = ghat;
-#pragma unroll
-                for (int l = 0; l < NX; l++) y = fmac_bc(y, pv, Gc[l], NU + l);
+                sfor<0, NX>([&](auto lc) {
+                    constexpr int l = decltype(lc)::value;
+                    y = fmac_bc<NU + l>(y, pv, Gc[l]);
+                });
                 float my_lr = 0.0f;
-#pragma unroll
-                for (int j = 0; j < NU; j++) {
-                    const float lrj = bc16(y * frcp(Lm[j]), j);  // (y_j / L_jj) from lane j
+                sfor<0, NU>([&](auto jc) {
+                    constexpr int j = decltype(jc)::value;
+                    const float lrj = bc<j>(y * frcp(Lm[j]));  // (y_j / L_jj) from lane j
                     if (r == j) my_lr = lrj;
                     y -= Lm[j] * lrj;
-                }
+                });
                 rc[R::LR] = my_lr;
                 pv = is_x ? y : 0.0f;
 #pragma unroll
@@ -504,6 +535,7 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
             piv = pi_new;
             if (act) rec_store<NQ>(tbase + (size_t)k * KS, rc);
         }
+        if (it < kStampItsC) STAMP(2 + 4 * it);
         // team reductions
         sum_c = row_sum16(lv ? sum_c : 0.0f);
         res_ineq = row_max16(lv ? res_ineq : 0.0f);
@@ -525,7 +557,12 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
                 stop = true;
             } else {
                 const bool stat_ok = res_stat <= P.tol_stat || res_stat <= kStatRelT * stat_scale;
-                if (res_ineq <= P.tol_ineq && ((stat_ok && mu <= P.tol_comp) || mu <= 1e-2f * P.tol_comp)) stop = true;
+                // fp32 floor: below ~1e-12 the complementarity no longer decreases and the fp32 multiplier
+                // updates (Sigma ~ 1e10 times the rounding of dz) degrade stationarity, so a stalled mu that is
+                // already under tol_comp ends the iteration as well
+                const bool stalled = mu <= P.tol_comp && mu > 0.5f * mu_prev;
+                if (res_ineq <= P.tol_ineq && ((stat_ok && mu <= P.tol_comp) || mu <= 1e-2f * P.tol_comp || stalled))
+                    stop = true;
                 if (it >= P.iter_max) stop = true;
             }
             if (stop) {
@@ -533,6 +570,7 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
                 it_done = it;
             }
         }
+        mu_prev = mu;
         if (__all(done)) break;
         const bool act2 = lv && !done;
 
@@ -560,17 +598,19 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
                 for (int q = 0; q < NU; q++) du_all[q] = 0.0f;
                 if (k < N) {
                     float w[NU];
-#pragma unroll
-                    for (int q = 0; q < NU; q++)
-                        w[q] = bc16(rc[R::LR], q) + ((k > 0) ? row_sum16(is_x ? rc[R::LM + q] * dxs : 0.0f) : 0.0f);
-#pragma unroll
-                    for (int qq = 0; qq < NU; qq++) {
-                        const int q = NU - 1 - qq;
+                    sfor<0, NU>([&](auto qc) {
+                        constexpr int q = decltype(qc)::value;
+                        w[q] = bc<q>(rc[R::LR]) + ((k > 0) ? row_sum16(is_x ? rc[R::LM + q] * dxs : 0.0f) : 0.0f);
+                    });
+                    sfor<0, NU>([&](auto qqc) {
+                        constexpr int q = NU - 1 - decltype(qqc)::value;
                         float s = w[q];
-#pragma unroll
-                        for (int j = q + 1; j < NU; j++) s -= bc16(rc[R::LM + q], j) * du_all[j];
-                        du_all[q] = s * frcp(bc16(rc[R::LM + q], q));
-                    }
+                        sfor<q + 1, NU>([&](auto jc) {
+                            constexpr int j = decltype(jc)::value;
+                            s -= bc<j>(rc[R::LM + q]) * du_all[j];
+                        });
+                        du_all[q] = s * frcp(bc<q>(rc[R::LM + q]));
+                    });
 #pragma unroll
                     for (int q = 0; q < NU; q++) du_all[q] = -du_all[q];
                 }
@@ -635,19 +675,19 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
                     pvc = is_x ? ghat : 0.0f;
                 } else {
                     float y = ghat;
-#pragma unroll
-                    for (int l = 0; l < NX; l++) {
+                    sfor<0, NX>([&](auto lc) {
+                        constexpr int l = decltype(lc)::value;
                         const float gl = (l < NGV) ? rc[R::GV + (l < NGV ? l : 0)] : gcol[l];
-                        y = fmac_bc(y, pvc, gl, NU + l);
-                    }
+                        y = fmac_bc<NU + l>(y, pvc, gl);
+                    });
                     float my_lr = 0.0f;
-#pragma unroll
-                    for (int j = 0; j < NU; j++) {
+                    sfor<0, NU>([&](auto jc) {
+                        constexpr int j = decltype(jc)::value;
                         const float Lmj = rc[R::LM + j];
-                        const float lrj = bc16(y * frcp(Lmj), j);
+                        const float lrj = bc<j>(y * frcp(Lmj));
                         if (r == j) my_lr = lrj;
                         y -= Lmj * lrj;
-                    }
+                    });
                     if (act2 && is_u) tbase[(size_t)k * KS + R::LR] = my_lr;
                     pvc = is_x ? y : 0.0f;
                 }
@@ -656,6 +696,7 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
 
         float amax, s1, s2;
         forward(0, amax, s1, s2);
+        if (it < kStampItsC) STAMP(3 + 4 * it);
         s1 = row_sum16(lv ? s1 : 0.0f);
         s2 = row_sum16(lv ? s2 : 0.0f);
         amax = row_min16(lv ? amax : 1e30f);
@@ -677,6 +718,7 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
             am = row_min16(lv ? am : 1e30f);
             alpha = fminf(1.0f, P.tau * am);
         }
+        if (it < kStampItsC) STAMP(4 + 4 * it);
         if (!__all(done || alpha >= 0.1f)) {
             if (!done && alpha < 0.1f) {
                 sigma_mu = fmaxf(sigma, 0.3f) * mu;
@@ -688,6 +730,7 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
                 alpha = fminf(1.0f, P.tau * am);
             }
         }
+        if (it < kStampItsC) STAMP(5 + 4 * it);
     }
 
     // ---- full SQP step + outputs ----------------------------------------------------------------------
@@ -761,5 +804,14 @@ template hipError_t launch_sqp_rti_team<Tric3>(const KParams&, const KArgs&, int
 template size_t team_scratch_floats<Diff2>(int, int);
 template size_t team_scratch_floats<Omni4>(int, int);
 template size_t team_scratch_floats<Tric3>(int, int);
+
+#ifdef NMPC_STAMPS
+extern "C" int nmpc_debug_stamps(unsigned long long* host, int n)
+{
+    const size_t bytes = sizeof(unsigned long long) * (size_t)n;
+    if (bytes > sizeof(g_stamps)) return -1;
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_stamps), bytes, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -2;
+}
+#endif
 
 }  // namespace nmpc

@@ -12,7 +12,21 @@
 
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 namespace nmpc {
+
+// Compile-time loop: f(std::integral_constant<int, I>) for I in [B, E). The DPP lane operand of the
+// broadcasts below must be an immediate; a switch over a runtime index inside #pragma unroll loops blows up
+// the unroller's size estimate (the loops then stay rolled and the switch becomes branches).
+template <int B, int E, class F>
+__device__ __forceinline__ void sfor(F&& f)
+{
+    if constexpr (B < E) {
+        f(std::integral_constant<int, B>{});
+        sfor<B + 1, E>(f);
+    }
+}
 
 template <int CTRL>
 __device__ __forceinline__ float dpp_f(float v)
@@ -20,7 +34,14 @@ __device__ __forceinline__ float dpp_f(float v)
     return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
 }
 
-// Value of lane j (0..15) of this lane's 16-lane row. j must fold to a constant after unrolling.
+// Value of lane J (0..15) of this lane's 16-lane row.
+template <int J>
+__device__ __forceinline__ float bc(float v)
+{
+    return dpp_f<0x150 + J>(v);
+}
+
+// Runtime-index form (j must fold to a constant; prefer bc<J> inside loops).
 __device__ __forceinline__ float bc16(float v, int j)
 {
     switch (j & 15) {
@@ -77,58 +98,16 @@ __device__ __forceinline__ double bc64_t(double v)
     return r;
 }
 
-#define NMPC_SWITCH16(EXPR)                                                                                     \
-    switch (j & 15) {                                                                                          \
-    case 0: return EXPR(0);                                                                                    \
-    case 1: return EXPR(1);                                                                                    \
-    case 2: return EXPR(2);                                                                                    \
-    case 3: return EXPR(3);                                                                                    \
-    case 4: return EXPR(4);                                                                                    \
-    case 5: return EXPR(5);                                                                                    \
-    case 6: return EXPR(6);                                                                                    \
-    case 7: return EXPR(7);                                                                                    \
-    case 8: return EXPR(8);                                                                                    \
-    case 9: return EXPR(9);                                                                                    \
-    case 10: return EXPR(10);                                                                                  \
-    case 11: return EXPR(11);                                                                                  \
-    case 12: return EXPR(12);                                                                                  \
-    case 13: return EXPR(13);                                                                                  \
-    case 14: return EXPR(14);                                                                                  \
-    default: return EXPR(15);                                                                                  \
-    }
-
-// j must fold to a constant after unrolling (the switch then disappears)
-__device__ __forceinline__ float fmac_bc(float acc, float a, float b, int j)
-{
-#define E_(J) fmac_bc_t<J, 1>(acc, a, b)
-    NMPC_SWITCH16(E_)
-#undef E_
-}
-__device__ __forceinline__ float fnmac_bc(float acc, float a, float b, int j)
-{
-#define E_(J) fmac_bc_t<J, -1>(acc, a, b)
-    NMPC_SWITCH16(E_)
-#undef E_
-}
-__device__ __forceinline__ double fmac_bc64(double acc, double a, double b, int j)
-{
-#define E_(J) fmac_bc64_t<J, 1>(acc, a, b)
-    NMPC_SWITCH16(E_)
-#undef E_
-}
-__device__ __forceinline__ double fnmac_bc64(double acc, double a, double b, int j)
-{
-#define E_(J) fmac_bc64_t<J, -1>(acc, a, b)
-    NMPC_SWITCH16(E_)
-#undef E_
-}
-__device__ __forceinline__ double bc64(double v, int j)
-{
-#define E_(J) bc64_t<J>(v)
-    NMPC_SWITCH16(E_)
-#undef E_
-}
-#undef NMPC_SWITCH16
+template <int J>
+__device__ __forceinline__ float fmac_bc(float acc, float a, float b) { return fmac_bc_t<J, 1>(acc, a, b); }
+template <int J>
+__device__ __forceinline__ float fnmac_bc(float acc, float a, float b) { return fmac_bc_t<J, -1>(acc, a, b); }
+template <int J>
+__device__ __forceinline__ double fmac_bc64(double acc, double a, double b) { return fmac_bc64_t<J, 1>(acc, a, b); }
+template <int J>
+__device__ __forceinline__ double fnmac_bc64(double acc, double a, double b) { return fmac_bc64_t<J, -1>(acc, a, b); }
+template <int J>
+__device__ __forceinline__ double bc64(double v) { return bc64_t<J>(v); }
 
 // fp64 broadcast through two 32-bit row_newbcast moves (compiler-scheduled, no asm)
 __device__ __forceinline__ double bc16d(double v, int j)
