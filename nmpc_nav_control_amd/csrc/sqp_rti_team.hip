@@ -21,6 +21,7 @@
 // The IPM iteration count is per team; a wave iterates until its four teams have converged (finished teams
 // skip their loads and stores).
 #include "nmpc_kernels.hpp"
+#include "team_asm_gen.hpp"
 #include "team_dpp.hpp"
 
 namespace nmpc {
@@ -65,6 +66,38 @@ constexpr int kStampItsC = kStampIts;
 #else
 constexpr int kStampItsC = 0;
 #endif
+
+// generated whole-block fused-DPP kernels (team_asm_gen.hpp), dispatched on the model shape
+template <int NX, int NU>
+__device__ __forceinline__ void lba_block(double (&acc)[NX], const double (&lrow)[NX + NU], const double (&gd)[NX])
+{
+    if constexpr (NX == 7 && NU == 2) lba_block_7_2(acc, lrow, gd);
+    else lba_block_11_4(acc, lrow, gd);
+}
+template <int NX, int NU>
+__device__ __forceinline__ void mrow_block(double (&acc)[NX + NU], double (&md)[NX + NU], const double (&lba)[NX])
+{
+    if constexpr (NX == 7 && NU == 2) mrow_block_7_2(acc, md, lba);
+    else mrow_block_11_4(acc, md, lba);
+}
+template <int NX, int NU, int J>
+__device__ __forceinline__ void chol_update(double (&lr)[NX + NU], double lj, double& piv)
+{
+    if constexpr (NX == 7 && NU == 2) chol_update_7_2<J>(lr, lj, piv);
+    else chol_update_11_4<J>(lr, lj, piv);
+}
+template <int NX, int NU>
+__device__ __forceinline__ float dot_x(float acc, float a, const float (&b)[NX])  // acc + sum_l bc_{NU+l}(a) b[l]
+{
+    if constexpr (NX == 7 && NU == 2) return dot_x_7_2(acc, a, b);
+    else return dot_x_11_4(acc, a, b);
+}
+template <int NX, int NU>
+__device__ __forceinline__ float dot_v(float acc, float a, const float (&b)[NX + NU])  // acc + sum_v bc_v(a) b[v]
+{
+    if constexpr (NX == 7 && NU == 2) return dot_v_7_2(acc, a, b);
+    else return dot_v_11_4(acc, a, b);
+}
 
 template <class M>
 __device__ __forceinline__ int xcomp(int xi)
@@ -368,12 +401,28 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
             const float s = row_sum16(lv ? rc[R::GV + i] * dzv : 0.0f);
             if (xi == i) nxt = s;
         }
-        float cr = 0.0f;
-        sfor<0, NV>([&](auto vc) {
-            constexpr int v = decltype(vc)::value;
-            cr = fmac_bc<v>(cr, dzv, grow[v]);
-        });
+        const float cr = dot_v<NX, NU>(0.0f, dzv, grow);
         return (xi >= NGV) ? cr : nxt;
+    };
+    // column v of [B A] at a stage (rows < NGV from the record)
+    auto column = [&](const float (&rc)[RS], float (&Gc)[NX]) {
+#pragma unroll
+        for (int i = 0; i < NX; i++) Gc[i] = (i < NGV) ? rc[R::GV + (i < NGV ? i : 0)] : gcol[i];
+    };
+    // Stage sweep k = k0, k0 + dir, ..., k1: the next stage's record is loaded while body(k, rec) runs.
+    auto sweep = [&](int k0, int k1, int dir, bool ld, auto&& body) {
+        float nx[RS];
+#pragma unroll
+        for (int f = 0; f < RS; f++) nx[f] = 0.0f;
+        if (ld) rec_load<NQ>(tbase + (size_t)k0 * KS, nx);
+        for (int k = k0;; k += dir) {
+            float rc[RS];
+#pragma unroll
+            for (int f = 0; f < RS; f++) rc[f] = nx[f];
+            if (ld && k != k1) rec_load<NQ>(tbase + (size_t)(k + dir) * KS, nx);
+            body(k, rc);
+            if (k == k1) break;
+        }
     };
 
     // ---- interior-point iterations ----------------------------------------------------------------------
@@ -385,20 +434,14 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
         // P1 (backward): apply the previous step, residuals, adjoint, fp64 square-root Riccati factorisation,
         // predictor rhs
         double Lrow[NV];  // row r of the factor of stage k+1 (state lanes carry the rows of L_{k+1})
+#pragma unroll
+        for (int j = 0; j < NV; j++) Lrow[j] = 0.0;
         float pv = 0.0f, piv = 0.0f;
         float res_stat = 0.0f, res_ineq = 0.0f, sum_c = 0.0f, stat_scale = 1.0f, nanf_ = 0.0f;
         bool fail = false;
         const bool act = lv && !done;
         const float a_upd = (it > 0 && !done) ? alpha : 0.0f;
-        float nx_rec[RS];
-#pragma unroll
-        for (int f = 0; f < RS; f++) nx_rec[f] = 0.0f;
-        if (act) rec_load<NQ>(tbase + (size_t)N * KS, nx_rec);
-        for (int k = N; k >= 0; k--) {
-            float rc[RS];
-#pragma unroll
-            for (int f = 0; f < RS; f++) rc[f] = nx_rec[f];
-            if (act && k > 0) rec_load<NQ>(tbase + (size_t)(k - 1) * KS, nx_rec);
+        sweep(N, 0, -1, act, [&](int k, float (&rc)[RS]) {
             const bool vu = is_u && k < N;
             const bool vx = is_x && k >= 1;
             const bool valid = vu || vx;
@@ -436,18 +479,10 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
                 sig = ll * itl + lu * itu;
                 gh = ll * rl * itl + ll - lu * rr * itu - lu;
             }
-            // column v of [B A] of this lane (stage k < N)
             float Gc[NX];
-#pragma unroll
-            for (int i = 0; i < NX; i++) Gc[i] = (i < NGV) ? rc[R::GV + (i < NGV ? i : 0)] : gcol[i];
+            column(rc, Gc);
             // adjoint: c_v = sum_l G[l][v] pi_{k+1}[l]
-            float cpi = 0.0f;
-            if (k < N) {
-                sfor<0, NX>([&](auto lc) {
-                    constexpr int l = decltype(lc)::value;
-                    cpi = fmac_bc<NU + l>(cpi, piv, Gc[l]);
-                });
-            }
+            const float cpi = (k < N) ? dot_x<NX, NU>(0.0f, piv, Gc) : 0.0f;
             const float hz = ((k < N) ? h_stage : we_lane) * z;
             const float g = rc[R::GR];
             const float base = hz + g - lamdiff + cpi;
@@ -473,40 +508,31 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
                 for (int l = 0; l < NX; l++) Gd[l] = (l < NGV) ? (double)Gc[l] : gcol64[l];
                 // LBA column v = L_{k+1}' G[:, v]; L[l][i] sits in lane NU+l at Lrow[NU+i]
                 double lba[NX];
-                sfor<0, NX>([&](auto ic) {
-                    constexpr int i = decltype(ic)::value;
-                    double s = 0.0;
-                    sfor<i, NX>([&](auto lc) {
-                        constexpr int l = decltype(lc)::value;
-                        s = fmac_bc64<NU + l>(s, Lrow[NU + i], Gd[l]);
-                    });
-                    lba[i] = s;
-                });
-                // row r of M = D + LBA' LBA, factored column by column (row-distributed Cholesky, fp64)
+#pragma unroll
+                for (int i = 0; i < NX; i++) lba[i] = 0.0;
+                lba_block<NX, NU>(lba, Lrow, Gd);
+                // row r of M = D + LBA' LBA, then its right-looking row-distributed Cholesky in fp64: column j's
+                // pivot comes from lane j, every later column is updated by one fused block
                 const double dg = valid ? (double)h_stage + (double)sig : 1.0;
-                double Lr[NV];
+                double Lr[NV], md[NV];
+#pragma unroll
+                for (int j = 0; j < NV; j++) Lr[j] = (r == j) ? dg : 0.0;
+                mrow_block<NX, NU>(Lr, md, lba);  // md[j] = M[j][j] (lane j's diagonal), md[0] = first pivot
+                double pivot = md[0];
                 sfor<0, NV>([&](auto jc) {
                     constexpr int j = decltype(jc)::value;
-                    double mj = (r == j) ? dg : 0.0;
-                    sfor<0, NX>([&](auto ic) {
-                        constexpr int i = decltype(ic)::value;
-                        mj = fmac_bc64<j>(mj, lba[i], lba[i]);
-                    });
-                    double s = mj;
-                    sfor<0, j>([&](auto qc) {
-                        constexpr int q = decltype(qc)::value;
-                        s = fnmac_bc64<j>(s, Lr[q], Lr[q]);
-                    });
-                    const double pivot = bc64<j>(s);
+                    const double s = Lr[j];  // M[r][j] minus the updates of columns < j
                     double rd;
                     if constexpr (j < NU) {
                         if (!(pivot > 0.0)) fail = true;
                         rd = drsq(fmax(pivot, 1e-300));
                     } else {
-                        const double mjj = bc64<j>(mj);
-                        rd = (pivot > 1e-10 * (1.0 + fabs(mjj))) ? drsq(pivot) : 0.0;  // PSD state block
+                        rd = (pivot > 1e-10 * (1.0 + fabs(md[j]))) ? drsq(pivot) : 0.0;  // PSD state block
                     }
-                    Lr[j] = (r == j) ? pivot * rd : ((r > j) ? s * rd : 0.0);
+                    const double lj = (r >= j) ? s * rd : 0.0;  // lane j: s == pivot
+                    Lr[j] = lj;
+                    // right-looking update M[r][j'] -= L[r][j] L[j'][j] (j' > j) and the next pivot
+                    if constexpr (j + 1 < NV) chol_update<NX, NU, j>(Lr, lj, pivot);
                 });
                 float Lm[NU];
 #pragma unroll
@@ -515,11 +541,7 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
                     rc[R::LM + q] = Lm[q];
                 }
                 // rhs: w = g^ + G' p_{k+1}; forward substitution over the input block (fp32)
-                float y = ghat;
-                sfor<0, NX>([&](auto lc) {
-                    constexpr int l = decltype(lc)::value;
-                    y = fmac_bc<NU + l>(y, pv, Gc[l]);
-                });
+                float y = dot_x<NX, NU>(ghat, pv, Gc);
                 float my_lr = 0.0f;
                 sfor<0, NU>([&](auto jc) {
                     constexpr int j = decltype(jc)::value;
@@ -534,7 +556,7 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
             }
             piv = pi_new;
             if (act) rec_store<NQ>(tbase + (size_t)k * KS, rc);
-        }
+        });
         if (it < kStampItsC) STAMP(2 + 4 * it);
         // team reductions
         sum_c = row_sum16(lv ? sum_c : 0.0f);
@@ -572,24 +594,64 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
         }
         mu_prev = mu;
         if (__all(done)) break;
-        const bool act2 = lv && !done;
 
-        // forward sweep: du from the stored factor, dz, bounded-variable directions, next-stage dx.
-        // pass 0: affine direction (stores DZA; s1, s2 of the mu_aff polynomial); pass > 0: combined (stores DZ)
-        auto forward = [&](int pass, float& amax, float& s1, float& s2) {
-            float dxs = 0.0f;
-            amax = 1e30f;
-            s1 = 0.0f;
-            s2 = 0.0f;
-            float nr[RS];
-#pragma unroll
-            for (int f = 0; f < RS; f++) nr[f] = 0.0f;
-            if (act2) rec_load<NQ>(tbase, nr);
-            for (int k = 0; k <= N; k++) {
-                float rc[RS];
-#pragma unroll
-                for (int f = 0; f < RS; f++) rc[f] = nr[f];
-                if (act2 && k < N) rec_load<NQ>(tbase + (size_t)(k + 1) * KS, nr);
+        // pass 0: affine direction (forward; stores DZA, sums s1/s2 of the mu_aff polynomial);
+        // pass 1: Mehrotra corrector (backward rhs through the stored factor, then forward; stores DZ);
+        // pass 2: pure-centring safeguard for teams whose pass-1 step stayed below 0.1
+        float sigma = 0.0f, alpha_aff = 0.0f;
+        for (int pass = 0; pass < 3; pass++) {
+            bool run = !done;
+            if (pass == 1) {
+                sigma_mu = sigma * mu;
+                eta = alpha_aff;
+            } else if (pass == 2) {
+                if (__all(done || alpha >= 0.1f)) break;
+                run = run && alpha < 0.1f;
+                sigma_mu = fmaxf(sigma, 0.3f) * mu;
+                eta = 0.0f;
+            }
+            const bool ld = lv && run;
+            if (pass > 0) {
+                // corrector rhs through the stored factorisation (backward)
+                float pvc = 0.0f;
+                sweep(N, 0, -1, ld, [&](int k, float (&rc)[RS]) {
+                    const bool vu = is_u && k < N;
+                    const bool vx = is_x && k >= 1;
+                    const bool valid = vu || vx;
+                    float ghat = 0.0f;
+                    if (valid && has_b) {
+                        const float z = rc[R::Z];
+                        const float tl = rc[R::TL], tu = rc[R::TU], ll = rc[R::LL], lu = rc[R::LU];
+                        const float rl = z - rc[R::LB] - tl, rr = rc[R::UB] - z - tu;
+                        const float itl = frcp(tl), itu = frcp(tu);
+                        const BoundDir da = bound_dir(rc[R::DZA], rl, rr, tl, tu, ll, lu, itl, itu, 0.0f, 0.0f);
+                        const float tgl = sigma_mu - eta * da.dll * da.dtl, tgu = sigma_mu - eta * da.dlu * da.dtu;
+                        ghat = -(tgl - ll * rl) * itl + ll + (tgu - lu * rr) * itu - lu;
+                    }
+                    if (vu) ghat += rc[R::RU];
+                    if (k == N) {
+                        pvc = is_x ? ghat : 0.0f;
+                    } else {
+                        float Gc[NX];
+                        column(rc, Gc);
+                        float y = dot_x<NX, NU>(ghat, pvc, Gc);
+                        float my_lr = 0.0f;
+                        sfor<0, NU>([&](auto jc) {
+                            constexpr int j = decltype(jc)::value;
+                            const float Lmj = rc[R::LM + j];
+                            const float lrj = bc<j>(y * frcp(Lmj));
+                            if (r == j) my_lr = lrj;
+                            y -= Lmj * lrj;
+                        });
+                        if (ld && is_u) tbase[(size_t)k * KS + R::LR] = my_lr;
+                        rc[R::LR] = my_lr;
+                        pvc = is_x ? y : 0.0f;
+                    }
+                });
+            }
+            // forward: du from the stored factor, dz, bounded-variable directions, next-stage dx
+            float dxs = 0.0f, amax = 1e30f, s1 = 0.0f, s2 = 0.0f;
+            sweep(0, N, 1, ld, [&](int k, float (&rc)[RS]) {
                 const bool vu = is_u && k < N;
                 const bool vx = is_x && k >= 1;
                 const bool valid = vu || vx;
@@ -604,12 +666,12 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
                     });
                     sfor<0, NU>([&](auto qqc) {
                         constexpr int q = NU - 1 - decltype(qqc)::value;
-                        float s = w[q];
+                        float sq = w[q];
                         sfor<q + 1, NU>([&](auto jc) {
                             constexpr int j = decltype(jc)::value;
-                            s -= bc<j>(rc[R::LM + q]) * du_all[j];
+                            sq -= bc<j>(rc[R::LM + q]) * du_all[j];
                         });
-                        du_all[q] = s * frcp(bc<q>(rc[R::LM + q]));
+                        du_all[q] = sq * frcp(bc<q>(rc[R::LM + q]));
                     });
 #pragma unroll
                     for (int q = 0; q < NU; q++) du_all[q] = -du_all[q];
@@ -640,94 +702,22 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
                         s2 += d.dll * d.dtl + d.dlu * d.dtu;
                     }
                 }
-                if (act2 && valid) tbase[(size_t)k * KS + (pass == 0 ? R::DZA : R::DZ)] = dz;
+                if (ld && valid) tbase[(size_t)k * KS + (pass == 0 ? R::DZA : R::DZ)] = dz;
                 if (k < N) dxs = dyn(rc, valid ? dz : 0.0f);
-            }
-        };
-
-        // corrector rhs through the stored factorisation (backward)
-        auto corrector_rhs = [&]() {
-            float pvc = 0.0f;
-            float nr[RS];
-#pragma unroll
-            for (int f = 0; f < RS; f++) nr[f] = 0.0f;
-            if (act2) rec_load<NQ>(tbase + (size_t)N * KS, nr);
-            for (int k = N; k >= 0; k--) {
-                float rc[RS];
-#pragma unroll
-                for (int f = 0; f < RS; f++) rc[f] = nr[f];
-                if (act2 && k > 0) rec_load<NQ>(tbase + (size_t)(k - 1) * KS, nr);
-                const bool vu = is_u && k < N;
-                const bool vx = is_x && k >= 1;
-                const bool valid = vu || vx;
-                float ghat = 0.0f;
-                if (valid && has_b) {
-                    const float z = rc[R::Z];
-                    const float tl = rc[R::TL], tu = rc[R::TU], ll = rc[R::LL], lu = rc[R::LU];
-                    const float rl = z - rc[R::LB] - tl, rr = rc[R::UB] - z - tu;
-                    const float itl = frcp(tl), itu = frcp(tu);
-                    const BoundDir da = bound_dir(rc[R::DZA], rl, rr, tl, tu, ll, lu, itl, itu, 0.0f, 0.0f);
-                    const float tgl = sigma_mu - eta * da.dll * da.dtl, tgu = sigma_mu - eta * da.dlu * da.dtu;
-                    ghat = -(tgl - ll * rl) * itl + ll + (tgu - lu * rr) * itu - lu;
-                }
-                if (vu) ghat += rc[R::RU];
-                if (k == N) {
-                    pvc = is_x ? ghat : 0.0f;
-                } else {
-                    float y = ghat;
-                    sfor<0, NX>([&](auto lc) {
-                        constexpr int l = decltype(lc)::value;
-                        const float gl = (l < NGV) ? rc[R::GV + (l < NGV ? l : 0)] : gcol[l];
-                        y = fmac_bc<NU + l>(y, pvc, gl);
-                    });
-                    float my_lr = 0.0f;
-                    sfor<0, NU>([&](auto jc) {
-                        constexpr int j = decltype(jc)::value;
-                        const float Lmj = rc[R::LM + j];
-                        const float lrj = bc<j>(y * frcp(Lmj));
-                        if (r == j) my_lr = lrj;
-                        y -= Lmj * lrj;
-                    });
-                    if (act2 && is_u) tbase[(size_t)k * KS + R::LR] = my_lr;
-                    pvc = is_x ? y : 0.0f;
-                }
-            }
-        };
-
-        float amax, s1, s2;
-        forward(0, amax, s1, s2);
-        if (it < kStampItsC) STAMP(3 + 4 * it);
-        s1 = row_sum16(lv ? s1 : 0.0f);
-        s2 = row_sum16(lv ? s2 : 0.0f);
-        amax = row_min16(lv ? amax : 1e30f);
-        const float alpha_aff = fminf(1.0f, amax);
-        float sigma;
-        {
-            const float mu_aff = (sum_c + alpha_aff * s1 + alpha_aff * alpha_aff * s2) * inv_m2;
-            float sg = (mu > 0.0f) ? mu_aff / mu : 0.0f;
-            sg = fmaxf(sg, 0.0f);
-            sigma = fminf(sg * sg * sg, 1.0f);
-        }
-        // pass 1: Mehrotra corrector; pass 2 (teams whose step stayed below 0.1): pure centring safeguard
-        sigma_mu = sigma * mu;
-        eta = alpha_aff;
-        corrector_rhs();
-        {
-            float am, t1, t2;
-            forward(1, am, t1, t2);
-            am = row_min16(lv ? am : 1e30f);
-            alpha = fminf(1.0f, P.tau * am);
-        }
-        if (it < kStampItsC) STAMP(4 + 4 * it);
-        if (!__all(done || alpha >= 0.1f)) {
-            if (!done && alpha < 0.1f) {
-                sigma_mu = fmaxf(sigma, 0.3f) * mu;
-                eta = 0.0f;
-                corrector_rhs();
-                float am, t1, t2;
-                forward(2, am, t1, t2);
-                am = row_min16(lv ? am : 1e30f);
-                alpha = fminf(1.0f, P.tau * am);
+            });
+            amax = row_min16(lv ? amax : 1e30f);
+            if (pass == 0) {
+                s1 = row_sum16(lv ? s1 : 0.0f);
+                s2 = row_sum16(lv ? s2 : 0.0f);
+                alpha_aff = fminf(1.0f, amax);
+                const float mu_aff = (sum_c + alpha_aff * s1 + alpha_aff * alpha_aff * s2) * inv_m2;
+                float sg = (mu > 0.0f) ? mu_aff / mu : 0.0f;
+                sg = fmaxf(sg, 0.0f);
+                sigma = fminf(sg * sg * sg, 1.0f);
+                if (it < kStampItsC) STAMP(3 + 4 * it);
+            } else {
+                if (run) alpha = fminf(1.0f, P.tau * amax);
+                if (pass == 1 && it < kStampItsC) STAMP(4 + 4 * it);
             }
         }
         if (it < kStampItsC) STAMP(5 + 4 * it);
