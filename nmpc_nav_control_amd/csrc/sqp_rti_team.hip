@@ -231,7 +231,9 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
     for (int c = 0; c < M::NBX; c++)
         if (cx == c) { lo_b = P.lbx[c]; hi_b = P.ubx[c]; }
     // this lane's record of stage k: tbase + k * 16 * RS
-    float* const tbase = a.scratch + ((size_t)team * (N + 1) * 16 + r) * RS;
+    // idle slots (r >= NV) alias slot 0's record: their (unpredicated) loads then read valid data and touch no
+    // extra cache lines; they never store
+    float* const tbase = a.scratch + ((size_t)team * (N + 1) * 16 + (lv ? r : 0)) * RS;
     constexpr int KS = 16 * RS;
 
 #define XB(k, j) a.xbar[((size_t)(k) * NX + (j)) * S + inst]
@@ -409,19 +411,25 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
 #pragma unroll
         for (int i = 0; i < NX; i++) Gc[i] = (i < NGV) ? rc[R::GV + (i < NGV ? i : 0)] : gcol[i];
     };
-    // Stage sweep k = k0, k0 + dir, ..., k1: the next stage's record is loaded while body(k, rec) runs.
+    // Stage sweep k = k0, k0 + dir, ..., k1 with the next stage's record in flight while body(k, rec) runs.
+    // Two register buffers used in turn (the loop is unrolled by two) and loads that are never predicated:
+    // a conditional load or a buffer copy would make the compiler move the in-flight registers, which waits
+    // for the load. Lanes that do not sweep (idle slots, converged teams) re-read one fixed record instead.
     auto sweep = [&](int k0, int k1, int dir, bool ld, auto&& body) {
-        float nx[RS];
-#pragma unroll
-        for (int f = 0; f < RS; f++) nx[f] = 0.0f;
-        if (ld) rec_load<NQ>(tbase + (size_t)k0 * KS, nx);
-        for (int k = k0;; k += dir) {
-            float rc[RS];
-#pragma unroll
-            for (int f = 0; f < RS; f++) rc[f] = nx[f];
-            if (ld && k != k1) rec_load<NQ>(tbase + (size_t)(k + dir) * KS, nx);
-            body(k, rc);
+        const ptrdiff_t step = ld ? (ptrdiff_t)KS * dir : 0;
+        const float* p = tbase + (size_t)k0 * KS;
+        float ra[RS], rb[RS];
+        rec_load<NQ>(p, ra);
+        for (int k = k0;; k += 2 * dir) {
+            const float* p1 = (k == k1) ? p : p + step;
+            rec_load<NQ>(p1, rb);
+            body(k, ra);
             if (k == k1) break;
+            const float* p2 = (k + dir == k1) ? p1 : p1 + step;
+            rec_load<NQ>(p2, ra);
+            body(k + dir, rb);
+            if (k + dir == k1) break;
+            p = p2;
         }
     };
 
@@ -446,39 +454,37 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
             const bool vx = is_x && k >= 1;
             const bool valid = vu || vx;
             const bool bnd = valid && has_b;
+            // Branch-free: slots without a bound hold t = 1, lambda = 0, bounds 0 (written in P0), for which
+            // every bounded-variable term below is 0; only the step (a_upd masked) and res_ineq need masks.
             float z = rc[R::Z];
             float tl = rc[R::TL], tu = rc[R::TU], ll = rc[R::LL], lu = rc[R::LU];
             const float lb = rc[R::LB], ubd = rc[R::UB];
-            if (a_upd > 0.0f) {
+            {
                 const float dz = rc[R::DZ];
-                if (bnd) {
-                    const float rl = z - lb - tl, rr = ubd - z - tu;
-                    const float itl = frcp(tl), itu = frcp(tu);
-                    const BoundDir da = bound_dir(rc[R::DZA], rl, rr, tl, tu, ll, lu, itl, itu, 0.0f, 0.0f);
-                    const float tgl = sigma_mu - eta * da.dll * da.dtl, tgu = sigma_mu - eta * da.dlu * da.dtu;
-                    const BoundDir d = bound_dir(dz, rl, rr, tl, tu, ll, lu, itl, itu, tgl, tgu);
-                    tl += a_upd * d.dtl;
-                    tu += a_upd * d.dtu;
-                    ll += a_upd * d.dll;
-                    lu += a_upd * d.dlu;
-                }
-                if (valid) z += a_upd * dz;
+                const float rl = z - lb - tl, rr = ubd - z - tu;
+                const float itl = frcp(tl), itu = frcp(tu);
+                const BoundDir da = bound_dir(rc[R::DZA], rl, rr, tl, tu, ll, lu, itl, itu, 0.0f, 0.0f);
+                const float tgl = sigma_mu - eta * da.dll * da.dtl, tgu = sigma_mu - eta * da.dlu * da.dtu;
+                const BoundDir d = bound_dir(dz, rl, rr, tl, tu, ll, lu, itl, itu, tgl, tgu);
+                const float ab = bnd ? a_upd : 0.0f, av = valid ? a_upd : 0.0f;
+                tl += ab * d.dtl;
+                tu += ab * d.dtu;
+                ll += ab * d.dll;
+                lu += ab * d.dlu;
+                z += av * dz;
                 rc[R::Z] = z;
                 rc[R::TL] = tl;
                 rc[R::TU] = tu;
                 rc[R::LL] = ll;
                 rc[R::LU] = lu;
             }
-            float lamdiff = 0.0f, sig = 0.0f, gh = 0.0f;
-            if (bnd) {
-                const float rl = z - lb - tl, rr = ubd - z - tu;
-                const float itl = frcp(tl), itu = frcp(tu);
-                res_ineq = nan_max(res_ineq, fmaxf(fabsf(rl), fabsf(rr)));
-                sum_c += ll * tl + lu * tu;
-                lamdiff = ll - lu;
-                sig = ll * itl + lu * itu;
-                gh = ll * rl * itl + ll - lu * rr * itu - lu;
-            }
+            const float rl = z - lb - tl, rr = ubd - z - tu;
+            const float itl = frcp(tl), itu = frcp(tu);
+            res_ineq = nan_max(res_ineq, bnd ? fmaxf(fabsf(rl), fabsf(rr)) : 0.0f);
+            sum_c += ll * tl + lu * tu;
+            const float lamdiff = ll - lu;
+            const float sig = ll * itl + lu * itu;
+            const float gh = ll * rl * itl + ll - lu * rr * itu - lu;
             float Gc[NX];
             column(rc, Gc);
             // adjoint: c_v = sum_l G[l][v] pi_{k+1}[l]
@@ -486,15 +492,11 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
             const float hz = ((k < N) ? h_stage : we_lane) * z;
             const float g = rc[R::GR];
             const float base = hz + g - lamdiff + cpi;
-            float ghat = gh;
-            if (vu) {
-                rc[R::RU] = base;
-                res_stat = nan_max(res_stat, fabsf(base));
-                stat_scale = fmaxf(stat_scale, fmaxf(fabsf(cpi), fmaxf(fabsf(g), fabsf(lamdiff))));
-                ghat += base;
-            }
+            rc[R::RU] = base;  // read back for the u slots only
+            res_stat = nan_max(res_stat, vu ? fabsf(base) : 0.0f);
+            stat_scale = fmaxf(stat_scale, vu ? fmaxf(fabsf(cpi), fmaxf(fabsf(g), fabsf(lamdiff))) : 0.0f);
+            const float ghat = valid ? (vu ? gh + base : gh) : 0.0f;
             const float pi_new = vx ? base : 0.0f;
-            if (!valid) ghat = 0.0f;
             if (ghat != ghat || sig != sig) nanf_ = 1.0f;
             if (k == N) {
                 // terminal: P_N = diag(W_e + Sigma) on the state lanes
@@ -618,8 +620,8 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
                     const bool vu = is_u && k < N;
                     const bool vx = is_x && k >= 1;
                     const bool valid = vu || vx;
-                    float ghat = 0.0f;
-                    if (valid && has_b) {
+                    float ghat;
+                    {  // branch-free: slots without a bound give 0 (t = 1, lambda = 0, see P1)
                         const float z = rc[R::Z];
                         const float tl = rc[R::TL], tu = rc[R::TU], ll = rc[R::LL], lu = rc[R::LU];
                         const float rl = z - rc[R::LB] - tl, rr = rc[R::UB] - z - tu;
@@ -627,8 +629,9 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
                         const BoundDir da = bound_dir(rc[R::DZA], rl, rr, tl, tu, ll, lu, itl, itu, 0.0f, 0.0f);
                         const float tgl = sigma_mu - eta * da.dll * da.dtl, tgu = sigma_mu - eta * da.dlu * da.dtu;
                         ghat = -(tgl - ll * rl) * itl + ll + (tgu - lu * rr) * itu - lu;
+                        ghat = (valid && has_b) ? ghat : 0.0f;
                     }
-                    if (vu) ghat += rc[R::RU];
+                    ghat += vu ? rc[R::RU] : 0.0f;
                     if (k == N) {
                         pvc = is_x ? ghat : 0.0f;
                     } else {
@@ -680,8 +683,8 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
 #pragma unroll
                 for (int q = 0; q < NU; q++)
                     if (r == q) dz = du_all[q];
-                if (is_x) dz = (k >= 1) ? dxs : 0.0f;
-                if (valid && has_b) {
+                dz = is_x ? ((k >= 1) ? dxs : 0.0f) : dz;
+                {  // branch-free (slots without a bound: t = 1, lambda = 0); the step bound is masked
                     const float z = rc[R::Z];
                     const float tl = rc[R::TL], tu = rc[R::TU], ll = rc[R::LL], lu = rc[R::LU];
                     const float rl = z - rc[R::LB] - tl, rr = rc[R::UB] - z - tu;
@@ -693,11 +696,12 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
                         tgu = sigma_mu - eta * da.dlu * da.dtu;
                     }
                     const BoundDir d = bound_dir(dz, rl, rr, tl, tu, ll, lu, itl, itu, tgl, tgu);
-                    amax = step_bound_r(amax, tl, d.dtl);
-                    amax = step_bound_r(amax, tu, d.dtu);
-                    amax = step_bound_r(amax, ll, d.dll);
-                    amax = step_bound_r(amax, lu, d.dlu);
-                    if (pass == 0) {
+                    float am = step_bound_r(amax, tl, d.dtl);
+                    am = step_bound_r(am, tu, d.dtu);
+                    am = step_bound_r(am, ll, d.dll);
+                    am = step_bound_r(am, lu, d.dlu);
+                    amax = (valid && has_b) ? am : amax;
+                    if (pass == 0) {  // both sums vanish on unbounded slots at zero targets
                         s1 += ll * d.dtl + tl * d.dll + lu * d.dtu + tu * d.dlu;
                         s2 += d.dll * d.dtl + d.dlu * d.dtu;
                     }
