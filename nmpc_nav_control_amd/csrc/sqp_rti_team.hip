@@ -609,8 +609,10 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
             } else if (pass == 2) {
                 if (__all(done || alpha >= 0.1f)) break;
                 run = run && alpha < 0.1f;
-                sigma_mu = fmaxf(sigma, 0.3f) * mu;
-                eta = 0.0f;
+                // only the teams that take the safeguard step change their targets: the next P1 rebuilds the
+                // slack / multiplier step of every team from (DZ, DZA, sigma_mu, eta)
+                sigma_mu = run ? fmaxf(sigma, 0.3f) * mu : sigma_mu;
+                eta = run ? 0.0f : eta;
             }
             const bool ld = lv && run;
             if (pass > 0) {
