@@ -104,6 +104,7 @@ def cpu_baseline(fleets, dev, sample, ticks, nthreads):
     two closed loops. Returns (CPU instance-iterations/s, u0 max-abs err, failed, solves)."""
     from oracle.oracle import Oracle
     total_time, total_solves, err, fails = 0.0, 0, 0.0, 0
+    time_1, solves_1 = 0.0, 0
     host = lambda a: np.ascontiguousarray(a.cpu().numpy(), np.float64)  # noqa: E731
     for f in fleets:
         S = min(sample, f.B)
@@ -121,6 +122,14 @@ def cpu_baseline(fleets, dev, sample, ticks, nthreads):
             traj = np.ascontiguousarray(host(f.traj[:, :, :S]).transpose(2, 0, 1))
             tlen = np.ascontiguousarray(f.tlen[:S].cpu().numpy(), np.int32)
             f.solve()
+            # single-core rate on a slice of the same inputs (copies: batch_tick updates the iterate in place)
+            S1 = min(S, 64)
+            sl = lambda a: None if a is None else np.array(a[:S1])  # noqa: E731
+            t0 = time.perf_counter()
+            o.batch_tick(sl(pose), sl(vel), sl(steer), sl(traj), sl(tlen), None, sl(carried), sl(xbar), sl(ubar),
+                         nthreads=1)
+            time_1 += time.perf_counter() - t0
+            solves_1 += S1
             t0 = time.perf_counter()
             nf, cmd_o, u0_o, st_o, _ = o.batch_tick(pose, vel, steer, traj, tlen, None, carried, xbar, ubar,
                                                     nthreads=nthreads)
@@ -132,7 +141,7 @@ def cpu_baseline(fleets, dev, sample, ticks, nthreads):
             if ok.any():
                 err = max(err, float(np.abs(f.u0[:, :S].cpu().numpy().T[ok] - u0_o[ok]).max()))
             f.advance()
-    return total_solves / total_time, err, fails, total_solves
+    return total_solves / total_time, err, fails, total_solves, solves_1 / time_1
 
 
 def main():
@@ -239,11 +248,12 @@ def main():
         u0_err = None
         if not args.no_cpu_baseline and world == 1:
             nthreads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
-            cpu_rate, u0_err, nf, ns = cpu_baseline(fleets, dev, args.cpu_sample, args.cpu_ticks, nthreads)
+            cpu_rate, u0_err, nf, ns, rate_1 = cpu_baseline(fleets, dev, args.cpu_sample, args.cpu_ticks, nthreads)
             cpu = {"value": round(cpu_rate, 1), "unit": "SQP-RTI iterations/sec", "cores": nthreads, "kind": "port",
                    "sample": f"{ns} instance-iterations: first {args.cpu_sample} robots of each model x "
                              f"{args.cpu_ticks} closed-loop ticks after the timed region, fp64 oracle/nmpc_oracle.c, "
-                             f"OpenMP {nthreads} threads, identical inputs", "failed": nf}
+                             f"OpenMP {nthreads} threads, identical inputs", "failed": nf,
+                   "value_1core": round(rate_1, 1)}
         result = {
             "metric": "SQP-RTI iterations/sec (whole node), diff N=40 batch=4096; u0 max-abs err",
             "value": round(value, 1), "unit": "SQP-RTI iterations/sec", "n_gpus": world, "steps": args.steps,

@@ -1,0 +1,110 @@
+"""GPU tests of the drop-in acados capsule ABI (include/acados_solver_{name}.h + acados_c/ocp_nlp_interface.h).
+
+The controller mirrors in nmpc_nav_control_amd/controller.py drive the capsule exactly as the reference's
+wrappers do (create, ocp_nlp_constraints_model_set / cost_model_set, {name}_acados_solve, ocp_nlp_out_get,
+ocp_nlp_get "time_tot", reset); the fp64 oracle replays the same wrapper semantics (prepare -> sqp_rti -> post)
+on the same inputs. Tolerance as in test_gpu_parity.py: |u0 - u0_oracle| <= 1e-3 and commands alike.
+"""
+import numpy as np
+import pytest
+
+from nmpc_nav_control_amd.controller import (CmdVelDiff, CmdVelOmni4, CmdVelTric, NMPCNavControlDiff,
+                                             NMPCNavControlOmni4, NMPCNavControlTric, Pose, Vel, batch_solve)
+from oracle.oracle import Oracle
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-3
+N = 20
+W_DIFF = [10, 10, 5, 0, 0, 0, 0, 1, 1]
+W_OMNI = [10, 10, 5] + [0] * 8 + [1, 1, 1, 1]
+
+
+def make(model):
+    if model == "diff":
+        return NMPCNavControlDiff(1 / 40, 0.270, 0.1, 1.0, 1.0, W_DIFF, N=N), CmdVelDiff
+    if model == "omni4":
+        return NMPCNavControlOmni4(1 / 40, 0.535, 0.1, 1.0, 1.0, W_OMNI, N=N), CmdVelOmni4
+    d2r = np.pi / 180
+    return NMPCNavControlTric(1 / 40, 0.270, 0.1, 0.5, 1.0, 1.0, -45 * d2r, 45 * d2r, 15 * d2r, W_DIFF, N=N), CmdVelTric
+
+
+def plant(model, o, x0, u0):
+    xn, _, _ = o.rk4(x0, u0, 1 / 40)
+    if model == "diff":
+        vel = (0.5 * (xn[3] + xn[4]), 0.0, (xn[4] - xn[3]) / 0.270)
+        return xn, vel, 0.0
+    if model == "omni4":
+        v = 0.25 * (xn[3] - xn[4] + xn[5] - xn[6])
+        vn = 0.25 * (-xn[3] - xn[4] + xn[5] + xn[6])
+        w = -(xn[3] + xn[4] + xn[5] + xn[6]) / (2 * 0.535)
+        return xn, (v, vn, w), 0.0
+    return xn, (xn[3], 0.0, 0.0), xn[4]
+
+
+def path(t0, n):
+    """A gentle arc of n reference poses ahead of time t0 (crosses +-pi in theta to exercise the unwrap)."""
+    s = 0.02 * (t0 + np.arange(1, n + 1))
+    th = 3.0 + 0.8 * s
+    th = (th + np.pi) % (2 * np.pi) - np.pi
+    return [Pose(0.3 * np.cos(0.8 * si), 0.3 * np.sin(0.8 * si), thi) for si, thi in zip(s, th)]
+
+
+@pytest.mark.parametrize("model", ["diff", "omni4", "tric"])
+def test_capsule_closed_loop_matches_oracle(built, model):
+    ctl, Cmd = make(model)
+    assert ctl.getHorizon() == N
+    o = Oracle(model, N)
+    xb, ub = o.iterate_create()
+    carried = np.zeros(o.nbx)
+    pose, vel, steer = np.array([0.05, -0.02, 2.9]), np.array([0.1, 0.0, 0.05]), 0.0
+    if model == "tric":
+        ctl.setSteeringWheelAngle(steer)
+    for tick in range(8):
+        refs = path(tick, N - 3 + tick % 4)  # sometimes shorter than N+1: exercises the padding
+        cmd = Cmd()
+        ok, ms = ctl.run(Pose(*pose), Vel(*vel), refs, cmd)
+        assert ok and ms >= 0.0
+        traj = np.array([[p.x, p.y, p.theta] for p in refs])
+        x0, yref, We = o.prepare(pose, vel, steer, traj, carried)
+        s, st, xb, ub = o.sqp_rti(xb, ub, x0, yref, We)
+        assert s == 0
+        cmd_o, carried = o.post(x0, ub[0])
+        np.testing.assert_allclose(ctl.u0, ub[0], atol=TOL)
+        got = [cmd.v, cmd.w] if model == "diff" else ([cmd.v, cmd.vn, cmd.w] if model == "omni4" else [cmd.v, cmd.alpha])
+        np.testing.assert_allclose(got, cmd_o[:len(got)], atol=TOL)
+        xn, v3, steer = plant(model, o, x0, ub[0])
+        pose, vel = xn[:3], np.array(v3)
+        if model == "tric":
+            ctl.setSteeringWheelAngle(steer)
+    # reset_mpc zeroes the iterate (acados reset semantics)
+    assert ctl.reset_mpc()
+    xs, us = ctl.iterate()
+    assert not xs.any() and not us.any()
+
+
+def test_capsule_errors_raise(built):
+    ctl, Cmd = make("diff")
+    with pytest.raises(RuntimeError, match="Invalid command velocity type"):
+        ctl.run(Pose(), Vel(), path(0, N + 1), CmdVelOmni4())
+
+
+def test_batch_solve_equals_individual(built):
+    """{name}_acados_batch_solve of many capsules = one solve per capsule."""
+    ctls = [make("diff")[0] for _ in range(6)]
+    twins = [make("diff")[0] for _ in range(6)]
+    for i, (a, b) in enumerate(zip(ctls, twins)):
+        x0 = np.array([0.1 * i, -0.05 * i, 0.3 * i, 0.1, -0.1, 0.05 * i, -0.05 * i])
+        for c in (a, b):
+            c._cset(0, "lbx", x0)
+            c._cset(0, "ubx", x0)
+            c.yref[:, :3] = [0.4, 0.2 * i, 0.1]
+            for k in range(N + 1):
+                c._wset(k, "yref", c.yref[k, : (c.nx if k == N else c.ny)])
+    status = batch_solve(ctls)
+    assert (status == 0).all()
+    for a, b in zip(ctls, twins):
+        b._solve()
+        xa, ua = a.iterate()
+        xb_, ub_ = b.iterate()
+        np.testing.assert_allclose(ua, ub_, atol=1e-6)
+        np.testing.assert_allclose(xa, xb_, atol=1e-6)
