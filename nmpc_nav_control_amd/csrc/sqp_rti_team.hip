@@ -61,6 +61,7 @@ namespace {
 
 constexpr float kBreakdownMuT = 1e-6f;
 constexpr float kStatRelT = 1e-5f;
+constexpr float kFar = 1e30f;  // sentinel bound / slack of unbounded slots (z + kFar - kFar == 0 in fp32)
 #ifdef NMPC_STAMPS
 constexpr int kStampItsC = kStampIts;
 #else
@@ -345,8 +346,13 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
         // iterate, bounds, slacks, multipliers
         const float z = vx ? dx : 0.0f;
         rec[R::Z] = z;
-        rec[R::TL] = 1.0f;
-        rec[R::TU] = 1.0f;
+        // slots without a bound (or outside their stage range) get a sentinel bound at +-kFar with slack kFar
+        // and zero multipliers: every bounded-variable expression of the sweeps then vanishes on them (r = 0,
+        // Sigma = 0, no step bound), so the sweeps need no per-lane branches
+        rec[R::TL] = kFar;
+        rec[R::TU] = kFar;
+        rec[R::LB] = -kFar;
+        rec[R::UB] = kFar;
         if (valid && has_b) {
             const float lb = lo_b - zbar, ubd = hi_b - zbar;
             const float tl = fmaxf(z - lb, P.thr0), tu = fmaxf(ubd - z, P.thr0);
@@ -454,8 +460,8 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
             const bool vx = is_x && k >= 1;
             const bool valid = vu || vx;
             const bool bnd = valid && has_b;
-            // Branch-free: slots without a bound hold t = 1, lambda = 0, bounds 0 (written in P0), for which
-            // every bounded-variable term below is 0; only the step (a_upd masked) and res_ineq need masks.
+            // Branch-free: slots without a bound hold the kFar sentinel (P0), for which every bounded-variable
+            // term below is 0; only the slack / multiplier step is masked (it would move lambda off zero).
             float z = rc[R::Z];
             float tl = rc[R::TL], tu = rc[R::TU], ll = rc[R::LL], lu = rc[R::LU];
             const float lb = rc[R::LB], ubd = rc[R::UB];
@@ -480,7 +486,7 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
             }
             const float rl = z - lb - tl, rr = ubd - z - tu;
             const float itl = frcp(tl), itu = frcp(tu);
-            res_ineq = nan_max(res_ineq, bnd ? fmaxf(fabsf(rl), fabsf(rr)) : 0.0f);
+            res_ineq = nan_max(res_ineq, fmaxf(fabsf(rl), fabsf(rr)));
             sum_c += ll * tl + lu * tu;
             const float lamdiff = ll - lu;
             const float sig = ll * itl + lu * itu;
@@ -623,7 +629,7 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
                     const bool vx = is_x && k >= 1;
                     const bool valid = vu || vx;
                     float ghat;
-                    {  // branch-free: slots without a bound give 0 (t = 1, lambda = 0, see P1)
+                    {  // branch-free: 0 on the kFar-sentinel slots (see P0)
                         const float z = rc[R::Z];
                         const float tl = rc[R::TL], tu = rc[R::TU], ll = rc[R::LL], lu = rc[R::LU];
                         const float rl = z - rc[R::LB] - tl, rr = rc[R::UB] - z - tu;
@@ -631,7 +637,6 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
                         const BoundDir da = bound_dir(rc[R::DZA], rl, rr, tl, tu, ll, lu, itl, itu, 0.0f, 0.0f);
                         const float tgl = sigma_mu - eta * da.dll * da.dtl, tgu = sigma_mu - eta * da.dlu * da.dtu;
                         ghat = -(tgl - ll * rl) * itl + ll + (tgu - lu * rr) * itu - lu;
-                        ghat = (valid && has_b) ? ghat : 0.0f;
                     }
                     ghat += vu ? rc[R::RU] : 0.0f;
                     if (k == N) {
@@ -686,7 +691,7 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
                 for (int q = 0; q < NU; q++)
                     if (r == q) dz = du_all[q];
                 dz = is_x ? ((k >= 1) ? dxs : 0.0f) : dz;
-                {  // branch-free (slots without a bound: t = 1, lambda = 0); the step bound is masked
+                {  // branch-free: the kFar-sentinel slots bound no step and add nothing to s1, s2
                     const float z = rc[R::Z];
                     const float tl = rc[R::TL], tu = rc[R::TU], ll = rc[R::LL], lu = rc[R::LU];
                     const float rl = z - rc[R::LB] - tl, rr = rc[R::UB] - z - tu;
@@ -698,12 +703,11 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
                         tgu = sigma_mu - eta * da.dlu * da.dtu;
                     }
                     const BoundDir d = bound_dir(dz, rl, rr, tl, tu, ll, lu, itl, itu, tgl, tgu);
-                    float am = step_bound_r(amax, tl, d.dtl);
-                    am = step_bound_r(am, tu, d.dtu);
-                    am = step_bound_r(am, ll, d.dll);
-                    am = step_bound_r(am, lu, d.dlu);
-                    amax = (valid && has_b) ? am : amax;
-                    if (pass == 0) {  // both sums vanish on unbounded slots at zero targets
+                    amax = step_bound_r(amax, tl, d.dtl);
+                    amax = step_bound_r(amax, tu, d.dtu);
+                    amax = step_bound_r(amax, ll, d.dll);
+                    amax = step_bound_r(amax, lu, d.dlu);
+                    if (pass == 0) {  // dll = dlu = 0 on sentinel slots at zero targets
                         s1 += ll * d.dtl + tl * d.dll + lu * d.dtu + tu * d.dlu;
                         s2 += d.dll * d.dtl + d.dlu * d.dtu;
                     }
