@@ -34,8 +34,16 @@ __device__ unsigned long long g_stamps[256][2 + 4 * kStampIts];
     do {                                                                                                         \
         if (r == 0 && (team & 3) == 0 && (team >> 2) < 256) g_stamps[team >> 2][(slot)] = __builtin_amdgcn_s_memtime(); \
     } while (0)
+// fine-grained stamps inside one P1 stage body (iteration 2, stage 20)
+__device__ unsigned long long g_stamps_p1[256][8];
+#define STAMPF(slot)                                                                                             \
+    do {                                                                                                         \
+        if (it == 2 && k == 20 && r == 0 && (team & 3) == 0 && (team >> 2) < 256)                                 \
+            g_stamps_p1[team >> 2][(slot)] = __builtin_amdgcn_s_memtime();                                        \
+    } while (0)
 #else
 #define STAMP(slot) ((void)0)
+#define STAMPF(slot) ((void)0)
 #endif
 
 template <class M>
@@ -417,11 +425,12 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
 #pragma unroll
         for (int i = 0; i < NX; i++) Gc[i] = (i < NGV) ? rc[R::GV + (i < NGV ? i : 0)] : gcol[i];
     };
-    // Stage sweep k = k0, k0 + dir, ..., k1 with the next stage's record in flight while body(k, rec) runs.
-    // Two register buffers used in turn (the loop is unrolled by two) and loads that are never predicated:
-    // a conditional load or a buffer copy would make the compiler move the in-flight registers, which waits
-    // for the load. Lanes that do not sweep (idle slots, converged teams) re-read one fixed record instead.
-    auto sweep = [&](int k0, int k1, int dir, bool ld, auto&& body) {
+    // Stage sweeps k = k0, k0 + dir, ..., k1 with the next stage's record (sweep2: the next two) in flight while
+    // body(k, rec) runs. The loop is unrolled by the number of register buffers, which are used in turn (no
+    // copies between them), and the loads are never predicated: a conditional load or a buffer copy would make
+    // the compiler move the in-flight registers, which waits for the load. Lanes that do not sweep (idle slots,
+    // converged teams) re-read one fixed record instead; past k1 the pointer stays on k1.
+    auto sweep = [&](int k0, int k1, int dir, bool ld, auto&& body) {  // 2 buffers (compute-heavy P1)
         const ptrdiff_t step = ld ? (ptrdiff_t)KS * dir : 0;
         const float* p = tbase + (size_t)k0 * KS;
         float ra[RS], rb[RS];
@@ -436,6 +445,32 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
             body(k + dir, rb);
             if (k + dir == k1) break;
             p = p2;
+        }
+    };
+    auto sweep3 = [&](int k0, int k1, int dir, bool ld, auto&& body) {  // 3 buffers (light sweeps)
+        const ptrdiff_t step = ld ? (ptrdiff_t)KS * dir : 0;
+        auto nxt = [&](const float* q, int kq) { return (kq == k1) ? q : q + step; };
+        auto kn = [&](int kq) { return (kq == k1) ? kq : kq + dir; };
+        const float* p0 = tbase + (size_t)k0 * KS;
+        const float* p1 = nxt(p0, k0);
+        float ra[RS], rb[RS], rc3[RS];
+        rec_load<NQ>(p0, ra);
+        rec_load<NQ>(p1, rb);
+        for (int k = k0;; k += 3 * dir) {
+            const int ka = kn(k), kb = kn(ka), kc = kn(kb);  // stages held by rb, rc3 (after load), next ra
+            const float* p2 = nxt(p1, ka);
+            rec_load<NQ>(p2, rc3);
+            body(k, ra);
+            if (k == k1) break;
+            const float* p3 = nxt(p2, kb);
+            rec_load<NQ>(p3, ra);
+            body(k + dir, rb);
+            if (k + dir == k1) break;
+            const float* p4 = nxt(p3, kc);
+            rec_load<NQ>(p4, rb);
+            body(k + 2 * dir, rc3);
+            if (k + 2 * dir == k1) break;
+            p1 = p4;
         }
     };
 
@@ -456,6 +491,7 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
         const bool act = lv && !done;
         const float a_upd = (it > 0 && !done) ? alpha : 0.0f;
         sweep(N, 0, -1, act, [&](int k, float (&rc)[RS]) {
+            STAMPF(0);
             const bool vu = is_u && k < N;
             const bool vx = is_x && k >= 1;
             const bool valid = vu || vx;
@@ -491,6 +527,7 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
             const float lamdiff = ll - lu;
             const float sig = ll * itl + lu * itu;
             const float gh = ll * rl * itl + ll - lu * rr * itu - lu;
+            STAMPF(1);
             float Gc[NX];
             column(rc, Gc);
             // adjoint: c_v = sum_l G[l][v] pi_{k+1}[l]
@@ -518,7 +555,9 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
                 double lba[NX];
 #pragma unroll
                 for (int i = 0; i < NX; i++) lba[i] = 0.0;
+                STAMPF(2);
                 lba_block<NX, NU>(lba, Lrow, Gd);
+                STAMPF(3);
                 // row r of M = D + LBA' LBA, then its right-looking row-distributed Cholesky in fp64: column j's
                 // pivot comes from lane j, every later column is updated by one fused block
                 const double dg = valid ? (double)h_stage + (double)sig : 1.0;
@@ -526,6 +565,7 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
 #pragma unroll
                 for (int j = 0; j < NV; j++) Lr[j] = (r == j) ? dg : 0.0;
                 mrow_block<NX, NU>(Lr, md, lba);  // md[j] = M[j][j] (lane j's diagonal), md[0] = first pivot
+                STAMPF(4);
                 double pivot = md[0];
                 sfor<0, NV>([&](auto jc) {
                     constexpr int j = decltype(jc)::value;
@@ -542,6 +582,7 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
                     // right-looking update M[r][j'] -= L[r][j] L[j'][j] (j' > j) and the next pivot
                     if constexpr (j + 1 < NV) chol_update<NX, NU, j>(Lr, lj, pivot);
                 });
+                STAMPF(5);
                 float Lm[NU];
 #pragma unroll
                 for (int q = 0; q < NU; q++) {
@@ -563,7 +604,9 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
                 for (int j = 0; j < NV; j++) Lrow[j] = Lr[j];
             }
             piv = pi_new;
+            STAMPF(6);
             if (act) rec_store<NQ>(tbase + (size_t)k * KS, rc);
+            STAMPF(7);
         });
         if (it < kStampItsC) STAMP(2 + 4 * it);
         // team reductions
@@ -624,7 +667,7 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
             if (pass > 0) {
                 // corrector rhs through the stored factorisation (backward)
                 float pvc = 0.0f;
-                sweep(N, 0, -1, ld, [&](int k, float (&rc)[RS]) {
+                sweep3(N, 0, -1, ld, [&](int k, float (&rc)[RS]) {
                     const bool vu = is_u && k < N;
                     const bool vx = is_x && k >= 1;
                     const bool valid = vu || vx;
@@ -661,7 +704,7 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
             }
             // forward: du from the stored factor, dz, bounded-variable directions, next-stage dx
             float dxs = 0.0f, amax = 1e30f, s1 = 0.0f, s2 = 0.0f;
-            sweep(0, N, 1, ld, [&](int k, float (&rc)[RS]) {
+            sweep3(0, N, 1, ld, [&](int k, float (&rc)[RS]) {
                 const bool vu = is_u && k < N;
                 const bool vx = is_x && k >= 1;
                 const bool valid = vu || vx;
@@ -806,6 +849,10 @@ template size_t team_scratch_floats<Omni4>(int, int);
 template size_t team_scratch_floats<Tric3>(int, int);
 
 #ifdef NMPC_STAMPS
+extern "C" int nmpc_debug_stamps_p1(unsigned long long* host)
+{
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_stamps_p1), sizeof(g_stamps_p1), 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -2;
+}
 extern "C" int nmpc_debug_stamps(unsigned long long* host, int n)
 {
     const size_t bytes = sizeof(unsigned long long) * (size_t)n;
