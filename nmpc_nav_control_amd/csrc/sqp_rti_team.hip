@@ -288,24 +288,57 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
     // ---- P0: linearisation (lane v: nominal step + column v), gradient, bounds, feasible initial iterate --
     const int len = (mode == kModeRun) ? (a.traj_len ? a.traj_len[inst] : N + 1) : 0;
     float ref_x = 0.0f, ref_y = 0.0f, ref_t = pose_th, prv_x = 0.0f, prv_y = 0.0f, prv_t = 0.0f;
-    float gcol[NX];  // column v of [B A]; rows >= NGV are constant for the launch
+    // Iterate rows are read two stages ahead (every lane of a team reads the same addresses: one request per
+    // wave), the reference row likewise.
+    auto load_row = [&](int k, float (&xr)[NX], float (&ur)[NU], float (&tr)[3]) {
+        const int kk = k <= N ? k : N;
 #pragma unroll
-    for (int i = 0; i < NX; i++) gcol[i] = 0.0f;
+        for (int j = 0; j < NX; j++) xr[j] = XB(kk, j);
+        const int ku = kk < N ? kk : N - 1;
+#pragma unroll
+        for (int j = 0; j < NU; j++) ur[j] = UBAR(ku, j);
+        if (mode == kModeRun) {
+            const int kt = kk < len ? kk : (len > 0 ? len - 1 : 0);
+#pragma unroll
+            for (int j = 0; j < 3; j++) tr[j] = a.traj[((size_t)kt * 3 + j) * Bn + inst];
+        } else {
+            tr[0] = tr[1] = tr[2] = 0.0f;
+        }
+    };
+    float xb[NX], ub[NU], tr[3], xb1[NX], ub1[NU], tr1[3];
+    load_row(0, xb, ub, tr);
+    load_row(1, xb1, ub1, tr1);
+    // constant rows of [B A] (rows >= NGV) from stage 0, before the sweep: lane v holds column v (gcol), lane
+    // NU+xi holds row xi (grow), so the initial-iterate dynamics below need only NGV row sums
+    float gcol[NX], grow[NV];
+    {
+        float xn0[NX], g0[NX];
+        rk4_column<M>(xb, ub, P, lv ? r : NU, xn0, g0);
+#pragma unroll
+        for (int i = 0; i < NX; i++) gcol[i] = (lv && i >= NGV) ? g0[i] : 0.0f;
+        sfor<0, NV>([&](auto vc) {
+            constexpr int v = decltype(vc)::value;
+            float sv = 0.0f;
+#pragma unroll
+            for (int i = NGV; i < NX; i++) {
+                const float t = bc<v>(gcol[i]);
+                if (is_x && xi == i) sv = t;
+            }
+            grow[v] = sv;
+        });
+    }
     float dx = is_x ? x0_lane - XB(0, xi) : 0.0f;  // this lane's state delta at the current stage
     for (int k = 0; k <= N; k++) {
-        float xb[NX], ub[NU];
-#pragma unroll
-        for (int j = 0; j < NX; j++) xb[j] = XB(k, j);
-#pragma unroll
-        for (int j = 0; j < NU; j++) ub[j] = (k < N) ? UBAR(k, j) : 0.0f;
+        float xb2[NX], ub2[NU], tr2[3];
+        load_row(k + 2, xb2, ub2, tr2);  // two stages ahead (clamped)
         // stage reference of this lane: run mode unwraps + pads the pose refs (NMPCNavControlDiff.cpp:104-118),
         // entries >= 3 of yref are left at zero
         float yr = 0.0f;
         if (mode == kModeRun) {
             if (k < len) {
-                ref_x = a.traj[((size_t)k * 3 + 0) * Bn + inst];
-                ref_y = a.traj[((size_t)k * 3 + 1) * Bn + inst];
-                float th = a.traj[((size_t)k * 3 + 2) * Bn + inst];
+                ref_x = tr[0];
+                ref_y = tr[1];
+                float th = tr[2];
                 const float d = th - ref_t;
                 if (d > kPi) th -= 2.0f * kPi;
                 else if (d < -kPi) th += 2.0f * kPi;
@@ -324,10 +357,6 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
 #pragma unroll
         for (int i = 0; i < NX; i++) { xn[i] = 0.0f; g[i] = 0.0f; }
         if (k < N) rk4_column<M>(xb, ub, P, lv ? r : NU, xn, g);
-        if (k == 0) {
-#pragma unroll
-            for (int i = NGV; i < NX; i++) gcol[i] = lv ? g[i] : 0.0f;
-        }
         const bool vu = is_u && k < N, vx = is_x && k >= 1;
         const bool valid = vu || vx;
         float zbar = 0.0f;
@@ -374,33 +403,29 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
 #pragma unroll
         for (int i = 0; i < NGV; i++) rec[R::GV + i] = (k < N && lv) ? g[i] : 0.0f;
         if (lv) rec_store<NQ>(tbase + (size_t)k * KS, rec);
-        // dynamics-feasible initial states: dx_{k+1} = A dx_k + b_k (inputs start at du = 0, dx_0 = x0 - xbar_0)
+        // dynamics-feasible initial states: dx_{k+1} = A dx_k + b_k (inputs start at du = 0, dx_0 = x0 - xbar_0);
+        // row i of [B A] dz: NGV row sums over the columns + the constant rows held in grow
         if (k < N) {
             const float dzd = is_x ? dx : 0.0f;
-            float nxt = 0.0f, bk = 0.0f;
+            float nxt = dot_v<NX, NU>(0.0f, dzd, grow);
+            float bk = 0.0f;
 #pragma unroll
-            for (int i = 0; i < NX; i++) {
-                const float s = row_sum16(lv ? g[i] * dzd : 0.0f);
-                if (xi == i) {
-                    nxt = s;
-                    bk = xn[i] - XB(k + 1, i);
-                }
+            for (int i = 0; i < NGV; i++) {
+                const float sr = row_sum16(lv ? g[i] * dzd : 0.0f);
+                if (xi == i) nxt = sr;
             }
+#pragma unroll
+            for (int i = 0; i < NX; i++)
+                if (xi == i) bk = xn[i] - xb1[i];
             dx = is_x ? nxt + bk : 0.0f;
         }
-    }
-    // row xi of the constant rows of [B A] (lane NU+xi, xi >= NGV): grow[v] = G[xi][v], from lane v's column
-    float grow[NV];
-    sfor<0, NV>([&](auto vc) {
-        constexpr int v = decltype(vc)::value;
-        float s = 0.0f;
 #pragma unroll
-        for (int i = NGV; i < NX; i++) {
-            const float t = bc<v>(gcol[i]);
-            if (is_x && xi == i) s = t;
-        }
-        grow[v] = s;
-    });
+        for (int j = 0; j < NX; j++) { xb[j] = xb1[j]; xb1[j] = xb2[j]; }
+#pragma unroll
+        for (int j = 0; j < NU; j++) { ub[j] = ub1[j]; ub1[j] = ub2[j]; }
+#pragma unroll
+        for (int j = 0; j < 3; j++) { tr[j] = tr1[j]; tr1[j] = tr2[j]; }
+    }
     double gcol64[NX];
 #pragma unroll
     for (int i = 0; i < NX; i++) gcol64[i] = (double)gcol[i];
