@@ -69,6 +69,9 @@ namespace {
 
 constexpr float kBreakdownMuT = 1e-6f;
 constexpr float kStatRelT = 1e-5f;
+#ifndef LIGHT_D
+#define LIGHT_D 4  // record buffers of the light (solve-only) sweeps
+#endif
 constexpr float kFar = 1e30f;  // sentinel bound / slack of unbounded slots (z + kFar - kFar == 0 in fp32)
 #ifdef NMPC_STAMPS
 constexpr int kStampItsC = kStampIts;
@@ -472,33 +475,38 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
             p = p2;
         }
     };
-    auto sweep3 = [&](int k0, int k1, int dir, bool ld, auto&& body) {  // 3 buffers (light sweeps)
+    // D buffers: buf[i] holds stage k + i*dir while the loop is at k; after body(k + i*dir) it is refilled with
+    // stage k + (i + D)*dir (clamped at k1), so D - 1 records are in flight during every body
+    auto sweepd = [&](auto dc, int k0, int k1, int dir, bool ld, auto&& body) {
+        constexpr int D = decltype(dc)::value;
         const ptrdiff_t step = ld ? (ptrdiff_t)KS * dir : 0;
-        auto nxt = [&](const float* q, int kq) { return (kq == k1) ? q : q + step; };
-        auto kn = [&](int kq) { return (kq == k1) ? kq : kq + dir; };
-        const float* p0 = tbase + (size_t)k0 * KS;
-        const float* p1 = nxt(p0, k0);
-        float ra[RS], rb[RS], rc3[RS];
-        rec_load<NQ>(p0, ra);
-        rec_load<NQ>(p1, rb);
-        for (int k = k0;; k += 3 * dir) {
-            const int ka = kn(k), kb = kn(ka), kc = kn(kb);  // stages held by rb, rc3 (after load), next ra
-            const float* p2 = nxt(p1, ka);
-            rec_load<NQ>(p2, rc3);
-            body(k, ra);
-            if (k == k1) break;
-            const float* p3 = nxt(p2, kb);
-            rec_load<NQ>(p3, ra);
-            body(k + dir, rb);
-            if (k + dir == k1) break;
-            const float* p4 = nxt(p3, kc);
-            rec_load<NQ>(p4, rb);
-            body(k + 2 * dir, rc3);
-            if (k + 2 * dir == k1) break;
-            p1 = p4;
+        float buf[D][RS];
+        const float* p = tbase + (size_t)k0 * KS;
+        int kl = k0;
+        rec_load<NQ>(p, buf[0]);
+        sfor<1, D>([&](auto ic) {
+            constexpr int i = decltype(ic)::value;
+            p = (kl == k1) ? p : p + step;
+            kl = (kl == k1) ? kl : kl + dir;
+            rec_load<NQ>(p, buf[i]);
+        });
+        for (int k = k0;; k += D * dir) {
+            bool stop = false;
+            sfor<0, D>([&](auto ic) {
+                constexpr int i = decltype(ic)::value;
+                if (stop) return;
+                body(k + i * dir, buf[i]);
+                if (k + i * dir == k1) {
+                    stop = true;
+                    return;
+                }
+                p = (kl == k1) ? p : p + step;
+                kl = (kl == k1) ? kl : kl + dir;
+                rec_load<NQ>(p, buf[i]);
+            });
+            if (stop) break;
         }
     };
-
     // ---- interior-point iterations ----------------------------------------------------------------------
     int status = 0, it_done = 0;
     bool done = false;
@@ -600,9 +608,12 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
                         if (!(pivot > 0.0)) fail = true;
                         rd = drsq(fmax(pivot, 1e-300));
                     } else {
-                        rd = (pivot > 1e-10 * (1.0 + fabs(md[j]))) ? drsq(pivot) : 0.0;  // PSD state block
+                        // PSD state block: pivot > 1e-10 (1 + |M_jj|)
+                        rd = (fma(-1e-10, fabs(md[j]), pivot) > 1e-10) ? drsq(pivot) : 0.0;
                     }
-                    const double lj = (r >= j) ? s * rd : 0.0;  // lane j: s == pivot
+                    // lane j: s == pivot. Rows r < j keep unmasked upper-triangle entries in the state columns
+                    // (~0, read only by row r itself); the input columns are stored (LM) and must be exact
+                    const double lj = (j >= NU || r >= j) ? s * rd : 0.0;
                     Lr[j] = lj;
                     // right-looking update M[r][j'] -= L[r][j] L[j'][j] (j' > j) and the next pivot
                     if constexpr (j + 1 < NV) chol_update<NX, NU, j>(Lr, lj, pivot);
@@ -692,10 +703,8 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
             if (pass > 0) {
                 // corrector rhs through the stored factorisation (backward)
                 float pvc = 0.0f;
-                sweep3(N, 0, -1, ld, [&](int k, float (&rc)[RS]) {
+                sweepd(std::integral_constant<int, LIGHT_D>{}, N, 0, -1, ld, [&](int k, float (&rc)[RS]) {
                     const bool vu = is_u && k < N;
-                    const bool vx = is_x && k >= 1;
-                    const bool valid = vu || vx;
                     float ghat;
                     {  // branch-free: 0 on the kFar-sentinel slots (see P0)
                         const float z = rc[R::Z];
@@ -729,7 +738,7 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
             }
             // forward: du from the stored factor, dz, bounded-variable directions, next-stage dx
             float dxs = 0.0f, amax = 1e30f, s1 = 0.0f, s2 = 0.0f;
-            sweep3(0, N, 1, ld, [&](int k, float (&rc)[RS]) {
+            sweepd(std::integral_constant<int, LIGHT_D>{}, 0, N, 1, ld, [&](int k, float (&rc)[RS]) {
                 const bool vu = is_u && k < N;
                 const bool vx = is_x && k >= 1;
                 const bool valid = vu || vx;
