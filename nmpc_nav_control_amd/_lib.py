@@ -49,7 +49,7 @@ BATCH_SYMBOLS = [
     "nmpc_model_dims", "nmpc_model_params_default", "nmpc_model_params_set_limits", "nmpc_batch_create",
     "nmpc_batch_destroy", "nmpc_batch_set_params", "nmpc_batch_get_params", "nmpc_batch_init_iterate",
     "nmpc_batch_solve", "nmpc_batch_run", "nmpc_batch_state", "nmpc_batch_set_kernel", "nmpc_fleet_sim_step",
-    "nmpc_last_error", "nmpc_version",
+    "nmpc_last_error", "nmpc_version", "nmpc_path_discretize",
 ]
 KERNELS = {"team": 0, "lane": 1}
 NLP_SYMBOLS = ["ocp_nlp_constraints_model_set", "ocp_nlp_cost_model_set", "ocp_nlp_out_get", "ocp_nlp_out_set",
@@ -90,6 +90,7 @@ def lib():
     L.nmpc_batch_set_kernel.argtypes = [vp, i]
     L.nmpc_batch_state.argtypes = [vp, ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.POINTER(vp), c_int_p]
     L.nmpc_fleet_sim_step.argtypes = [vp, i, vp, vp, vp, vp, vp, vp, vp, vp, vp, i, vp]
+    L.nmpc_path_discretize.argtypes = [i, vp, i, vp, vp, ctypes.c_double, i, i, vp, vp, vp]
     L.nmpc_last_error.restype = ctypes.c_char_p
     L.nmpc_version.restype = ctypes.c_char_p
     for name in MODEL_NAMES.values():

@@ -1,5 +1,6 @@
 // nmpc_batch.cpp -- C ABI of the batched solve path (include/nmpc_amd/nmpc_batch.h).
 #include "nmpc_amd/nmpc_batch.h"
+#include "nmpc_amd/nmpc_path.h"
 
 #include <hip/hip_runtime.h>
 
@@ -396,6 +397,21 @@ int nmpc_fleet_sim_step(nmpc_batch* b, int B, const float* path, float* s, float
         break;
     }
     return hip_err(e, "fleet_sim launch");
+}
+
+int nmpc_path_discretize(int B, const nmpc_path_segment* segs, int seg_stride, const int* nseg,
+                         const double* nearest_u, double sample_period, int num_poses, int is_holonomic,
+                         float* traj, double* traj64, void* stream)
+{
+    if (B < 0) return set_err(NMPC_ERR_ARG, "B < 0");
+    if (B == 0) return NMPC_OK;
+    if (!segs || !nseg || !nearest_u) return set_err(NMPC_ERR_ARG, "segs, nseg and nearest_u are required");
+    if (seg_stride < 1) return set_err(NMPC_ERR_ARG, "seg_stride < 1");
+    if (num_poses < 1 || num_poses > 8192) return set_err(NMPC_ERR_ARG, "num_poses out of range [1, 8192]");
+    if (!(sample_period >= 0.0)) return set_err(NMPC_ERR_ARG, "sample_period must be >= 0");
+    return hip_err(launch_path_discretize(B, segs, seg_stride, nseg, nearest_u, sample_period, num_poses,
+                                          is_holonomic ? 1 : 0, traj, traj64, (hipStream_t)stream),
+                   "path_discretize launch");
 }
 
 }  // extern "C"

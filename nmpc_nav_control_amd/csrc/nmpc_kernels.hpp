@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 #include <stddef.h>
 
+#include "nmpc_amd/nmpc_path.h"
 #include "nmpc_models.hpp"
 
 namespace nmpc {
@@ -83,5 +84,8 @@ template <class M>
 hipError_t launch_fleet_sim(const KParams& P, int B, int stride, const float* path, float* s, float* pose, float* vel,
                             float* steer, const float* u0, const int* status, const float* carried, float* traj,
                             int* traj_len, int advance, hipStream_t stream);
+hipError_t launch_path_discretize(int B, const nmpc_path_segment* segs, int seg_stride, const int* nseg,
+                                  const double* nearest_u, double period, int num_poses, int holo, float* traj,
+                                  double* traj64, hipStream_t stream);
 
 }  // namespace nmpc

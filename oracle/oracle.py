@@ -77,6 +77,9 @@ def lib():
                                        ctypes.POINTER(ctypes.c_ubyte), dp, dp, dp, dp, dp,
                                        ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int), ctypes.c_int]
         _lib.oc_batch_tick.restype = ctypes.c_int
+        _lib.oc_path_discretize.argtypes = [ctypes.c_int, dp, ctypes.c_int, ctypes.POINTER(ctypes.c_int), dp,
+                                            ctypes.c_double, ctypes.c_int, ctypes.c_int, dp,
+                                            ctypes.POINTER(ctypes.c_int)]
     return _lib
 
 
@@ -228,3 +231,17 @@ class Oracle:
                                  _p(carried), _p(xbar), _p(ubar), _p(cmd), _p(u0), _ip(status), _ip(qp_iter),
                                  int(nthreads))
         return nf, cmd, u0, status, qp_iter
+
+
+def path_discretize(segs, nseg, nearest_u, sample_period, num_poses, is_holonomic=False):
+    """PathDiscretizer::getNextNPoses (oracle/path_oracle.c) for B robots: segs float64 [B][S][16] (the
+    nmpc_path_segment layout), nseg int32 [B], nearest_u [B]. Returns (poses [B][num_poses][3], steps [B])."""
+    segs = np.ascontiguousarray(segs, np.float64)
+    nseg = np.ascontiguousarray(nseg, np.int32)
+    nearest_u = np.ascontiguousarray(nearest_u, np.float64)
+    B, S = segs.shape[0], segs.shape[1]
+    out = np.zeros((B, num_poses, 3))
+    steps = np.zeros(B, np.int32)
+    lib().oc_path_discretize(B, _p(segs), S, _ip(nseg), _p(nearest_u), float(sample_period), int(num_poses),
+                             1 if is_holonomic else 0, _p(out), _ip(steps))
+    return out, steps
