@@ -49,7 +49,9 @@ BATCH_SYMBOLS = [
     "nmpc_model_dims", "nmpc_model_params_default", "nmpc_model_params_set_limits", "nmpc_batch_create",
     "nmpc_batch_destroy", "nmpc_batch_set_params", "nmpc_batch_get_params", "nmpc_batch_init_iterate",
     "nmpc_batch_solve", "nmpc_batch_run", "nmpc_batch_state", "nmpc_batch_set_kernel", "nmpc_fleet_sim_step",
-    "nmpc_last_error", "nmpc_version", "nmpc_path_discretize",
+    "nmpc_last_error", "nmpc_version", "nmpc_path_discretize", "nmpc_codegen_default", "nmpc_capsule_new",
+    "nmpc_capsule_delete", "nmpc_capsule_create", "nmpc_capsule_reset", "nmpc_capsule_update_params",
+    "nmpc_capsule_solve", "nmpc_capsule_batch_solve", "nmpc_capsule_free", "nmpc_capsule_print_stats",
 ]
 KERNELS = {"team": 0, "lane": 1}
 NLP_SYMBOLS = ["ocp_nlp_constraints_model_set", "ocp_nlp_cost_model_set", "ocp_nlp_out_get", "ocp_nlp_out_set",
@@ -93,17 +95,9 @@ def lib():
     L.nmpc_path_discretize.argtypes = [i, vp, i, vp, vp, ctypes.c_double, i, i, vp, vp, vp]
     L.nmpc_last_error.restype = ctypes.c_char_p
     L.nmpc_version.restype = ctypes.c_char_p
-    for name in MODEL_NAMES.values():
-        cp = ctypes.POINTER(SolverCapsule)
-        getattr(L, f"{name}_acados_create_capsule").restype = cp
-        getattr(L, f"{name}_acados_free_capsule").argtypes = [cp]
-        getattr(L, f"{name}_acados_create").argtypes = [cp]
-        getattr(L, f"{name}_acados_create_with_discretization").argtypes = [cp, i, c_double_p]
-        getattr(L, f"{name}_acados_reset").argtypes = [cp, i]
-        getattr(L, f"{name}_acados_update_params").argtypes = [cp, i, c_double_p, i]
-        getattr(L, f"{name}_acados_solve").argtypes = [cp]
-        getattr(L, f"{name}_acados_batch_solve").argtypes = [ctypes.POINTER(cp), c_int_p, i]
-        getattr(L, f"{name}_acados_free").argtypes = [cp]
+    cp = ctypes.POINTER(SolverCapsule)
+    L.nmpc_capsule_new.restype = cp
+    L.nmpc_capsule_new.argtypes = [i]
     L.ocp_nlp_constraints_model_set.argtypes = [vp, vp, vp, vp, i, ctypes.c_char_p, vp]
     L.ocp_nlp_cost_model_set.argtypes = [vp, vp, vp, i, ctypes.c_char_p, vp]
     L.ocp_nlp_out_get.argtypes = [vp, vp, vp, i, ctypes.c_char_p, vp]
@@ -111,6 +105,36 @@ def lib():
     L.ocp_nlp_get.argtypes = [vp, ctypes.c_char_p, vp]
     _lib = L
     return L
+
+
+_solver_libs = {}
+
+
+def solver_lib(name):
+    """libacados_ocp_solver_{name}.so: the generated per-model ABI (tools/generate_solver_libs.py) that
+    forwards to libnmpc_amd.so with the codegen configuration baked in."""
+    if name in _solver_libs:
+        return _solver_libs[name]
+    lib()  # libnmpc_amd.so first (RTLD_GLOBAL): the solver library resolves to the same instance
+    path = os.path.join(os.path.dirname(LIB_PATH), f"libacados_ocp_solver_{name}.so")
+    if not os.path.exists(path):
+        path = os.path.join(LIB_DIR, f"libacados_ocp_solver_{name}.so")
+    if not os.path.exists(path):
+        raise RuntimeError(f"{path} not found: build it with `make -C nmpc_nav_control_amd/csrc`")
+    S = ctypes.CDLL(path)
+    cp = ctypes.POINTER(SolverCapsule)
+    i = ctypes.c_int
+    getattr(S, f"{name}_acados_create_capsule").restype = cp
+    getattr(S, f"{name}_acados_free_capsule").argtypes = [cp]
+    getattr(S, f"{name}_acados_create").argtypes = [cp]
+    getattr(S, f"{name}_acados_create_with_discretization").argtypes = [cp, i, c_double_p]
+    getattr(S, f"{name}_acados_reset").argtypes = [cp, i]
+    getattr(S, f"{name}_acados_update_params").argtypes = [cp, i, c_double_p, i]
+    getattr(S, f"{name}_acados_solve").argtypes = [cp]
+    getattr(S, f"{name}_acados_batch_solve").argtypes = [ctypes.POINTER(cp), c_int_p, i]
+    getattr(S, f"{name}_acados_free").argtypes = [cp]
+    _solver_libs[name] = S
+    return S
 
 
 def check(rc, what="nmpc call"):

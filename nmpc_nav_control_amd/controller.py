@@ -14,7 +14,7 @@ from dataclasses import dataclass
 
 import numpy as np
 
-from ._lib import MODEL_NAMES, lib, model_dims
+from ._lib import MODEL_NAMES, lib, model_dims, solver_lib
 
 
 @dataclass
@@ -67,11 +67,12 @@ class NMPCNavControl:
         self._name = MODEL_NAMES[self.model]
         L = lib()
         self._L = L
-        self._capsule = getattr(L, f"{self._name}_acados_create_capsule")()
+        self._S = S = solver_lib(self._name)  # the generated per-model ABI
+        self._capsule = getattr(S, f"{self._name}_acados_create_capsule")()
         if N is None:
-            status = getattr(L, f"{self._name}_acados_create")(self._capsule)
+            status = getattr(S, f"{self._name}_acados_create")(self._capsule)
         else:
-            status = getattr(L, f"{self._name}_acados_create_with_discretization")(self._capsule, int(N), None)
+            status = getattr(S, f"{self._name}_acados_create_with_discretization")(self._capsule, int(N), None)
         self.processCreateStatus(status)
         self.N = self._dims_N()
         c = self._capsule.contents
@@ -92,8 +93,8 @@ class NMPCNavControl:
 
     def __del__(self):
         try:
-            getattr(self._L, f"{self._name}_acados_free")(self._capsule)
-            getattr(self._L, f"{self._name}_acados_free_capsule")(self._capsule)
+            getattr(self._S, f"{self._name}_acados_free")(self._capsule)
+            getattr(self._S, f"{self._name}_acados_free_capsule")(self._capsule)
         except Exception:
             pass
 
@@ -163,7 +164,7 @@ class NMPCNavControl:
         self.W = np.diag(np.asarray(W_diag[: self.ny], np.float64))
         self.W_e = np.diag(np.asarray(W_diag[: self.nx], np.float64))
         for i in range(self.N):
-            rc = getattr(self._L, f"{self._name}_acados_update_params")(self._capsule, i, _dp(self.p), self.np)
+            rc = getattr(self._S, f"{self._name}_acados_update_params")(self._capsule, i, _dp(self.p), self.np)
             if rc != 0:
                 raise RuntimeError("update_params failed")
         for i in range(1, self.N + 1):
@@ -193,7 +194,7 @@ class NMPCNavControl:
             self._wset(i, "yref", self.yref[i, : (self.nx if i == self.N else self.ny)])
 
     def _solve(self):
-        status = getattr(self._L, f"{self._name}_acados_solve")(self._capsule)
+        status = getattr(self._S, f"{self._name}_acados_solve")(self._capsule)
         self.processAcadosStatus(status)
         self.status = status
         self.kkt_res = self._capsule.contents.nlp_out.contents.inf_norm_res
@@ -204,7 +205,7 @@ class NMPCNavControl:
         return self.cpu_time
 
     def reset_mpc(self):
-        getattr(self._L, f"{self._name}_acados_reset")(self._capsule, 1)
+        getattr(self._S, f"{self._name}_acados_reset")(self._capsule, 1)
         return True
 
 
@@ -320,6 +321,6 @@ def batch_solve(controllers):
     arr_t = ctypes.POINTER(type(controllers[0]._capsule.contents)) * len(controllers)
     arr = arr_t(*[c._capsule for c in controllers])
     status = np.zeros(len(controllers), np.int32)
-    getattr(lib(), f"{name}_acados_batch_solve")(arr, status.ctypes.data_as(ctypes.POINTER(ctypes.c_int)),
-                                                 len(controllers))
+    solve = getattr(solver_lib(name), f"{name}_acados_batch_solve")
+    solve(arr, status.ctypes.data_as(ctypes.POINTER(ctypes.c_int)), len(controllers))
     return status

@@ -23,10 +23,8 @@
 #include <string>
 #include <vector>
 
-#include "acados_solver_diff2amr.h"
-#include "acados_solver_omni4amr.h"
-#include "acados_solver_tric3amr.h"
 #include "nmpc_amd/nmpc_batch.h"
+#include "nmpc_amd/nmpc_capsule.h"
 
 struct nmpc_capsule_impl {
     int model = 0, N = 0;
@@ -74,16 +72,6 @@ std::map<std::pair<int, int>, std::unique_ptr<Engine>> g_engines;
 
 void log_err(const char* what, const std::string& msg) { std::fprintf(stderr, "[nmpc_amd] %s: %s\n", what, msg.c_str()); }
 
-int model_default_N(int model)
-{
-    static const char* env[3] = {"NMPC_AMD_DIFF2AMR_N", "NMPC_AMD_OMNI4AMR_N", "NMPC_AMD_TRIC3AMR_N"};
-    if (const char* e = std::getenv(env[model])) {
-        const int n = std::atoi(e);
-        if (n > 0) return n;
-    }
-    return 80;  // tf_ini 2.0 s at freq 40 Hz (config/nmpc_nav_control_acados_models.yaml:3-4,27-28,51-52)
-}
-
 void stage_W_diag(nmpc_capsule_impl* c, int k, const double* d, int n)
 {
     double* W = c->W.data() + (size_t)k * c->ny * c->ny;
@@ -91,44 +79,23 @@ void stage_W_diag(nmpc_capsule_impl* c, int k, const double* d, int n)
     for (int i = 0; i < n; i++) W[i + n * i] = d[i];
 }
 
-// Values baked into the acados-generated code by the shipped codegen yaml
-// (config/nmpc_nav_control_acados_models.yaml) and scripts/*/generate_c_code.py; the wrappers overwrite
-// p, bounds and W at construction time (e.g. NMPCNavControlDiff.cpp:16-73).
-void codegen_defaults(nmpc_capsule_impl* c)
+// Values scripts/*/generate_c_code.py bakes into the generated solver, here from a codegen descriptor
+// (nmpc_codegen_default: the shipped config/nmpc_nav_control_acados_models.yaml); the wrappers overwrite p,
+// bounds and W at construction time (e.g. NMPCNavControlDiff.cpp:16-73).
+void codegen_defaults(nmpc_capsule_impl* c, const nmpc_codegen_desc& d)
 {
     nmpc_model_params_default(c->model, c->N, &c->prm);
     c->prm.terminal_hack = 0;  // the wrappers apply it themselves through cost_model_set(N, "W")
-    const double deg = M_PI / 180.0;
-    double Q[11] = {0}, R[4] = {0}, QN[11] = {0};
-    if (c->model == NMPC_MODEL_DIFF2AMR) {
-        c->prm.p[0] = 0.270; c->prm.p[1] = 0.1;                     // yaml:30-31
-        nmpc_model_params_set_limits(&c->prm, 1.0, 2.0, 0, 0, 0);  // yaml:33-34
-        const double q[7] = {10, 10, 5, 0, 0, 0, 0}, qn[7] = {1000, 1000, 500, 0, 0, 0, 0};  // yaml:37-47
-        std::memcpy(Q, q, sizeof(q));
-        std::memcpy(QN, qn, sizeof(qn));
-        R[0] = R[1] = 1.0;
-    } else if (c->model == NMPC_MODEL_OMNI4AMR) {
-        c->prm.p[0] = 0.535; c->prm.p[1] = 0.1;                     // yaml:6-7
-        nmpc_model_params_set_limits(&c->prm, 1.0, 1.0, 0, 0, 0);  // yaml:9-10
-        const double q[11] = {10, 10, 10, 0, 0, 0, 0, 0, 0, 0, 0};  // yaml:13-23
-        std::memcpy(Q, q, sizeof(q));
-        std::memcpy(QN, q, sizeof(q));
-        R[0] = R[1] = R[2] = R[3] = 1.0;
-    } else {
-        c->prm.p[0] = 0.270; c->prm.p[1] = 0.1; c->prm.p[2] = 0.5;                               // yaml:54-56
-        nmpc_model_params_set_limits(&c->prm, 1.0, 1.0, -30.0 * deg, 30.0 * deg, 120.0 * deg);  // yaml:58-62
-        const double q[7] = {10, 10, 5, 0, 0, 0, 0}, qn[7] = {1000, 1000, 500, 0, 0, 0, 0};     // yaml:65-75
-        std::memcpy(Q, q, sizeof(q));
-        std::memcpy(QN, qn, sizeof(qn));
-        R[0] = R[1] = 1.0;
-    }
+    c->prm.dt = d.tf / d.N;    // uniform time steps tf / N_codegen (ocp.solver_options.tf, N_horizon)
+    std::memcpy(c->prm.p, d.p, sizeof(d.p));
+    std::memcpy(c->prm.lbx, d.lbx, sizeof(d.lbx));
+    std::memcpy(c->prm.ubx, d.ubx, sizeof(d.ubx));
+    std::memcpy(c->prm.lbu, d.lbu, sizeof(d.lbu));
+    std::memcpy(c->prm.ubu, d.ubu, sizeof(d.ubu));
     const int N = c->N, nx = c->nx, nu = c->nu, ny = c->ny;
     c->W.assign((size_t)(N + 1) * ny * ny, 0.0);
-    double wd[15];
-    for (int i = 0; i < nx; i++) wd[i] = Q[i];
-    for (int i = 0; i < nu; i++) wd[nx + i] = R[i];
-    for (int k = 0; k < N; k++) stage_W_diag(c, k, wd, ny);
-    stage_W_diag(c, N, QN, nx);
+    for (int k = 0; k < N; k++) stage_W_diag(c, k, d.W, ny);
+    stage_W_diag(c, N, d.W_e, nx);
     c->yref.assign((size_t)(N + 1) * ny, 0.0);
     c->lbx.assign((size_t)(N + 1) * nx, 0.0);
     c->ubx.assign((size_t)(N + 1) * nx, 0.0);
@@ -171,11 +138,11 @@ nmpc_capsule_impl* new_impl(int model)
     return c;
 }
 
-int impl_create(nmpc_capsule_impl* c, int N)
+int impl_create(nmpc_capsule_impl* c, int N, const nmpc_codegen_desc& d)
 {
     if (N < 1) return 1;
     c->N = N;
-    codegen_defaults(c);
+    codegen_defaults(c, d);
     c->dims.N = N;
     c->dims.nx = c->nx;
     c->dims.nu = c->nu;
@@ -513,104 +480,153 @@ int ocp_nlp_dims_get_from_attr(ocp_nlp_config* config, ocp_nlp_dims* dims, ocp_n
 }  // extern "C"
 
 // ------------------------------------------------------------------------------------------------------
-// Per-model generated-solver ABI
+// Model-generic capsule engine (include/nmpc_amd/nmpc_capsule.h). The per-model {name}_acados_* functions
+// are generated by tools/generate_solver_libs.py into libacados_ocp_solver_{name}.so and forward here.
 // ------------------------------------------------------------------------------------------------------
-#define NMPC_DEFINE_MODEL_ABI(name, MODEL)                                                                       \
-    extern "C" name##_solver_capsule* name##_acados_create_capsule(void)                                        \
-    {                                                                                                            \
-        name##_solver_capsule* cap = new name##_solver_capsule();                                               \
-        nmpc_capsule_impl* c = new_impl(MODEL);                                                                  \
-        cap->impl = c;                                                                                           \
-        cap->nlp_config = &c->config;                                                                            \
-        cap->nlp_dims = &c->dims;                                                                                \
-        cap->nlp_in = &c->in;                                                                                    \
-        cap->nlp_out = &c->out;                                                                                  \
-        cap->nlp_solver = &c->solver;                                                                            \
-        cap->nlp_opts = nullptr;                                                                                 \
-        return cap;                                                                                              \
-    }                                                                                                            \
-    extern "C" int name##_acados_free_capsule(name##_solver_capsule* capsule)                                   \
-    {                                                                                                            \
-        if (!capsule) return 1;                                                                                  \
-        delete capsule->impl;                                                                                    \
-        delete capsule;                                                                                          \
-        return 0;                                                                                                \
-    }                                                                                                            \
-    extern "C" int name##_acados_create_with_discretization(name##_solver_capsule* capsule, int n_time_steps,    \
-                                                            double* new_time_steps)                              \
-    {                                                                                                            \
-        if (!capsule || !capsule->impl) return 1;                                                                \
-        if (new_time_steps) {                                                                                    \
-            log_err("create", "non-uniform time steps are not supported");                                      \
-            return 1;                                                                                            \
-        }                                                                                                        \
-        return impl_create(capsule->impl, n_time_steps);                                                        \
-    }                                                                                                            \
-    extern "C" int name##_acados_create(name##_solver_capsule* capsule)                                         \
-    {                                                                                                            \
-        return name##_acados_create_with_discretization(capsule, model_default_N(MODEL), nullptr);             \
-    }                                                                                                            \
-    extern "C" int name##_acados_reset(name##_solver_capsule* capsule, int reset_qp_solver_mem)                 \
-    {                                                                                                            \
-        (void)reset_qp_solver_mem; /* the IPM cold-starts every QP: no QP memory to reset */                    \
-        if (!capsule || !capsule->impl || !capsule->impl->created) return 1;                                    \
-        nmpc_capsule_impl* c = capsule->impl;                                                                    \
-        std::fill(c->xbar.begin(), c->xbar.end(), 0.0);                                                          \
-        std::fill(c->ubar.begin(), c->ubar.end(), 0.0);                                                          \
-        return 0;                                                                                                \
-    }                                                                                                            \
-    extern "C" int name##_acados_update_params(name##_solver_capsule* capsule, int stage, double* value, int np) \
-    {                                                                                                            \
-        if (!capsule || !capsule->impl || !capsule->impl->created || !value) return 1;                          \
-        nmpc_capsule_impl* c = capsule->impl;                                                                    \
-        if (np != c->np) {                                                                                       \
-            log_err("update_params", "np does not match the model");                                            \
-            return 1;                                                                                            \
-        }                                                                                                        \
-        if (stage < 0 || stage > c->N) return 1;                                                                 \
-        for (int i = 0; i < np; i++) c->p[(size_t)stage * np + i] = value[i];                                    \
-        return 0;                                                                                                \
-    }                                                                                                            \
-    extern "C" int name##_acados_solve(name##_solver_capsule* capsule)                                          \
-    {                                                                                                            \
-        if (!capsule || !capsule->impl) return 4;                                                                \
-        std::vector<nmpc_capsule_impl*> cs{capsule->impl};                                                       \
-        batch_solve_impl(cs, nullptr);                                                                           \
-        return capsule->impl->status;                                                                            \
-    }                                                                                                            \
-    extern "C" int name##_acados_batch_solve(name##_solver_capsule** capsules, int* status_out, int N_batch)    \
-    {                                                                                                            \
-        if (!capsules || N_batch < 0) return -1;                                                                 \
-        std::vector<nmpc_capsule_impl*> cs(N_batch);                                                             \
-        for (int i = 0; i < N_batch; i++) cs[i] = capsules[i] ? capsules[i]->impl : nullptr;                    \
-        return batch_solve_impl(cs, status_out);                                                                 \
-    }                                                                                                            \
-    extern "C" int name##_acados_free(name##_solver_capsule* capsule)                                           \
-    {                                                                                                            \
-        if (!capsule || !capsule->impl) return 1;                                                                \
-        capsule->impl->created = false;                                                                          \
-        return 0;                                                                                                \
-    }                                                                                                            \
-    extern "C" void name##_acados_print_stats(name##_solver_capsule* capsule)                                   \
-    {                                                                                                            \
-        if (!capsule || !capsule->impl) return;                                                                  \
-        const nmpc_capsule_impl* c = capsule->impl;                                                              \
-        std::printf("%s: status %d, sqp_iter %d, qp_iter %d, time_tot %.3f ms\n", #name, c->status, c->sqp_iter, \
-                    c->qp_iter, c->time_tot * 1e3);                                                              \
-    }                                                                                                            \
-    extern "C" ocp_nlp_in* name##_acados_get_nlp_in(name##_solver_capsule* capsule) { return capsule->nlp_in; }  \
-    extern "C" ocp_nlp_out* name##_acados_get_nlp_out(name##_solver_capsule* capsule) { return capsule->nlp_out; } \
-    extern "C" ocp_nlp_solver* name##_acados_get_nlp_solver(name##_solver_capsule* capsule)                     \
-    {                                                                                                            \
-        return capsule->nlp_solver;                                                                              \
-    }                                                                                                            \
-    extern "C" ocp_nlp_config* name##_acados_get_nlp_config(name##_solver_capsule* capsule)                     \
-    {                                                                                                            \
-        return capsule->nlp_config;                                                                              \
-    }                                                                                                            \
-    extern "C" void* name##_acados_get_nlp_opts(name##_solver_capsule* capsule) { return capsule->nlp_opts; }    \
-    extern "C" ocp_nlp_dims* name##_acados_get_nlp_dims(name##_solver_capsule* capsule) { return capsule->nlp_dims; }
+extern "C" {
 
-NMPC_DEFINE_MODEL_ABI(diff2amr, NMPC_MODEL_DIFF2AMR)
-NMPC_DEFINE_MODEL_ABI(omni4amr, NMPC_MODEL_OMNI4AMR)
-NMPC_DEFINE_MODEL_ABI(tric3amr, NMPC_MODEL_TRIC3AMR)
+int nmpc_codegen_default(int model, nmpc_codegen_desc* d)
+{
+    if (!d || model < 0 || model > 2) return NMPC_ERR_ARG;
+    std::memset(d, 0, sizeof(*d));
+    d->model = model;
+    d->N = 80;  // tf_ini 2.0 s at freq 40 Hz (scripts/diff/common.py:5-9)
+    d->tf = 80.0 / 40.0;
+    const double deg = M_PI / 180.0;
+    nmpc_model_params prm;
+    nmpc_model_params_default(model, d->N, &prm);
+    if (model == NMPC_MODEL_DIFF2AMR) {
+        d->p[0] = 0.270; d->p[1] = 0.1;
+        nmpc_model_params_set_limits(&prm, 1.0, 2.0, 0, 0, 0);
+        const double w[9] = {10, 10, 5, 0, 0, 0, 0, 1, 1}, we[7] = {1000, 1000, 500, 0, 0, 0, 0};
+        std::memcpy(d->W, w, sizeof(w));
+        std::memcpy(d->W_e, we, sizeof(we));
+    } else if (model == NMPC_MODEL_OMNI4AMR) {
+        d->p[0] = 0.535; d->p[1] = 0.1;
+        nmpc_model_params_set_limits(&prm, 1.0, 1.0, 0, 0, 0);
+        const double w[15] = {10, 10, 10, 0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1};
+        std::memcpy(d->W, w, sizeof(w));
+        std::memcpy(d->W_e, w, sizeof(double) * 11);
+    } else {
+        d->p[0] = 0.270; d->p[1] = 0.1; d->p[2] = 0.5;
+        nmpc_model_params_set_limits(&prm, 1.0, 1.0, -30.0 * deg, 30.0 * deg, 120.0 * deg);
+        const double w[9] = {10, 10, 5, 0, 0, 0, 0, 1, 1}, we[7] = {1000, 1000, 500, 0, 0, 0, 0};
+        std::memcpy(d->W, w, sizeof(w));
+        std::memcpy(d->W_e, we, sizeof(we));
+    }
+    std::memcpy(d->lbx, prm.lbx, sizeof(d->lbx));
+    std::memcpy(d->ubx, prm.ubx, sizeof(d->ubx));
+    std::memcpy(d->lbu, prm.lbu, sizeof(d->lbu));
+    std::memcpy(d->ubu, prm.ubu, sizeof(d->ubu));
+    return NMPC_OK;
+}
+
+nmpc_solver_capsule* nmpc_capsule_new(int model)
+{
+    if (model < 0 || model > 2) return nullptr;
+    nmpc_solver_capsule* cap = new nmpc_solver_capsule();
+    nmpc_capsule_impl* c = new_impl(model);
+    cap->impl = c;
+    cap->nlp_config = &c->config;
+    cap->nlp_dims = &c->dims;
+    cap->nlp_in = &c->in;
+    cap->nlp_out = &c->out;
+    cap->nlp_solver = &c->solver;
+    cap->nlp_opts = nullptr;
+    return cap;
+}
+
+int nmpc_capsule_delete(nmpc_solver_capsule* capsule)
+{
+    if (!capsule) return 1;
+    delete capsule->impl;
+    delete capsule;
+    return 0;
+}
+
+int nmpc_capsule_create(nmpc_solver_capsule* capsule, const nmpc_codegen_desc* desc, int n_time_steps,
+                        const double* new_time_steps)
+{
+    if (!capsule || !capsule->impl) return 1;
+    nmpc_codegen_desc d;
+    if (desc) {
+        if (desc->model != capsule->impl->model || desc->N < 1 || !(desc->tf > 0.0)) {
+            log_err("create", "codegen descriptor does not match the capsule's model");
+            return 1;
+        }
+        d = *desc;
+    } else {
+        nmpc_codegen_default(capsule->impl->model, &d);
+    }
+    if (new_time_steps) {
+        for (int k = 1; k < n_time_steps; k++)
+            if (std::fabs(new_time_steps[k] - new_time_steps[0]) > 1e-12 * std::fabs(new_time_steps[0])) {
+                log_err("create", "non-uniform time steps are not supported");
+                return 1;
+            }
+        if (n_time_steps >= 1) {
+            d.N = n_time_steps;
+            d.tf = new_time_steps[0] * n_time_steps;
+        }
+    } else if (n_time_steps >= 1 && n_time_steps != d.N) {
+        d.tf = d.tf / d.N * n_time_steps;  // acados keeps the step size tf / N of the codegen
+        d.N = n_time_steps;
+    }
+    return impl_create(capsule->impl, n_time_steps, d);
+}
+
+int nmpc_capsule_reset(nmpc_solver_capsule* capsule, int reset_qp_solver_mem)
+{
+    (void)reset_qp_solver_mem;  // the IPM cold-starts every QP: no QP memory to reset
+    if (!capsule || !capsule->impl || !capsule->impl->created) return 1;
+    nmpc_capsule_impl* c = capsule->impl;
+    std::fill(c->xbar.begin(), c->xbar.end(), 0.0);
+    std::fill(c->ubar.begin(), c->ubar.end(), 0.0);
+    return 0;
+}
+
+int nmpc_capsule_update_params(nmpc_solver_capsule* capsule, int stage, const double* value, int np)
+{
+    if (!capsule || !capsule->impl || !capsule->impl->created || !value) return 1;
+    nmpc_capsule_impl* c = capsule->impl;
+    if (np != c->np) {
+        log_err("update_params", "np does not match the model");
+        return 1;
+    }
+    if (stage < 0 || stage > c->N) return 1;
+    for (int i = 0; i < np; i++) c->p[(size_t)stage * np + i] = value[i];
+    return 0;
+}
+
+int nmpc_capsule_solve(nmpc_solver_capsule* capsule)
+{
+    if (!capsule || !capsule->impl) return 4;
+    std::vector<nmpc_capsule_impl*> cs{capsule->impl};
+    batch_solve_impl(cs, nullptr);
+    return capsule->impl->status;
+}
+
+int nmpc_capsule_batch_solve(nmpc_solver_capsule** capsules, int* status_out, int n)
+{
+    if (!capsules || n < 0) return -1;
+    std::vector<nmpc_capsule_impl*> cs(n);
+    for (int i = 0; i < n; i++) cs[i] = capsules[i] ? capsules[i]->impl : nullptr;
+    return batch_solve_impl(cs, status_out);
+}
+
+int nmpc_capsule_free(nmpc_solver_capsule* capsule)
+{
+    if (!capsule || !capsule->impl) return 1;
+    capsule->impl->created = false;
+    return 0;
+}
+
+void nmpc_capsule_print_stats(const nmpc_solver_capsule* capsule, const char* name)
+{
+    if (!capsule || !capsule->impl) return;
+    const nmpc_capsule_impl* c = capsule->impl;
+    std::printf("%s: status %d, sqp_iter %d, qp_iter %d, time_tot %.3f ms\n", name ? name : "nmpc", c->status,
+                c->sqp_iter, c->qp_iter, c->time_tot * 1e3);
+}
+
+}  // extern "C"

@@ -56,6 +56,7 @@ namespace {
 
 constexpr float kBreakdownMu = 1e-6f;
 constexpr float kStatRel = 1e-5f;  // ~100 ulp of fp32
+constexpr float kCompMaxRatio = 30.0f;  // largest complementarity product at exit / tol_comp (sqp_rti_team.hip)
 
 // max that propagates NaN (fmaxf drops it)
 __device__ inline float nan_max(float a, float b) { return (b > a || b != b) ? b : a; }
@@ -256,7 +257,7 @@ __global__ __launch_bounds__(64, 1) void k_sqp_rti_lane(KParams P, KArgs a, int 
     for (it = 0;; it++) {
         // P1 (backward): apply previous update, residuals, adjoint pi, factorisation + predictor rhs.
         float Lp[NX][NX], pv[NX], pin[NX];
-        float res_stat = 0.0f, res_ineq = 0.0f, sum_c = 0.0f, stat_scale = 1.0f;
+        float res_stat = 0.0f, res_ineq = 0.0f, sum_c = 0.0f, max_c = 0.0f, stat_scale = 1.0f;
         bool fail = false;
         for (int k = N; k >= 0; k--) {
             float du[NU], dx[NX];
@@ -310,6 +311,7 @@ __global__ __launch_bounds__(64, 1) void k_sqp_rti_lane(KParams P, KArgs a, int 
                 const float rl = z - lb - tl, rr = ubd - z - tu;
                 res_ineq = nan_max(res_ineq, fmaxf(fabsf(rl), fabsf(rr)));
                 sum_c += ll * tl + lu * tu;
+                max_c = fmaxf(max_c, fmaxf(ll * tl, lu * tu));
                 // predictor rhs (target 0) and barrier Hessian
                 const float gh = (ll * rl) / tl + ll - (lu * rr) / tu - lu;
                 const float sg = ll / tl + lu / tu;
@@ -493,8 +495,11 @@ __global__ __launch_bounds__(64, 1) void k_sqp_rti_lane(KParams P, KArgs a, int 
         // fp32 stopping rule: the u-stationarity residual is a sum of terms of size stat_scale, so it cannot
         // fall below ~kStatRel * stat_scale; and once mu is 100x below its target the iterate is final.
         const bool stat_ok = res_stat <= P.tol_stat || res_stat <= kStatRel * stat_scale;
+        const bool cmax_ok = max_c <= kCompMaxRatio * P.tol_comp;
         const bool stalled = mu <= P.tol_comp && mu > 0.5f * mu_prev;  // fp32 floor (see sqp_rti_team.hip)
-        if (res_ineq <= P.tol_ineq && ((stat_ok && mu <= P.tol_comp) || mu <= 1e-2f * P.tol_comp || stalled)) break;
+        if (res_ineq <= P.tol_ineq &&
+            ((stat_ok && mu <= P.tol_comp && cmax_ok) || mu <= 1e-2f * P.tol_comp || (stalled && cmax_ok)))
+            break;
         if (it >= P.iter_max) break;
         mu_prev = mu;
 

@@ -69,6 +69,10 @@ namespace {
 
 constexpr float kBreakdownMuT = 1e-6f;
 constexpr float kStatRelT = 1e-5f;
+// largest single complementarity product at exit, relative to tol_comp: the mean (mu) alone lets one pair keep
+// m * mu, which leaves a nearly active bound's multiplier at ~1e-5 and moves u0 by ~1e-3 through the weak input
+// curvature R dt (DESIGN.md "Stopping rule")
+constexpr float kCompMaxRatio = 30.0f;
 #ifndef LIGHT_D
 #define LIGHT_D 4  // record buffers of the light (solve-only) sweeps
 #endif
@@ -519,7 +523,7 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
 #pragma unroll
         for (int j = 0; j < NV; j++) Lrow[j] = 0.0;
         float pv = 0.0f, piv = 0.0f;
-        float res_stat = 0.0f, res_ineq = 0.0f, sum_c = 0.0f, stat_scale = 1.0f, nanf_ = 0.0f;
+        float res_stat = 0.0f, res_ineq = 0.0f, sum_c = 0.0f, max_c = 0.0f, stat_scale = 1.0f, nanf_ = 0.0f;
         bool fail = false;
         const bool act = lv && !done;
         const float a_upd = (it > 0 && !done) ? alpha : 0.0f;
@@ -557,6 +561,7 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
             const float itl = frcp(tl), itu = frcp(tu);
             res_ineq = nan_max(res_ineq, fmaxf(fabsf(rl), fabsf(rr)));
             sum_c += ll * tl + lu * tu;
+            max_c = fmaxf(max_c, fmaxf(ll * tl, lu * tu));
             const float lamdiff = ll - lu;
             const float sig = ll * itl + lu * itu;
             const float gh = ll * rl * itl + ll - lu * rr * itu - lu;
@@ -647,6 +652,7 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
         if (it < kStampItsC) STAMP(2 + 4 * it);
         // team reductions
         sum_c = row_sum16(lv ? sum_c : 0.0f);
+        max_c = row_max16(lv ? max_c : 0.0f);
         res_ineq = row_max16(lv ? res_ineq : 0.0f);
         res_stat = row_max16(lv ? res_stat : 0.0f);
         stat_scale = row_max16(stat_scale);
@@ -669,8 +675,10 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
                 // fp32 floor: below ~1e-12 the complementarity no longer decreases and the fp32 multiplier
                 // updates (Sigma ~ 1e10 times the rounding of dz) degrade stationarity, so a stalled mu that is
                 // already under tol_comp ends the iteration as well
+                const bool cmax_ok = max_c <= kCompMaxRatio * P.tol_comp;
                 const bool stalled = mu <= P.tol_comp && mu > 0.5f * mu_prev;
-                if (res_ineq <= P.tol_ineq && ((stat_ok && mu <= P.tol_comp) || mu <= 1e-2f * P.tol_comp || stalled))
+                if (res_ineq <= P.tol_ineq &&
+                    ((stat_ok && mu <= P.tol_comp && cmax_ok) || mu <= 1e-2f * P.tol_comp || (stalled && cmax_ok)))
                     stop = true;
                 if (it >= P.iter_max) stop = true;
             }

@@ -1,4 +1,5 @@
-"""CPU tests of the drop-in boundary: libnmpc_amd.so exports every function include/*.h declares, the
+"""CPU tests of the drop-in boundary: libnmpc_amd.so plus the generated libacados_ocp_solver_{name}.so export
+every function include/*.h declares, the model-descriptor codegen (tools/generate_solver_libs.py), the
 host-side calls that need no GPU (dims, default parameters, limits, version), and the parameter loaders
 (nmpc_nav_control.yaml / acados_models.yaml surfaces, NMPCNavControlROS::readParam)."""
 import glob
@@ -29,9 +30,14 @@ def declared_functions():
     return names
 
 
-def exported_symbols():
-    out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True, check=True)
+def exported_symbols(path=None):
+    out = subprocess.run(["nm", "-D", "--defined-only", path or _lib.LIB_PATH], capture_output=True, text=True,
+                         check=True)
     return {l.split()[-1] for l in out.stdout.splitlines() if " T " in l}
+
+
+def solver_lib_path(name):
+    return os.path.join(_lib.LIB_DIR, f"libacados_ocp_solver_{name}.so")
 
 
 def test_headers_declare_the_reference_abi(built):
@@ -41,15 +47,26 @@ def test_headers_declare_the_reference_abi(built):
 
 
 def test_library_exports_every_declared_function(built):
-    missing = declared_functions() - exported_symbols()
+    """libnmpc_amd.so (the libacados part: ocp_nlp_*, nmpc_*) + the three generated solver libraries."""
+    exported = exported_symbols()
+    for name in _lib.MODEL_NAMES.values():
+        exported |= exported_symbols(solver_lib_path(name))
+    missing = declared_functions() - exported
     assert not missing, sorted(missing)
 
 
-def test_capsule_aliases_resolve_to_same_library(built):
-    """libacados_ocp_solver_<name>.so are the link names the reference's CMakeLists uses (CMakeLists.txt:30-44)."""
+def test_solver_libraries_follow_the_acados_split(built):
+    """libacados_ocp_solver_<name>.so (the link names of CMakeLists.txt:112-114) holds exactly the model's
+    {name}_acados_* ABI and loads libnmpc_amd.so; libnmpc_amd.so holds no per-model symbol, so a process that
+    links all three solver libraries (as the reference does) resolves each model to its own generated code."""
+    core = exported_symbols()
     for name in _lib.MODEL_NAMES.values():
-        p = os.path.join(_lib.LIB_DIR, f"libacados_ocp_solver_{name}.so")
-        assert os.path.exists(p) and os.path.realpath(p) == os.path.realpath(_lib.LIB_PATH)
+        p = solver_lib_path(name)
+        syms = exported_symbols(p)
+        assert syms == {f"{name}_acados_{s}" for s in _lib.CAPSULE_SUFFIXES}, sorted(syms)
+        assert not any(s.startswith(f"{name}_") for s in core)
+        dyn = subprocess.run(["readelf", "-d", p], capture_output=True, text=True, check=True).stdout
+        assert "[libnmpc_amd.so]" in dyn and "$ORIGIN" in dyn
 
 
 @pytest.mark.parametrize("model,dims", [

@@ -1,0 +1,130 @@
+"""CPU tests of the model-descriptor codegen (tools/generate_solver_libs.py), the counterpart of the reference's
+scripts/generate_acados_libs.py + scripts/<geometry>/generate_c_code.py: what a codegen yaml bakes
+(scripts/<geometry>/common.py load_parameters), the generated c_generated_code/ layout, and a C program that
+includes the generated header and links the generated library the way CMakeLists.txt:66-72,112-114 does."""
+import json
+import math
+import os
+import subprocess
+import sys
+
+import pytest
+import yaml
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+import generate_solver_libs as gen  # noqa: E402
+
+from nmpc_nav_control_amd import _lib  # noqa: E402
+
+SHIPPED = os.path.join(ROOT, "configs", "acados_models.yaml")
+
+
+def test_shipped_descriptors():
+    P = yaml.safe_load(open(SHIPPED))
+    d = gen.load_parameters("diff", P["diff_params"])
+    assert (d["N"], d["tf"]) == (80, 2.0)
+    assert d["p"] == [0.270, 0.1] and d["lbu"] == [-2.0, -2.0] and d["ubx"] == [1.0, 1.0]
+    assert d["W"] == [10, 10, 5, 0, 0, 0, 0, 1, 1] and d["W_e"] == [1000, 1000, 500, 0, 0, 0, 0]
+    t = gen.load_parameters("tric", P["tric_params"])
+    deg = math.pi / 180
+    assert t["p"] == [0.270, 0.1, 0.5]
+    assert t["lbx"] == [-1.0, -30 * deg] and t["ubx"] == [1.0, 30 * deg]
+    assert t["lbu"] == [-1.0, -120 * deg] and t["ubu"] == [1.0, 120 * deg]
+    o = gen.load_parameters("omni4", P["omni4_params"])
+    assert o["p"] == [0.535, 0.1] and o["lbx"] == [-1.0] * 4 and len(o["W"]) == 15
+
+
+def test_horizon_rounds_up():
+    """N = ceil(tf_ini / (1/freq)) (scripts/diff/common.py:7-8), TF = N dt."""
+    P = yaml.safe_load(open(SHIPPED))["diff_params"]
+    d = gen.load_parameters("diff", dict(P, tf_ini=1.01, freq=20))
+    assert d["N"] == 21 and d["tf"] == pytest.approx(21 / 20)
+
+
+def test_library_descriptors_match_the_shipped_defaults(built):
+    """The in-tree libraries are generated from configs/acados_models.yaml; nmpc_codegen_default holds the
+    same values (used when a capsule is created without a descriptor)."""
+    import ctypes
+
+    class Desc(ctypes.Structure):
+        _fields_ = [("model", ctypes.c_int), ("N", ctypes.c_int), ("tf", ctypes.c_double),
+                    ("p", ctypes.c_double * 3), ("lbx", ctypes.c_double * 4), ("ubx", ctypes.c_double * 4),
+                    ("lbu", ctypes.c_double * 4), ("ubu", ctypes.c_double * 4), ("W", ctypes.c_double * 15),
+                    ("W_e", ctypes.c_double * 11)]
+
+    P = yaml.safe_load(open(SHIPPED))
+    L = _lib.lib()
+    for geom, model in (("diff", 0), ("omni4", 1), ("tric", 2)):
+        exp = gen.load_parameters(geom, P[f"{geom}_params"])
+        got = Desc()
+        assert L.nmpc_codegen_default(model, ctypes.byref(got)) == 0
+        assert (got.N, got.tf) == (exp["N"], exp["tf"])
+        for k in ("p", "lbx", "ubx", "lbu", "ubu", "W", "W_e"):
+            assert list(getattr(got, k))[:len(exp[k])] == pytest.approx(exp[k], abs=1e-15), (geom, k)
+        gen_json = json.load(open(os.path.join(ROOT, "build", "generated", geom, f"acados_ocp_{exp['name']}.json")))
+        assert gen_json["N"] == exp["N"] and gen_json["W"] == exp["W"]
+
+
+PROGRAM = r"""
+#include <stdio.h>
+#include "acados_solver_diff2amr.h"
+#include "acados_c/ocp_nlp_interface.h"
+int main(void) {
+    diff2amr_solver_capsule* c = diff2amr_acados_create_capsule();
+    int st = diff2amr_acados_create(c);
+    double x[DIFF2AMR_NX];
+    ocp_nlp_out_get(c->nlp_config, c->nlp_dims, c->nlp_out, 0, "x", x);
+    int nu = ocp_nlp_dims_get_from_attr(c->nlp_config, c->nlp_dims, c->nlp_out, DIFF2AMR_N - 1, "u");
+    printf("%d %d %d %d %.6f\n", st, DIFF2AMR_N, c->nlp_dims->N, nu, x[2]);
+    diff2amr_acados_free(c);
+    diff2amr_acados_free_capsule(c);
+    return 0;
+}
+"""
+
+
+def test_generated_tree_links_like_the_reference(built, tmp_path):
+    cfg = yaml.safe_load(open(SHIPPED))
+    cfg["diff_params"].update(tf_ini=1.0, freq=20)  # N = 20
+    del cfg["omni4_params"]
+    yml = tmp_path / "models.yaml"
+    yml.write_text(yaml.safe_dump(cfg))
+    out = tmp_path / "scripts"
+    rc = gen.main([str(yml), "--out", str(out)])
+    assert rc == 0
+    cg = out / "diff" / "c_generated_code"
+    assert sorted(os.listdir(cg)) == ["acados_ocp_diff2amr.json", "acados_solver_diff2amr.h",
+                                      "diff2amr_solver.c", "libacados_ocp_solver_diff2amr.so"]
+    assert not (out / "omni4").exists() and (out / "tric" / "c_generated_code").exists()
+    assert "#define DIFF2AMR_N      20" in (cg / "acados_solver_diff2amr.h").read_text()
+    # CMakeLists.txt: include_directories(${ACADOS_INCLUDE_DIRS} ${diff2amr_model}), link ${ACADOS_LIBRARIES}
+    # (= libnmpc_amd.so) and ${diff2amr_model}/libacados_ocp_solver_diff2amr.so
+    (tmp_path / "main.c").write_text(PROGRAM)
+    exe = tmp_path / "main"
+    subprocess.run(["gcc", "-std=c11", "-I", str(cg), "-I", os.path.join(ROOT, "include"), str(tmp_path / "main.c"),
+                    _lib.LIB_PATH, str(cg / "libacados_ocp_solver_diff2amr.so"), "-o", str(exe)], check=True)
+    env = dict(os.environ)
+    env.pop("NMPC_AMD_DIFF2AMR_N", None)
+    res = subprocess.run([str(exe)], capture_output=True, text=True, env=env, timeout=120)
+    assert res.returncode == 0, res.stderr
+    st, n_macro, n_dims, nu, th = res.stdout.split()
+    assert (int(st), int(n_macro), int(n_dims), int(nu)) == (0, 20, 20, 2)
+    assert float(th) == pytest.approx(math.pi, abs=1e-6)  # create(): x = ocp.constraints.x0 = [0, 0, pi, ...]
+    # run-time override of the baked horizon
+    env["NMPC_AMD_DIFF2AMR_N"] = "12"
+    res = subprocess.run([str(exe)], capture_output=True, text=True, env=env, timeout=120)
+    assert res.stdout.split()[2] == "12"
+
+
+def test_generator_errors(tmp_path, caplog):
+    assert gen.main([]) == 1
+    assert "The path for the YAML file is required" in caplog.text
+    bad = tmp_path / "bad.yaml"
+    bad.write_text(yaml.safe_dump({"diff_params": {"tf_ini": 2.0, "freq": 40}}))
+    assert gen.main([str(bad), "--out", str(tmp_path / "o")]) == 1
+    assert "Failed to generate Acados solver libraries" in caplog.text
+    empty = tmp_path / "empty.yaml"
+    empty.write_text(yaml.safe_dump({"other": 1}))
+    assert gen.main([str(empty), "--out", str(tmp_path / "o2")]) == 0
+    assert "No parameters found in YAML file to generate the 'diff' libraries." in caplog.text

@@ -1,0 +1,70 @@
+"""GPU test of the model-descriptor codegen: a solver library generated from a non-default codegen yaml solves
+with the baked horizon, step size, parameters, bounds and weights (scripts/diff/generate_c_code.py:8-60) when the
+caller sets only x0 and the references, and matches the fp64 oracle configured with the same values
+(tolerance as test_gpu_parity.py)."""
+import ctypes
+import os
+import sys
+
+import numpy as np
+import pytest
+import yaml
+
+from nmpc_nav_control_amd import _lib
+from oracle.oracle import Oracle
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+import generate_solver_libs as gen  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+
+def test_generated_defaults_drive_the_solve(built, tmp_path):
+    cfg = yaml.safe_load(open(os.path.join(ROOT, "configs", "acados_models.yaml")))
+    dp = dict(cfg["diff_params"], tf_ini=0.5, freq=40, dist_b=0.3, tau_v=0.15, v_max=0.8, a_max=0.5,
+              Q_diag=[20.0, 20.0, 2.0, 0.0, 0.0, 0.0, 0.0], R_diag=[0.5, 0.5],
+              QN_diag=[200.0, 200.0, 20.0, 0.0, 0.0, 0.0, 0.0])
+    yml = tmp_path / "m.yaml"
+    yml.write_text(yaml.safe_dump({"diff_params": dp}))
+    assert gen.main([str(yml), "--out", str(tmp_path / "scripts")]) == 0
+    so = tmp_path / "scripts" / "diff" / "c_generated_code" / "libacados_ocp_solver_diff2amr.so"
+    L = _lib.lib()
+    S = ctypes.CDLL(str(so))
+    cp = ctypes.POINTER(_lib.SolverCapsule)
+    S.diff2amr_acados_create_capsule.restype = cp
+    S.diff2amr_acados_create.argtypes = [cp]
+    S.diff2amr_acados_solve.argtypes = [cp]
+    S.diff2amr_acados_free.argtypes = [cp]
+    S.diff2amr_acados_free_capsule.argtypes = [cp]
+    os.environ.pop("NMPC_AMD_DIFF2AMR_N", None)
+    cap = S.diff2amr_acados_create_capsule()
+    assert S.diff2amr_acados_create(cap) == 0
+    c = cap.contents
+    N, nx, nu = 20, 7, 2
+    dptr = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+    x0 = np.array([0.1, -0.2, 0.3, 0.2, 0.1, 0.15, 0.05])
+    for f in (b"lbx", b"ubx"):
+        assert L.ocp_nlp_constraints_model_set(c.nlp_config, c.nlp_dims, c.nlp_in, c.nlp_out, 0, f, dptr(x0)) == 0
+    rng = np.random.default_rng(4)
+    yref = np.zeros((N + 1, nx + nu))
+    yref[:, :3] = [0.6, 0.3, 0.5] + rng.uniform(-0.05, 0.05, (N + 1, 3))
+    for k in range(N + 1):
+        row = np.ascontiguousarray(yref[k, : (nx if k == N else nx + nu)])
+        assert L.ocp_nlp_cost_model_set(c.nlp_config, c.nlp_dims, c.nlp_in, k, b"yref", dptr(row)) == 0
+    assert S.diff2amr_acados_solve(cap) == 0
+    u0 = np.zeros(nu)
+    L.ocp_nlp_out_get(c.nlp_config, c.nlp_dims, c.nlp_out, 0, b"u", dptr(u0))
+    S.diff2amr_acados_free(cap)
+    S.diff2amr_acados_free_capsule(cap)
+
+    d = gen.load_parameters("diff", dp)
+    o = Oracle("diff", N, dt=d["tf"] / d["N"], p=d["p"] + [0.0], W=d["W"] + [0.0] * 6, W_e=d["W_e"] + [0.0] * 4,
+               lbx=d["lbx"] + [0, 0], ubx=d["ubx"] + [0, 0], lbu=d["lbu"] + [0, 0], ubu=d["ubu"] + [0, 0],
+               terminal_hack=0)
+    xb, ub = o.iterate_create()
+    st, _, _, ub_new = o.sqp_rti(xb, ub, x0, yref, np.array(d["W_e"]))
+    assert st == 0
+    np.testing.assert_allclose(u0, ub_new[0], atol=1e-3)
+    # the bound baked from a_max is active on the first input
+    assert np.abs(u0).max() == pytest.approx(0.5, abs=1e-3)

@@ -79,10 +79,16 @@ def test_solve_matches_oracle(built, kernel, model, N, B, ticks):
 
 @pytest.mark.parametrize("kernel", KERNELS)
 @pytest.mark.parametrize("model", MODELS)
-def test_run_closed_loop_matches_oracle(built, kernel, model):
+@pytest.mark.parametrize("resets", [False, True])
+def test_run_closed_loop_matches_oracle(built, kernel, model, resets):
     """Batched run() + closed-loop plant on the GPU; the oracle replays the same per-tick inputs with its own
-    fp64 warm-start chain (prepare -> sqp_rti -> post, NMPCNavControl*::run)."""
+    fp64 warm-start chain (prepare -> sqp_rti -> post, NMPCNavControl*::run: no shift, x1 -> x0 carry of the
+    vel-refs, NMPCNavControlDiff.cpp:168-172). With resets, every fifth robot is reset
+    ({name}_acados_reset(capsule, 1), NMPCNavControlDiff.cpp:177-181) before the solves of ticks 3 and 8."""
+    if kernel == "lane" and resets:
+        pytest.skip("reset semantics are shared host logic; covered with the product kernel")
     N, B, T = 20, 70, 12
+    reset_mask = torch.from_numpy((np.arange(B) % 5 == 0).astype(np.uint8)).to(DEV)
     fl = make_fleet(model, B, seed=11)
     solver = BatchSolver(model, N, B, kernel=kernel)
     o = Oracle(model, N)
@@ -109,9 +115,10 @@ def test_run_closed_loop_matches_oracle(built, kernel, model):
         steer_h = np.ascontiguousarray(steer.cpu().numpy(), np.float64)
         traj_h = np.ascontiguousarray(traj.cpu().numpy().transpose(2, 0, 1), np.float64)
         tlen_h = np.ascontiguousarray(tlen.cpu().numpy(), np.int32)
-        solver.run(pose, vel, traj, steer=steer_arg, traj_len=tlen, cmd=cmd, u0=u0, status=status)
+        rs = reset_mask if resets and tick in (3, 8) else None
+        solver.run(pose, vel, traj, steer=steer_arg, traj_len=tlen, reset=rs, cmd=cmd, u0=u0, status=status)
         nf, cmd_o, u0_o, st_o, _ = o.batch_tick(pose_h, vel_h, steer_h if model == "tric" else None, traj_h, tlen_h,
-                                                None, carried, xbar, ubar)
+                                                None if rs is None else rs.cpu().numpy(), carried, xbar, ubar)
         torch.cuda.synchronize()
         assert nf == 0
         assert (status.cpu().numpy() == 0).all()
