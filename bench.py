@@ -258,7 +258,7 @@ def main():
             "metric": "SQP-RTI iterations/sec (whole node), diff N=40 batch=4096; u0 max-abs err",
             "value": round(value, 1), "unit": "SQP-RTI iterations/sec", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+            "scaling": "weak", "vs_baseline": None, "dtype": "fp32+fp64",
             "data": "synthetic seeded closed-loop fleet (SURVEY 8d), random-arc paths + goal poses",
             "config": {"workload": cfg["desc"], "config": args.config, "N": cfg["N"],
                        "batch_per_gpu": B_rank, "global_batch": B_rank * world,
