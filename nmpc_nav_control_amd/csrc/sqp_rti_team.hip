@@ -559,7 +559,7 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
             }
             const float rl = z - lb - tl, rr = ubd - z - tu;
             const float itl = frcp(tl), itu = frcp(tu);
-            res_ineq = nan_max(res_ineq, fmaxf(fabsf(rl), fabsf(rr)));
+            res_ineq = fmaxf(res_ineq, fmaxf(fabsf(rl), fabsf(rr)));  // NaN: caught by nanf_ (ghat, sig)
             sum_c += ll * tl + lu * tu;
             max_c = fmaxf(max_c, fmaxf(ll * tl, lu * tu));
             const float lamdiff = ll - lu;
@@ -574,7 +574,7 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
             const float g = rc[R::GR];
             const float base = hz + g - lamdiff + cpi;
             rc[R::RU] = base;  // read back for the u slots only
-            res_stat = nan_max(res_stat, vu ? fabsf(base) : 0.0f);
+            res_stat = fmaxf(res_stat, vu ? fabsf(base) : 0.0f);
             stat_scale = fmaxf(stat_scale, vu ? fmaxf(fabsf(cpi), fmaxf(fabsf(g), fabsf(lamdiff))) : 0.0f);
             const float ghat = valid ? (vu ? gh + base : gh) : 0.0f;
             const float pi_new = vx ? base : 0.0f;
