@@ -45,7 +45,8 @@ KERNELS = ["team", "lane"]
 
 @pytest.mark.parametrize("kernel", KERNELS)
 @pytest.mark.parametrize("model", MODELS)
-@pytest.mark.parametrize("N,B,ticks", [(20, 48, 8), (40, 5, 4)])
+# (80: the shipped codegen horizon; 1 and 2: the shortest horizons; B not a multiple of the 4 teams per wave)
+@pytest.mark.parametrize("N,B,ticks", [(20, 48, 8), (40, 5, 4), (80, 13, 3), (1, 7, 4), (2, 3, 4)])
 def test_solve_matches_oracle(built, kernel, model, N, B, ticks):
     o, rec = oracle_closed_loop(model, N, B, ticks)
     solver = BatchSolver(model, N, 64, kernel=kernel)
