@@ -36,6 +36,13 @@ __device__ unsigned long long g_stamps[256][2 + 4 * kStampIts];
     } while (0)
 // fine-grained stamps inside one P1 stage body (iteration 2, stage 20)
 __device__ unsigned long long g_stamps_p1[256][8];
+// end of the corrector backward sweep (C1) of iteration it, first team of the first 256 waves
+__device__ unsigned long long g_stamps_c1[256][kStampIts];
+#define STAMPC1()                                                                                                \
+    do {                                                                                                         \
+        if (it < kStampIts && r == 0 && (team & 3) == 0 && (team >> 2) < 256)                                   \
+            g_stamps_c1[team >> 2][it] = __builtin_amdgcn_s_memtime();                                           \
+    } while (0)
 #define STAMPF(slot)                                                                                             \
     do {                                                                                                         \
         if (it == 2 && k == 20 && r == 0 && (team & 3) == 0 && (team >> 2) < 256)                                 \
@@ -44,6 +51,7 @@ __device__ unsigned long long g_stamps_p1[256][8];
 #else
 #define STAMP(slot) ((void)0)
 #define STAMPF(slot) ((void)0)
+#define STAMPC1() ((void)0)
 #endif
 
 template <class M>
@@ -744,6 +752,7 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
                     }
                 });
             }
+            if (pass == 1) STAMPC1();
             // forward: du from the stored factor, dz, bounded-variable directions, next-stage dx
             float dxs = 0.0f, amax = 1e30f, s1 = 0.0f, s2 = 0.0f;
             sweepd(std::integral_constant<int, LIGHT_D>{}, 0, N, 1, ld, [&](int k, float (&rc)[RS]) {
@@ -891,6 +900,10 @@ template size_t team_scratch_floats<Omni4>(int, int);
 template size_t team_scratch_floats<Tric3>(int, int);
 
 #ifdef NMPC_STAMPS
+extern "C" int nmpc_debug_stamps_c1(unsigned long long* host)
+{
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_stamps_c1), sizeof(g_stamps_c1), 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -2;
+}
 extern "C" int nmpc_debug_stamps_p1(unsigned long long* host)
 {
     return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_stamps_p1), sizeof(g_stamps_p1), 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -2;

@@ -3,7 +3,7 @@ NMPC_STAMPS): P0 / P1 / F0 / C1F1 / safeguard cycles per IPM iteration and the P
 usage (GPU box): python tools/phase_stamps.py [model] [B] [N]"""
 import os, sys, ctypes, numpy as np, torch
 root = os.environ.get("GRAFT_REPO_ROOT", "/root/repo")
-os.environ["NMPC_AMD_LIB"] = os.path.join(root, "nmpc_nav_control_amd/lib/diag/libnmpc_amd.so")
+os.environ["NMPC_AMD_LIB"] = os.environ.get("STAMPS_LIB") or os.path.join(root, "nmpc_nav_control_amd/lib/diag/libnmpc_amd.so")
 sys.path.insert(0, root)
 import bench
 from nmpc_nav_control_amd._lib import lib
@@ -55,3 +55,16 @@ ok = (s2[:, 7] > s2[:, 0]) & (s2[:, 0] > 0)
 d2 = np.diff(s2[ok], axis=1)
 names = ["update+resid", "adjoint+terminal..Gd", "lba", "mrow", "cholesky", "rhs+LR+carry", "store"]
 print("P1 stage sub-phases (cycles, median over waves):", {n: int(np.median(d2[:, i])) for i, n in enumerate(names)}, "total", int(np.median(s2[ok, 7] - s2[ok, 0])))
+
+buf3 = (ctypes.c_ulonglong * (256 * 64))()
+L.nmpc_debug_stamps_c1.argtypes = [ctypes.c_void_p]
+assert L.nmpc_debug_stamps_c1(buf3) == 0
+s3 = np.frombuffer(buf3, dtype=np.uint64).reshape(256, 64).astype(np.int64)[:nw]
+c1, f1 = [], []
+for w in range(nw):
+    for i in range(min(itw[w], 64)):
+        base = 2 + 4 * i
+        if s3[w, i] > 0:
+            c1.append(s3[w, i] - st[w, base + 1])
+            f1.append(st[w, base + 2] - s3[w, i])
+print("C1 mean %.0f p50 %.0f   F1 mean %.0f p50 %.0f" % (np.mean(c1), np.median(c1), np.mean(f1), np.median(f1)))
