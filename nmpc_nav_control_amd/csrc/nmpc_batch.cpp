@@ -195,7 +195,10 @@ int nmpc_model_params_default(int model, int N, nmpc_model_params* prm)
     prm->qp_tol_ineq = 1e-6;
     prm->qp_tol_comp = 1e-10;
     prm->qp_mu0 = 1.0;
-    prm->qp_thr0 = 0.5;
+    // initial slack floor t0 = max(z - lb, thr0): 0.25 instead of the oracle's 0.5 starts nearly active bounds
+    // closer to their solution (steady-state closed loop: 8.0 -> 7.5 IPM iterations, 6 % faster ticks) while
+    // the cold-start tail grows by at most 2 iterations (DESIGN.md "Algorithm and precision")
+    prm->qp_thr0 = 0.25;
     prm->qp_tau = 0.995;
     return NMPC_OK;
 }
