@@ -70,6 +70,10 @@ class Fleet:
         self.model, self.B, self.N = model, B, N
         self.stream = stream  # None: the current stream; mixed fleets give each model its own HIP stream
         self.solver = BatchSolver(model, N, B, device=dev)
+        if stream is not None and "NMPC_AMD_SCHED" not in os.environ:
+            # concurrent launches of several models share the CUs: pair hard and easy blocks
+            # (include/nmpc_amd/nmpc_batch.h NMPC_SCHED_INTERLEAVED)
+            self.solver.set_schedule("interleaved")
         fl = make_fleet(model, B, seed=seed, start=start)
         t = lambda a, dt=torch.float32: torch.from_numpy(np.ascontiguousarray(a)).to(dev, dt)  # noqa: E731
         self.pose, self.vel, self.path, self.s = t(fl["pose"]), t(fl["vel"]), t(fl["path"]), t(fl["s"])

@@ -103,6 +103,23 @@ int nmpc_batch_run(nmpc_batch* b, int B, const float* pose, const float* vel, co
 #define NMPC_KERNEL_LANE 1
 int nmpc_batch_set_kernel(nmpc_batch* b, int kernel);
 
+/* Team placement of the team kernel (no effect on any result; DESIGN.md "Scheduling"). A robot's IPM iteration
+ * count persists from tick to tick, so the handle keeps each robot's last count and, before a launch, orders the
+ * robots by it (one small sort kernel on the same stream):
+ *   NMPC_SCHED_OFF          robot i in team slot i;
+ *   NMPC_SCHED_AUTO         (default) NMPC_SCHED_SORTED when the launch has more waves (B/4) than the device
+ *                           has SIMDs, else OFF (with one wave per SIMD the slowest robot sets the time
+ *                           whatever the placement);
+ *   NMPC_SCHED_SORTED       hardest robots in the lowest slots (tric N=60 B=8192: 5.24 -> 5.06 ms per tick);
+ *   NMPC_SCHED_INTERLEAVED  even 16-team blocks from the hard end, odd blocks from the easy end (best when
+ *                           several models' launches share the GPU on concurrent streams: mixed fleet
+ *                           4.44 -> 4.26 ms per tick). */
+#define NMPC_SCHED_OFF 0
+#define NMPC_SCHED_AUTO 1
+#define NMPC_SCHED_SORTED 2
+#define NMPC_SCHED_INTERLEAVED 3
+int nmpc_batch_set_schedule(nmpc_batch* b, int mode);
+
 /* Device pointers of the resident state: xbar [(N+1)*NX][stride], ubar [N*NU][stride],
  * carried [NBX][stride]; stride = capacity. */
 int nmpc_batch_state(nmpc_batch* b, float** xbar, float** ubar, float** carried, int* stride);

@@ -48,12 +48,14 @@ class SolverCapsule(ctypes.Structure):
 BATCH_SYMBOLS = [
     "nmpc_model_dims", "nmpc_model_params_default", "nmpc_model_params_set_limits", "nmpc_batch_create",
     "nmpc_batch_destroy", "nmpc_batch_set_params", "nmpc_batch_get_params", "nmpc_batch_init_iterate",
-    "nmpc_batch_solve", "nmpc_batch_run", "nmpc_batch_state", "nmpc_batch_set_kernel", "nmpc_fleet_sim_step",
+    "nmpc_batch_solve", "nmpc_batch_run", "nmpc_batch_state", "nmpc_batch_set_kernel", "nmpc_batch_set_schedule",
+    "nmpc_fleet_sim_step",
     "nmpc_last_error", "nmpc_version", "nmpc_path_discretize", "nmpc_codegen_default", "nmpc_capsule_new",
     "nmpc_capsule_delete", "nmpc_capsule_create", "nmpc_capsule_reset", "nmpc_capsule_update_params",
     "nmpc_capsule_solve", "nmpc_capsule_batch_solve", "nmpc_capsule_free", "nmpc_capsule_print_stats",
 ]
 KERNELS = {"team": 0, "lane": 1}
+SCHEDULES = {"off": 0, "auto": 1, "sorted": 2, "interleaved": 3}
 NLP_SYMBOLS = ["ocp_nlp_constraints_model_set", "ocp_nlp_cost_model_set", "ocp_nlp_out_get", "ocp_nlp_out_set",
                "ocp_nlp_get", "ocp_nlp_dims_get_from_attr"]
 CAPSULE_SUFFIXES = ["create_capsule", "free_capsule", "create", "create_with_discretization", "reset",
@@ -90,6 +92,7 @@ def lib():
     L.nmpc_batch_solve.argtypes = [vp, i, vp, vp, i, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]
     L.nmpc_batch_run.argtypes = [vp, i, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]
     L.nmpc_batch_set_kernel.argtypes = [vp, i]
+    L.nmpc_batch_set_schedule.argtypes = [vp, i]
     L.nmpc_batch_state.argtypes = [vp, ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.POINTER(vp), c_int_p]
     L.nmpc_fleet_sim_step.argtypes = [vp, i, vp, vp, vp, vp, vp, vp, vp, vp, vp, i, vp]
     L.nmpc_path_discretize.argtypes = [i, vp, i, vp, vp, ctypes.c_double, i, i, vp, vp, vp]

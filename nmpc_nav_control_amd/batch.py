@@ -9,7 +9,7 @@ import os
 
 import torch
 
-from ._lib import KERNELS, MODEL_IDS, ModelParams, check, default_params, lib, model_dims
+from ._lib import KERNELS, MODEL_IDS, SCHEDULES, ModelParams, check, default_params, lib, model_dims
 
 
 def _ptr(t):
@@ -57,6 +57,11 @@ class BatchSolver:
         """'team' (16-lane team per robot, default) or 'lane' (one lane per robot)."""
         check(lib().nmpc_batch_set_kernel(self._h, KERNELS[kernel]), "nmpc_batch_set_kernel")
         self.kernel = kernel
+
+    def set_schedule(self, mode):
+        """Team placement of the team kernel: 'auto' (default), 'off', 'sorted' or 'interleaved'
+        (include/nmpc_amd/nmpc_batch.h; no effect on any result)."""
+        check(lib().nmpc_batch_set_schedule(self._h, SCHEDULES[mode]), "nmpc_batch_set_schedule")
 
     def close(self):
         if self._h:

@@ -24,6 +24,11 @@ struct nmpc_batch {
     float* carried = nullptr;
     float* scratch = nullptr;
     int kernel = 0;  // 0: team-per-instance (default), 1: lane-per-instance
+    int sched = NMPC_SCHED_AUTO;
+    int n_simd = 1024;           // SIMDs of the device (4 per CU)
+    int* iter_key = nullptr;     // [capacity] last executed IPM iterations per robot (written by the team kernel)
+    int* order = nullptr;        // [capacity] team slot -> robot
+    int* sorted = nullptr;       // [capacity] sort scratch
 };
 
 namespace {
@@ -99,8 +104,22 @@ hipError_t launch_m(nmpc_batch* b, const KArgs& a, int mode, hipStream_t s)
                                          : launch_sqp_rti_team<M>(b->kp, a, mode, s);
 }
 
-hipError_t launch(nmpc_batch* b, const KArgs& a, int mode, hipStream_t s)
+// Team placement before a team-kernel launch (schedule.hip); fills a.order / a.iter_key
+hipError_t schedule(nmpc_batch* b, KArgs& a, hipStream_t s)
 {
+    if (b->kernel != NMPC_KERNEL_TEAM) return hipSuccess;
+    a.iter_key = b->iter_key;
+    int layout = b->sched;
+    if (layout == NMPC_SCHED_AUTO) layout = ((a.B + 3) / 4 > b->n_simd) ? NMPC_SCHED_SORTED : NMPC_SCHED_OFF;
+    if (layout == NMPC_SCHED_OFF) return hipSuccess;
+    a.order = b->order;
+    return launch_team_order(b->iter_key, a.B, layout, b->sorted, b->order, s);
+}
+
+hipError_t launch(nmpc_batch* b, KArgs& a, int mode, hipStream_t s)
+{
+    const hipError_t e = schedule(b, a, s);
+    if (e != hipSuccess) return e;
     switch (b->prm.model) {
     case NMPC_MODEL_DIFF2AMR: return launch_m<Diff2>(b, a, mode, s);
     case NMPC_MODEL_OMNI4AMR: return launch_m<Omni4>(b, a, mode, s);
@@ -236,10 +255,24 @@ int nmpc_batch_create(const nmpc_model_params* prm, int capacity, nmpc_batch** o
     b->ny = b->nx + b->nu;
     b->kp = to_kparams(*prm, b->nx, b->nu, b->nbx, b->nbu);
     if (const char* kv = std::getenv("NMPC_AMD_KERNEL")) b->kernel = (std::strcmp(kv, "lane") == 0) ? 1 : 0;
+    if (const char* sv = std::getenv("NMPC_AMD_SCHED")) {  // off | auto | sorted | interleaved
+        const char* names[4] = {"off", "auto", "sorted", "interleaved"};
+        for (int i = 0; i < 4; i++)
+            if (std::strcmp(sv, names[i]) == 0) b->sched = i;
+    }
     const int N = prm->N;
     const size_t S = (size_t)capacity;
     hipError_t e;
-    if ((e = hipMalloc(&b->xbar, sizeof(float) * (N + 1) * b->nx * S)) != hipSuccess ||
+    int dev = 0;
+    hipDeviceProp_t props;
+    if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&props, dev) == hipSuccess &&
+        props.multiProcessorCount > 0)
+        b->n_simd = 4 * props.multiProcessorCount;
+    if ((e = hipMalloc(&b->iter_key, sizeof(int) * S)) != hipSuccess ||
+        (e = hipMalloc(&b->order, sizeof(int) * S)) != hipSuccess ||
+        (e = hipMalloc(&b->sorted, sizeof(int) * S)) != hipSuccess ||
+        (e = hipMemset(b->iter_key, 0, sizeof(int) * S)) != hipSuccess ||
+        (e = hipMalloc(&b->xbar, sizeof(float) * (N + 1) * b->nx * S)) != hipSuccess ||
         (e = hipMalloc(&b->ubar, sizeof(float) * N * b->nu * S)) != hipSuccess ||
         (e = hipMalloc(&b->carried, sizeof(float) * b->nbx * S)) != hipSuccess ||
         (e = hipMalloc(&b->scratch, sizeof(float) * scratch_floats(prm->model, N, capacity))) != hipSuccess) {
@@ -263,6 +296,9 @@ int nmpc_batch_destroy(nmpc_batch* b)
     (void)hipFree(b->ubar);
     (void)hipFree(b->carried);
     (void)hipFree(b->scratch);
+    (void)hipFree(b->iter_key);
+    (void)hipFree(b->order);
+    (void)hipFree(b->sorted);
     delete b;
     return NMPC_OK;
 }
@@ -364,6 +400,14 @@ int nmpc_batch_set_kernel(nmpc_batch* b, int kernel)
     if (!b) return set_err(NMPC_ERR_ARG, "batch is NULL");
     if (kernel != NMPC_KERNEL_TEAM && kernel != NMPC_KERNEL_LANE) return set_err(NMPC_ERR_ARG, "unknown kernel");
     b->kernel = kernel;
+    return NMPC_OK;
+}
+
+int nmpc_batch_set_schedule(nmpc_batch* b, int mode)
+{
+    if (!b) return set_err(NMPC_ERR_ARG, "batch is NULL");
+    if (mode < NMPC_SCHED_OFF || mode > NMPC_SCHED_INTERLEAVED) return set_err(NMPC_ERR_ARG, "unknown schedule");
+    b->sched = mode;
     return NMPC_OK;
 }
 

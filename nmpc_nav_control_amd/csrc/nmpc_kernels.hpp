@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 #include <stddef.h>
 
+#include "nmpc_amd/nmpc_batch.h"
 #include "nmpc_amd/nmpc_path.h"
 #include "nmpc_models.hpp"
 
@@ -42,6 +43,9 @@ struct KArgs {
     float* qp_res; // [3][B] res_stat, res_ineq, mu at IPM exit
     float* xtraj;  // [(N+1)*NX][B]
     float* utraj;  // [N*NU][B]
+    // team placement (schedule.hip): team slot -> instance, or nullptr (slot i = instance i)
+    const int* order;
+    int* iter_key;  // [stride] resident: executed IPM iterations of the last solve, or nullptr
 };
 
 template <int NU>
@@ -84,6 +88,7 @@ template <class M>
 hipError_t launch_fleet_sim(const KParams& P, int B, int stride, const float* path, float* s, float* pose, float* vel,
                             float* steer, const float* u0, const int* status, const float* carried, float* traj,
                             int* traj_len, int advance, hipStream_t stream);
+hipError_t launch_team_order(const int* key, int B, int layout, int* sorted, int* order, hipStream_t stream);
 hipError_t launch_path_discretize(int B, const nmpc_path_segment* segs, int seg_stride, const int* nseg,
                                   const double* nearest_u, double period, int num_poses, int holo, float* traj,
                                   double* traj64, hipStream_t stream);

@@ -1,0 +1,89 @@
+// schedule.hip -- difficulty-ordered team placement for launches with more waves than SIMDs.
+//
+// The team kernel's time is the busiest SIMD's: a wave iterates until its slowest team converges, and when
+// a SIMD holds two or more waves they share its issue slots. A robot's IPM iteration count persists from
+// tick to tick (DESIGN.md "Scheduling"), so the previous tick's count (iter_key, written by the kernel)
+// predicts the next one. k_team_order sorts the robots by that key (stable counting sort, hardest first)
+// and lays the sorted list out over the team slots:
+//   sorted      slot s <- rank s: waves hold robots of like difficulty, the hard half of the blocks is
+//               dispatched first;
+//   interleaved even blocks take ranks from the hard end, odd blocks from the easy end, so neighbouring
+//               blocks (which share CUs) pair a hard block with an easy one.
+// Every robot keeps its own arithmetic whatever slot it lands in, so the order changes no result.
+#include "nmpc_kernels.hpp"
+
+namespace nmpc {
+
+namespace {
+
+constexpr int kOrderThreads = 1024;
+constexpr int kOrderBins = 32;  // keys clamp to [0, 31] (IPM iterations; iter_max reaches 50 only on failures)
+
+__global__ __launch_bounds__(kOrderThreads) void k_team_order(const int* __restrict__ key, int B, int layout,
+                                                               int* __restrict__ sorted, int* __restrict__ order)
+{
+    // cnt[bin][thread]: private column per thread, then one exclusive scan in (bin descending, thread) order
+    __shared__ unsigned cnt[kOrderBins][kOrderThreads];
+    __shared__ unsigned part[kOrderThreads];
+    const int t = threadIdx.x;
+    const int E = (B + kOrderThreads - 1) / kOrderThreads;
+    const int i0 = min(B, t * E), i1 = min(B, i0 + E);
+    for (int b = 0; b < kOrderBins; b++) cnt[b][t] = 0;
+    for (int i = i0; i < i1; i++) {
+        const int k = min(max(key[i], 0), kOrderBins - 1);
+        cnt[kOrderBins - 1 - k][t]++;
+    }
+    __syncthreads();
+    // flattened index f = bin * T + thread; thread t scans f in [32 t, 32 t + 32)
+    unsigned loc[kOrderBins];
+    unsigned s = 0;
+#pragma unroll
+    for (int j = 0; j < kOrderBins; j++) {
+        const int f = t * kOrderBins + j;
+        loc[j] = s;
+        s += cnt[f / kOrderThreads][f % kOrderThreads];
+    }
+    part[t] = s;
+    __syncthreads();
+    // Hillis-Steele inclusive scan of the partial sums
+    for (int d = 1; d < kOrderThreads; d <<= 1) {
+        const unsigned v = (t >= d) ? part[t - d] : 0u;
+        __syncthreads();
+        part[t] += v;
+        __syncthreads();
+    }
+    const unsigned base = part[t] - s;
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < kOrderBins; j++) {
+        const int f = t * kOrderBins + j;
+        cnt[f / kOrderThreads][f % kOrderThreads] = base + loc[j];
+    }
+    __syncthreads();
+    int* dst = (layout == NMPC_SCHED_SORTED) ? order : sorted;
+    for (int i = i0; i < i1; i++) {
+        const int k = min(max(key[i], 0), kOrderBins - 1);
+        dst[cnt[kOrderBins - 1 - k][t]++] = i;
+    }
+    if (layout == NMPC_SCHED_SORTED) return;
+    __threadfence_block();
+    __syncthreads();
+    // interleaved: slot s in block j = s / 16 (16 teams per block); even blocks count up from the hardest
+    // rank, odd blocks down from the easiest (only the last block can be partial, so both runs are dense)
+    for (int sl = t; sl < B; sl += kOrderThreads) {
+        const int j = sl >> 4, w = sl & 15;
+        const int q = (j >> 1) * 16 + w;
+        order[sl] = sorted[(j & 1) ? B - 1 - q : q];
+    }
+}
+
+}  // namespace
+
+hipError_t launch_team_order(const int* key, int B, int layout, int* sorted, int* order, hipStream_t stream)
+{
+    if (B <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_team_order, dim3(1), dim3(kOrderThreads), 0, stream, key, B, layout, sorted, order);
+    return hipGetLastError();
+}
+
+}  // namespace nmpc

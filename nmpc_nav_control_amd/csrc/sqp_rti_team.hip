@@ -238,7 +238,7 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
     const int N = P.N;
     const size_t S = (size_t)a.stride;  // resident state stride (capacity)
     const size_t Bn = (size_t)a.B;
-    const int inst = team;
+    const int inst = a.order ? a.order[team] : team;  // difficulty-ordered placement (schedule.hip)
     const bool lv = r < NV;
     const bool is_u = r < NU;
     const bool is_x = lv && !is_u;
@@ -857,6 +857,7 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
         }
         if (a.status) a.status[inst] = status;
         if (a.qp_iter) a.qp_iter[inst] = it_done;
+        if (a.iter_key) a.iter_key[inst] = it_done;
         if (a.qp_res) {
 #pragma unroll
             for (int j = 0; j < 3; j++) a.qp_res[(size_t)j * Bn + inst] = exit_res[j];
