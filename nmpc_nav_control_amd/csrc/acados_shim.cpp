@@ -37,6 +37,13 @@ struct nmpc_capsule_impl {
     std::vector<double> lbu, ubu;    // N * NBU
     std::vector<double> p;           // (N+1) * NP
     std::vector<double> xbar, ubar;  // iterate (N+1)*NX, N*NU
+    // validation cache of the stage-uniform data (W, W_e, bounds of stages >= 1, inputs, p): the wrappers set
+    // them once in their constructors and only x0 and yref per tick, so solve() re-checks them only after a
+    // setter touched them
+    bool uniform_dirty = true, uniform_ok = false;
+    std::string uniform_why;
+    nmpc_model_params uniform_prm;
+    std::vector<double> uniform_We;
     double time_tot = 0.0, time_lin = 0.0, time_qp = 0.0;
     int status = 5, qp_iter = 0, sqp_iter = 0;  // ACADOS_READY before the first solve
     ocp_nlp_config config;
@@ -56,6 +63,9 @@ struct Engine {
     int cap = 0;
     float *x0 = nullptr, *yref = nullptr, *We = nullptr, *xtraj = nullptr, *utraj = nullptr;
     int *status = nullptr, *qp_iter = nullptr;
+    // pinned host staging of the same shapes ([row][n] dense): no per-call allocation, DMA-able copies
+    float *h_x0 = nullptr, *h_yref = nullptr, *h_We = nullptr, *h_xb = nullptr, *h_ub = nullptr;
+    int *h_status = nullptr, *h_qp_iter = nullptr;
     ~Engine() { release(); }
     void release()
     {
@@ -63,8 +73,12 @@ struct Engine {
         batch = nullptr;
         (void)hipFree(x0); (void)hipFree(yref); (void)hipFree(We); (void)hipFree(xtraj); (void)hipFree(utraj);
         (void)hipFree(status); (void)hipFree(qp_iter);
+        (void)hipHostFree(h_x0); (void)hipHostFree(h_yref); (void)hipHostFree(h_We); (void)hipHostFree(h_xb);
+        (void)hipHostFree(h_ub); (void)hipHostFree(h_status); (void)hipHostFree(h_qp_iter);
         x0 = yref = We = xtraj = utraj = nullptr;
         status = qp_iter = nullptr;
+        h_x0 = h_yref = h_We = h_xb = h_ub = nullptr;
+        h_status = h_qp_iter = nullptr;
         cap = 0;
     }
 };
@@ -152,6 +166,7 @@ int impl_create(nmpc_capsule_impl* c, int N, const nmpc_codegen_desc& d)
     c->dims.nbu = c->nbu;
     c->dims.np = c->np;
     c->created = true;
+    c->uniform_dirty = true;
     c->status = 5;
     return 0;
 }
@@ -160,19 +175,18 @@ int impl_create(nmpc_capsule_impl* c, int N, const nmpc_codegen_desc& d)
 // batched kernel does not implement.
 struct Packed {
     nmpc_model_params prm;
-    std::vector<double> x0, yref, We;
+    const double* x0 = nullptr;    // stage-0 lbx (= ubx)
+    const double* yref = nullptr;  // (N+1) * NY
+    const double* We = nullptr;    // NX
 };
 
-bool pack(const nmpc_capsule_impl* c, Packed& o, std::string& why)
+// Stage-uniform data -> kernel parameters (validated: diagonal W identical on stages 0..N-1, diagonal W_e,
+// bounds and parameters identical on their stages)
+bool validate_uniform(nmpc_capsule_impl* c, std::string& why)
 {
-    const int N = c->N, nx = c->nx, nu = c->nu, ny = c->ny;
-    o.prm = c->prm;
-    o.x0.resize(nx);
-    for (int i = 0; i < nx; i++) {
-        if (c->lbx[i] != c->ubx[i]) { why = "stage-0 lbx != ubx (x0 must be an equality)"; return false; }
-        o.x0[i] = c->lbx[i];
-    }
-    // stage weights: diagonal, identical on stages 0..N-1
+    const int N = c->N, nx = c->nx, ny = c->ny;
+    nmpc_model_params& prm = c->uniform_prm;
+    prm = c->prm;
     const double* W0 = c->W.data();
     for (int k = 0; k < N; k++) {
         const double* Wk = c->W.data() + (size_t)k * ny * ny;
@@ -182,40 +196,83 @@ bool pack(const nmpc_capsule_impl* c, Packed& o, std::string& why)
                 if (Wk[i + ny * j] != W0[i + ny * j]) { why = "stage-varying W"; return false; }
             }
     }
-    for (int i = 0; i < ny; i++) o.prm.W[i] = W0[i + ny * i];
+    for (int i = 0; i < ny; i++) prm.W[i] = W0[i + ny * i];
     const double* WN = c->W.data() + (size_t)N * ny * ny;
-    o.We.resize(nx);
+    c->uniform_We.resize(nx);
     for (int j = 0; j < nx; j++)
         for (int i = 0; i < nx; i++) {
             if (i != j && WN[i + nx * j] != 0.0) { why = "non-diagonal W_e"; return false; }
-            if (i == j) o.We[i] = WN[i + nx * i];
+            if (i == j) c->uniform_We[i] = WN[i + nx * i];
         }
     for (int i = 0; i < c->nbx; i++) {
-        o.prm.lbx[i] = c->lbx[(size_t)nx + i];
-        o.prm.ubx[i] = c->ubx[(size_t)nx + i];
+        prm.lbx[i] = c->lbx[(size_t)nx + i];
+        prm.ubx[i] = c->ubx[(size_t)nx + i];
         for (int k = 2; k <= N; k++)
-            if (c->lbx[(size_t)k * nx + i] != o.prm.lbx[i] || c->ubx[(size_t)k * nx + i] != o.prm.ubx[i]) {
+            if (c->lbx[(size_t)k * nx + i] != prm.lbx[i] || c->ubx[(size_t)k * nx + i] != prm.ubx[i]) {
                 why = "stage-varying state bounds";
                 return false;
             }
     }
     for (int i = 0; i < c->nbu; i++) {
-        o.prm.lbu[i] = c->lbu[i];
-        o.prm.ubu[i] = c->ubu[i];
+        prm.lbu[i] = c->lbu[i];
+        prm.ubu[i] = c->ubu[i];
         for (int k = 1; k < N; k++)
-            if (c->lbu[(size_t)k * c->nbu + i] != o.prm.lbu[i] || c->ubu[(size_t)k * c->nbu + i] != o.prm.ubu[i]) {
+            if (c->lbu[(size_t)k * c->nbu + i] != prm.lbu[i] || c->ubu[(size_t)k * c->nbu + i] != prm.ubu[i]) {
                 why = "stage-varying input bounds";
                 return false;
             }
     }
     for (int i = 0; i < c->np; i++) {
-        o.prm.p[i] = c->p[i];
+        prm.p[i] = c->p[i];
         for (int k = 1; k < N; k++)
-            if (c->p[(size_t)k * c->np + i] != o.prm.p[i]) { why = "stage-varying parameters"; return false; }
+            if (c->p[(size_t)k * c->np + i] != prm.p[i]) { why = "stage-varying parameters"; return false; }
     }
-    o.yref.assign(c->yref.begin(), c->yref.end());
-    (void)nu;
     return true;
+}
+
+bool pack(nmpc_capsule_impl* c, Packed& o, std::string& why)
+{
+    for (int i = 0; i < c->nx; i++)
+        if (c->lbx[i] != c->ubx[i]) { why = "stage-0 lbx != ubx (x0 must be an equality)"; return false; }
+    if (c->uniform_dirty) {
+        c->uniform_why.clear();
+        c->uniform_ok = validate_uniform(c, c->uniform_why);
+        c->uniform_dirty = false;
+    }
+    if (!c->uniform_ok) {
+        why = c->uniform_why;
+        return false;
+    }
+    o.prm = c->uniform_prm;
+    o.x0 = c->lbx.data();
+    o.yref = c->yref.data();
+    o.We = c->uniform_We.data();
+    return true;
+}
+
+// dst[r * n + q] = (float)src[q][r] for r < rows, q < n: capsule-major host data -> instance-minor staging,
+// in blocks of 32 capsules (each row of a block is one 128-B line; 32 read streams)
+void to_soa(float* dst, int n, size_t rows, const std::vector<const double*>& src)
+{
+    for (int q0 = 0; q0 < n; q0 += 32) {
+        const int q1 = std::min(n, q0 + 32);
+        for (size_t r = 0; r < rows; r++) {
+            float* d = dst + r * n;
+            for (int q = q0; q < q1; q++) d[q] = (float)src[q][r];
+        }
+    }
+}
+
+void from_soa(const float* srcv, int n, size_t rows, const std::vector<double*>& dst)
+{
+    for (int q0 = 0; q0 < n; q0 += 32) {
+        const int q1 = std::min(n, q0 + 32);
+        for (size_t r = 0; r < rows; r++) {
+            const float* v = srcv + r * n;
+            for (int q = q0; q < q1; q++)
+                if (dst[q]) dst[q][r] = v[q];
+        }
+    }
 }
 
 bool same_params(const nmpc_model_params& a, const nmpc_model_params& b)
@@ -243,7 +300,14 @@ int ensure_engine(Engine& e, const nmpc_model_params& prm, int n, std::string& w
         (r = hipMalloc(&e.xtraj, sizeof(float) * (N + 1) * nx * cap)) != hipSuccess ||
         (r = hipMalloc(&e.utraj, sizeof(float) * N * nu * cap)) != hipSuccess ||
         (r = hipMalloc(&e.status, sizeof(int) * cap)) != hipSuccess ||
-        (r = hipMalloc(&e.qp_iter, sizeof(int) * cap)) != hipSuccess) {
+        (r = hipMalloc(&e.qp_iter, sizeof(int) * cap)) != hipSuccess ||
+        (r = hipHostMalloc(&e.h_x0, sizeof(float) * nx * cap)) != hipSuccess ||
+        (r = hipHostMalloc(&e.h_yref, sizeof(float) * (N + 1) * ny * cap)) != hipSuccess ||
+        (r = hipHostMalloc(&e.h_We, sizeof(float) * nx * cap)) != hipSuccess ||
+        (r = hipHostMalloc(&e.h_xb, sizeof(float) * (N + 1) * nx * cap)) != hipSuccess ||
+        (r = hipHostMalloc(&e.h_ub, sizeof(float) * N * nu * cap)) != hipSuccess ||
+        (r = hipHostMalloc(&e.h_status, sizeof(int) * cap)) != hipSuccess ||
+        (r = hipHostMalloc(&e.h_qp_iter, sizeof(int) * cap)) != hipSuccess) {
         why = hipGetErrorString(r);
         e.release();
         return -1;
@@ -267,45 +331,63 @@ void solve_group(std::vector<nmpc_capsule_impl*>& cs, std::vector<Packed>& ps, c
         for (int i : idx) cs[i]->status = 4;
     };
     if (ensure_engine(e, ps[idx[0]].prm, n, why)) return fail_all(why);
+    const auto ta = std::chrono::steady_clock::now();
     const int S = e.cap;
-    std::vector<float> hx0((size_t)nx * n), hyref((size_t)(N + 1) * ny * n), hWe((size_t)nx * n);
-    std::vector<float> hxb((size_t)(N + 1) * nx * n), hub((size_t)N * nu * n);
-    for (int q = 0; q < n; q++) {
-        const Packed& P = ps[idx[q]];
-        const nmpc_capsule_impl* c = cs[idx[q]];
-        for (int i = 0; i < nx; i++) {
-            hx0[(size_t)i * n + q] = (float)P.x0[i];
-            hWe[(size_t)i * n + q] = (float)P.We[i];
+    float *hx0 = e.h_x0, *hyref = e.h_yref, *hWe = e.h_We, *hxb = e.h_xb, *hub = e.h_ub;
+    const size_t n_x0 = (size_t)nx * n, n_yref = (size_t)(N + 1) * ny * n, n_xb = (size_t)(N + 1) * nx * n,
+                 n_ub = (size_t)N * nu * n;
+    {
+        std::vector<const double*> x0s(n), yrefs(n), Wes(n), xbs(n), ubs(n);
+        for (int q = 0; q < n; q++) {
+            const Packed& P = ps[idx[q]];
+            x0s[q] = P.x0;
+            yrefs[q] = P.yref;
+            Wes[q] = P.We;
+            xbs[q] = cs[idx[q]]->xbar.data();
+            ubs[q] = cs[idx[q]]->ubar.data();
         }
-        for (int k = 0; k <= N; k++)
-            for (int j = 0; j < ny; j++) hyref[((size_t)k * ny + j) * n + q] = (float)P.yref[(size_t)k * ny + j];
-        for (size_t r = 0; r < (size_t)(N + 1) * nx; r++) hxb[r * n + q] = (float)c->xbar[r];
-        for (size_t r = 0; r < (size_t)N * nu; r++) hub[r * n + q] = (float)c->ubar[r];
+        to_soa(hx0, n, nx, x0s);
+        to_soa(hWe, n, nx, Wes);
+        to_soa(hyref, n, (size_t)(N + 1) * ny, yrefs);
+        to_soa(hxb, n, (size_t)(N + 1) * nx, xbs);
+        to_soa(hub, n, (size_t)N * nu, ubs);
     }
+    const auto tb = std::chrono::steady_clock::now();
     float *dxb, *dub;
     nmpc_batch_state(e.batch, &dxb, &dub, nullptr, nullptr);
+    // the iterate goes to the dense [row][n] output buffers first (contiguous host->device copies), then into
+    // the [row][S] resident state by one device-side 2-D copy (a pitched copy from pageable host memory runs
+    // row by row); the solve overwrites the output buffers afterwards, in stream order
     hipError_t r = hipSuccess;
-    if ((r = hipMemcpy(e.x0, hx0.data(), sizeof(float) * hx0.size(), hipMemcpyHostToDevice)) != hipSuccess ||
-        (r = hipMemcpy(e.yref, hyref.data(), sizeof(float) * hyref.size(), hipMemcpyHostToDevice)) != hipSuccess ||
-        (r = hipMemcpy(e.We, hWe.data(), sizeof(float) * hWe.size(), hipMemcpyHostToDevice)) != hipSuccess ||
-        (r = hipMemcpy2D(dxb, sizeof(float) * S, hxb.data(), sizeof(float) * n, sizeof(float) * n, (size_t)(N + 1) * nx,
-                         hipMemcpyHostToDevice)) != hipSuccess ||
-        (r = hipMemcpy2D(dub, sizeof(float) * S, hub.data(), sizeof(float) * n, sizeof(float) * n, (size_t)N * nu,
-                         hipMemcpyHostToDevice)) != hipSuccess)
+    if ((r = hipMemcpy(e.x0, hx0, sizeof(float) * n_x0, hipMemcpyHostToDevice)) != hipSuccess ||
+        (r = hipMemcpy(e.yref, hyref, sizeof(float) * n_yref, hipMemcpyHostToDevice)) != hipSuccess ||
+        (r = hipMemcpy(e.We, hWe, sizeof(float) * n_x0, hipMemcpyHostToDevice)) != hipSuccess ||
+        (r = hipMemcpy(e.xtraj, hxb, sizeof(float) * n_xb, hipMemcpyHostToDevice)) != hipSuccess ||
+        (r = hipMemcpy(e.utraj, hub, sizeof(float) * n_ub, hipMemcpyHostToDevice)) != hipSuccess ||
+        (r = hipMemcpy2D(dxb, sizeof(float) * S, e.xtraj, sizeof(float) * n, sizeof(float) * n, (size_t)(N + 1) * nx,
+                         hipMemcpyDeviceToDevice)) != hipSuccess ||
+        (r = hipMemcpy2D(dub, sizeof(float) * S, e.utraj, sizeof(float) * n, sizeof(float) * n, (size_t)N * nu,
+                         hipMemcpyDeviceToDevice)) != hipSuccess)
         return fail_all(hipGetErrorString(r));
     const auto t1 = std::chrono::steady_clock::now();
     if (nmpc_batch_solve(e.batch, n, e.x0, e.yref, ny, e.We, nullptr, nullptr, nullptr, e.xtraj, e.utraj, e.status,
                          e.qp_iter, nullptr, nullptr) != NMPC_OK)
         return fail_all(nmpc_last_error());
-    std::vector<int> hst(n), hit(n);
-    if ((r = hipMemcpy(hxb.data(), e.xtraj, sizeof(float) * hxb.size(), hipMemcpyDeviceToHost)) != hipSuccess ||
-        (r = hipMemcpy(hub.data(), e.utraj, sizeof(float) * hub.size(), hipMemcpyDeviceToHost)) != hipSuccess ||
-        (r = hipMemcpy(hst.data(), e.status, sizeof(int) * n, hipMemcpyDeviceToHost)) != hipSuccess ||
-        (r = hipMemcpy(hit.data(), e.qp_iter, sizeof(int) * n, hipMemcpyDeviceToHost)) != hipSuccess)
+    int *hst = e.h_status, *hit = e.h_qp_iter;
+    if ((r = hipMemcpy(hxb, e.xtraj, sizeof(float) * n_xb, hipMemcpyDeviceToHost)) != hipSuccess ||
+        (r = hipMemcpy(hub, e.utraj, sizeof(float) * n_ub, hipMemcpyDeviceToHost)) != hipSuccess ||
+        (r = hipMemcpy(hst, e.status, sizeof(int) * n, hipMemcpyDeviceToHost)) != hipSuccess ||
+        (r = hipMemcpy(hit, e.qp_iter, sizeof(int) * n, hipMemcpyDeviceToHost)) != hipSuccess)
         return fail_all(hipGetErrorString(r));
     const auto t2 = std::chrono::steady_clock::now();
     const double tt = std::chrono::duration<double>(t2 - t0).count();
     const double tq = std::chrono::duration<double>(t2 - t1).count();
+    if (std::getenv("NMPC_AMD_SHIM_TIMING"))
+        std::fprintf(stderr, "[nmpc_amd] solve_group n=%d engine %.3f pack %.3f h2d %.3f solve+d2h %.3f ms\n", n,
+                     std::chrono::duration<double>(ta - t0).count() * 1e3,
+                     std::chrono::duration<double>(tb - ta).count() * 1e3,
+                     std::chrono::duration<double>(t1 - tb).count() * 1e3, tq * 1e3);
+    std::vector<double*> xbs(n), ubs(n);  // failed solves keep their iterate (nullptr: skipped)
     for (int q = 0; q < n; q++) {
         nmpc_capsule_impl* c = cs[idx[q]];
         c->status = hst[q];
@@ -315,11 +397,11 @@ void solve_group(std::vector<nmpc_capsule_impl*>& cs, std::vector<Packed>& ps, c
         c->time_tot = tt;
         c->time_qp = tq;
         c->time_lin = 0.0;
-        if (hst[q] == 0) {
-            for (size_t rr = 0; rr < (size_t)(N + 1) * nx; rr++) c->xbar[rr] = hxb[rr * n + q];
-            for (size_t rr = 0; rr < (size_t)N * nu; rr++) c->ubar[rr] = hub[rr * n + q];
-        }
+        xbs[q] = hst[q] == 0 ? c->xbar.data() : nullptr;
+        ubs[q] = hst[q] == 0 ? c->ubar.data() : nullptr;
     }
+    from_soa(hxb, n, (size_t)(N + 1) * nx, xbs);
+    from_soa(hub, n, (size_t)N * nu, ubs);
 }
 
 int batch_solve_impl(std::vector<nmpc_capsule_impl*>& cs, int* status_out)
@@ -384,12 +466,14 @@ int ocp_nlp_constraints_model_set(ocp_nlp_config* config, ocp_nlp_dims* dims, oc
         std::vector<double>& dst = (field[0] == 'l') ? c->lbx : c->ubx;
         const int n = (stage == 0) ? nx : c->nbx;  // nbx0 = NX (x0), nbx = NBX on idxbx
         for (int i = 0; i < n; i++) dst[(size_t)stage * nx + i] = v[i];
+        if (stage > 0) c->uniform_dirty = true;
         return 0;
     }
     if (!std::strcmp(field, "lbu") || !std::strcmp(field, "ubu")) {
         if (stage >= c->N) return -1;
         std::vector<double>& dst = (field[0] == 'l') ? c->lbu : c->ubu;
         for (int i = 0; i < c->nbu; i++) dst[(size_t)stage * c->nbu + i] = v[i];
+        c->uniform_dirty = true;
         return 0;
     }
     log_err("ocp_nlp_constraints_model_set", std::string("unsupported field ") + field);
@@ -409,6 +493,7 @@ int ocp_nlp_cost_model_set(ocp_nlp_config* config, ocp_nlp_dims* dims, ocp_nlp_i
         double* W = c->W.data() + (size_t)stage * c->ny * c->ny;
         std::fill(W, W + c->ny * c->ny, 0.0);
         for (int i = 0; i < n * n; i++) W[i] = v[i];  // col-major n x n
+        c->uniform_dirty = true;
         return 0;
     }
     if (!std::strcmp(field, "yref")) {
@@ -595,6 +680,7 @@ int nmpc_capsule_update_params(nmpc_solver_capsule* capsule, int stage, const do
     }
     if (stage < 0 || stage > c->N) return 1;
     for (int i = 0; i < np; i++) c->p[(size_t)stage * np + i] = value[i];
+    c->uniform_dirty = true;
     return 0;
 }
 
