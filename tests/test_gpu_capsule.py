@@ -108,3 +108,32 @@ def test_batch_solve_equals_individual(built):
         xb_, ub_ = b.iterate()
         np.testing.assert_allclose(ua, ub_, atol=1e-6)
         np.testing.assert_allclose(xa, xb_, atol=1e-6)
+
+
+def test_unsupported_ocp_data_rejected_and_recovered(built):
+    """The shim rejects OCP data the batched kernel does not implement (status 4 -> the wrapper's exception) and
+    re-validates after every setter: the cached stage-uniform data must not hide a later change either way."""
+    ctl, _ = make("diff")
+    x0 = np.array([0.1, -0.05, 0.3, 0.1, -0.1, 0.05, -0.05])
+    ctl._cset(0, "lbx", x0)
+    ctl._cset(0, "ubx", x0)
+    ctl._solve()
+    assert ctl.status == 0
+    Wd = np.diag(W_DIFF).astype(float)
+    Wn = Wd.copy()
+    Wn[0, 1] = Wn[1, 0] = 0.5
+    ctl._wset(3, "W", Wn.flatten(order="F"))
+    with pytest.raises(RuntimeError):
+        ctl._solve()
+    ctl._wset(3, "W", Wd.flatten(order="F"))
+    ctl._solve()
+    assert ctl.status == 0
+    ctl._cset(5, "lbu", np.array([-0.5, -1.0]))  # stage-varying input bound
+    with pytest.raises(RuntimeError):
+        ctl._solve()
+    ctl._cset(5, "lbu", np.array([-1.0, -1.0]))
+    ctl._solve()
+    assert ctl.status == 0
+    ctl._cset(0, "ubx", x0 + 0.1)  # x0 must stay an equality
+    with pytest.raises(RuntimeError):
+        ctl._solve()
