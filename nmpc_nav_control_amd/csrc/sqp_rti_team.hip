@@ -104,6 +104,19 @@ __device__ __forceinline__ void mrow_block(double (&acc)[NX + NU], double (&md)[
     if constexpr (NX == 7 && NU == 2) mrow_block_7_2(acc, md, lba);
     else mrow_block_11_4(acc, md, lba);
 }
+template <int NX, int NU>
+__device__ __forceinline__ void pg_block(double (&acc)[NX], const double (&prow)[NX + NU], const double (&gd)[NX])
+{
+    if constexpr (NX == 7 && NU == 2) pg_block_7_2(acc, prow, gd);
+    else pg_block_11_4(acc, prow, gd);
+}
+template <int NX, int NU>
+__device__ __forceinline__ void mrow_pg_block(double (&acc)[NX + NU], double& md0, const double (&pg)[NX],
+                                              const double (&gd)[NX])
+{
+    if constexpr (NX == 7 && NU == 2) mrow_pg_block_7_2(acc, md0, pg, gd);
+    else mrow_pg_block_11_4(acc, md0, pg, gd);
+}
 template <int NX, int NU, int J>
 __device__ __forceinline__ void chol_update(double (&lr)[NX + NU], double lj, double& piv)
 {
@@ -588,8 +601,12 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
             const float pi_new = vx ? base : 0.0f;
             if (ghat != ghat || sig != sig) nanf_ = 1.0f;
             if (k == N) {
-                // terminal: P_N = diag(W_e + Sigma) on the state lanes
+                // terminal: P_N = diag(W_e + Sigma) on the state lanes (square-root form: its Cholesky factor)
+#ifdef NMPC_SQRT_RICCATI
                 const double d = is_x ? sqrt((double)fmaxf(we_lane + sig, 0.0f)) : 0.0;
+#else
+                const double d = is_x ? (double)fmaxf(we_lane + sig, 0.0f) : 0.0;
+#endif
 #pragma unroll
                 for (int j = 0; j < NV; j++) Lrow[j] = (is_x && j == r) ? d : 0.0;
                 pv = is_x ? ghat : 0.0f;
@@ -597,6 +614,7 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
                 double Gd[NX];
 #pragma unroll
                 for (int l = 0; l < NX; l++) Gd[l] = (l < NGV) ? (double)Gc[l] : gcol64[l];
+#ifdef NMPC_SQRT_RICCATI
                 // LBA column v = L_{k+1}' G[:, v]; L[l][i] sits in lane NU+l at Lrow[NU+i]
                 double lba[NX];
 #pragma unroll
@@ -631,6 +649,34 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
                     // right-looking update M[r][j'] -= L[r][j] L[j'][j] (j' > j) and the next pivot
                     if constexpr (j + 1 < NV) chol_update<NX, NU, j>(Lr, lj, pivot);
                 });
+#else
+                // classic Riccati in fp64: PG column v = P_{k+1} G[:, v] (P[i][l] sits in lane NU+i at Lrow[NU+l]),
+                // row r of M = D + G' P G, then the right-looking row-distributed Cholesky of the input block only:
+                // after the NU input pivots the state block of M holds the Schur complement
+                // Qxx - Qxu Quu^-1 Qux = P_k, which the state lanes carry to the next stage
+                double pg[NX];
+#pragma unroll
+                for (int i = 0; i < NX; i++) pg[i] = 0.0;
+                STAMPF(2);
+                pg_block<NX, NU>(pg, Lrow, Gd);
+                STAMPF(3);
+                const double dg = valid ? (double)h_stage + (double)sig : 1.0;
+                double Lr[NV];
+#pragma unroll
+                for (int j = 0; j < NV; j++) Lr[j] = (r == j) ? dg : 0.0;
+                double pivot;
+                mrow_pg_block<NX, NU>(Lr, pivot, pg, Gd);  // pivot = M[0][0]
+                STAMPF(4);
+                sfor<0, NU>([&](auto jc) {
+                    constexpr int j = decltype(jc)::value;
+                    if (!(pivot > 0.0)) fail = true;
+                    const double rd = drsq(fmax(pivot, 1e-300));
+                    // lane j: Lr[j] == pivot; rows r < j are the upper triangle of the stored input columns (LM)
+                    const double lj = (r >= j) ? Lr[j] * rd : 0.0;
+                    Lr[j] = lj;
+                    chol_update<NX, NU, j>(Lr, lj, pivot);
+                });
+#endif
                 STAMPF(5);
                 float Lm[NU];
 #pragma unroll

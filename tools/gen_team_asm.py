@@ -51,6 +51,38 @@ def mrow_block(nx, nu):
             f" const double (&lba)[{nx}])\n{{\n    asm(\"{body}\"\n        : {outs}\n        : {ins});\n}}\n")
 
 
+def pg_block(nx, nu):
+    # classic Riccati: pg[i] += bcast_{nu+i}(Prow[nu+l]) * Gd[l] (column v of P_{k+1} [B A]); lane nu+i holds row i
+    # of P_{k+1}; operands: acc 0..nx-1 (+v), Prow x-part nx.., Gd 2nx..
+    lines = ["s_nop 1"]
+    for l in range(nx):
+        for i in range(nx):
+            lines.append(f"v_fmac_f64_dpp %{i}, %{nx + l}, %{2 * nx + l} row_newbcast:{nu + i}{M}")
+    outs = ", ".join(f'"+v"(acc[{i}])' for i in range(nx))
+    ins = ", ".join([f'"v"(prow[{nu + l}])' for l in range(nx)] + [f'"v"(gd[{l}])' for l in range(nx)])
+    body = "\\n\\t".join(lines)
+    return (f"__device__ __forceinline__ void pg_block_{nx}_{nu}(double (&acc)[{nx}], const double (&prow)[{nx + nu}],"
+            f" const double (&gd)[{nx}])\n{{\n    asm(\"{body}\"\n        : {outs}\n        : {ins});\n}}\n")
+
+
+def mrow_pg_block(nx, nu):
+    # classic Riccati: Mr[j] += bcast_j(pg[i]) * Gd[i] (row r of [B A]' P [B A]: lane r holds column r of [B A]),
+    # then md0 = bcast_0(Mr[0]), the first pivot; operands: Mr 0..nv-1 (+v), md0 (=v), pg .., Gd ..
+    nv = nx + nu
+    lines = ["s_nop 1"]
+    for i in range(nx):
+        for j in range(nv):
+            lines.append(f"v_fmac_f64_dpp %{j}, %{nv + 1 + i}, %{nv + 1 + nx + i} row_newbcast:{j}{M}")
+    lines.append("s_nop 1")
+    lines.append(f"v_mov_b64_dpp %{nv}, %0 row_newbcast:0{M}")
+    outs = ", ".join([f'"+v"(acc[{j}])' for j in range(nv)] + ['"=&v"(md0)'])
+    ins = ", ".join([f'"v"(pg[{i}])' for i in range(nx)] + [f'"v"(gd[{i}])' for i in range(nx)])
+    body = "\\n\\t".join(lines)
+    return (f"__device__ __forceinline__ void mrow_pg_block_{nx}_{nu}(double (&acc)[{nv}], double& md0,"
+            f" const double (&pg)[{nx}], const double (&gd)[{nx}])\n{{\n    asm(\"{body}\"\n        : {outs}\n"
+            f"        : {ins});\n}}\n")
+
+
 def chol_update(nx, nu):
     # column j done: Lr[jp] -= bcast_jp(lj) * lj for jp > j, then pivot of column j+1 = bcast_{j+1}(Lr[j+1])
     nv = nx + nu
@@ -97,7 +129,7 @@ def main():
              "#pragma once", "", "#include <hip/hip_runtime.h>", "", "namespace nmpc {", ""]
     for nx, nu in SHAPES:
         nv = nx + nu
-        parts += [lba_block(nx, nu), mrow_block(nx, nu), chol_update(nx, nu),
+        parts += [lba_block(nx, nu), mrow_block(nx, nu), pg_block(nx, nu), mrow_pg_block(nx, nu), chol_update(nx, nu),
                   dot_f32(nx, nu, f"dot_x_{nx}_{nu}"), dot_f32(nv, 0, f"dot_v_{nx}_{nu}")]
     parts += ["}  // namespace nmpc", ""]
     with open(OUT, "w") as fh:
