@@ -57,12 +57,16 @@ __device__ unsigned long long g_stamps_c1[256][kStampIts];
 template <class M>
 struct TeamRec {
     static constexpr int NX = M::NX, NU = M::NU, NV = NX + NU, NGV = M::NGV;
+    // Field order = the light sweeps' needs first, so they load a prefix of the record: the forward sweeps read
+    // [0, NF), the corrector's backward sweep [0, NB); P1 reads and writes all RS floats.
     static constexpr int TL = 0, TU = 1, LL = 2, LU = 3;  // slacks / multipliers of the box bound (bounded slots)
-    static constexpr int Z = 4, LB = 5, UB = 6, DZA = 7;   // QP iterate, bounds relative to the SQP iterate, affine dir
-    static constexpr int DZ = 8, GR = 9, RU = 10, LR = 11; // combined dir, cost gradient, u-residual, Luu^-1 rhs
-    static constexpr int LM = 12;                          // NU floats: row v of the stage factor, input columns
-    static constexpr int GV = LM + NU;                     // NGV floats: varying rows of column v of [B A]
-    static constexpr int RS = (GV + NGV + 3) / 4 * 4;      // record floats (dwordx4 aligned)
+    static constexpr int Z = 4, LB = 5, UB = 6, LR = 7;   // QP iterate, bounds relative to the SQP iterate, Luu^-1 rhs
+    static constexpr int LM = 8;                          // NU floats: row v of the stage factor, input columns
+    static constexpr int GV = LM + NU;                    // NGV floats: varying rows of column v of [B A]
+    static constexpr int DZA = GV + NGV, RU = DZA + 1;    // affine direction, u-stationarity residual
+    static constexpr int DZ = RU + 1, GR = RU + 2;        // combined direction, cost gradient (P1 only)
+    static constexpr int NF = DZA + 1, NB = RU + 1;       // prefixes read by the forward / backward light sweeps
+    static constexpr int RS = (GR + 1 + 3) / 4 * 4;       // record floats (dwordx4 aligned)
     static constexpr int NQ = RS / 4;
     static_assert(NV <= 16, "a team holds at most 16 variables");
 };
@@ -207,6 +211,35 @@ __device__ __forceinline__ void rec_load(const float* p, float (&v)[NQ * 4])
         v[4 * i + 1] = t.y;
         v[4 * i + 2] = t.z;
         v[4 * i + 3] = t.w;
+    }
+}
+
+// the first NF floats of a record: NF/4 dwordx4 loads and one dword, dwordx2 or dwordx3 load for the rest
+template <int NF, int RS>
+__device__ __forceinline__ void rec_load_prefix(const float* p, float (&v)[RS])
+{
+    static_assert(NF <= RS, "prefix longer than the record");
+    const float4* q = reinterpret_cast<const float4*>(p);
+#pragma unroll
+    for (int i = 0; i < NF / 4; i++) {
+        const float4 t = q[i];
+        v[4 * i + 0] = t.x;
+        v[4 * i + 1] = t.y;
+        v[4 * i + 2] = t.z;
+        v[4 * i + 3] = t.w;
+    }
+    constexpr int o = NF / 4 * 4, rem = NF % 4;
+    if constexpr (rem == 1) {
+        v[o] = p[o];
+    } else if constexpr (rem == 2) {
+        const float2 t = *reinterpret_cast<const float2*>(p + o);
+        v[o] = t.x;
+        v[o + 1] = t.y;
+    } else if constexpr (rem == 3) {
+        const float3 t = *reinterpret_cast<const float3*>(p + o);
+        v[o] = t.x;
+        v[o + 1] = t.y;
+        v[o + 2] = t.z;
     }
 }
 
@@ -502,18 +535,23 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
     };
     // D buffers: buf[i] holds stage k + i*dir while the loop is at k; after body(k + i*dir) it is refilled with
     // stage k + (i + D)*dir (clamped at k1), so D - 1 records are in flight during every body
-    auto sweepd = [&](auto dc, int k0, int k1, int dir, bool ld, auto&& body) {
+    auto sweepd = [&](auto dc, auto fc, int k0, int k1, int dir, bool ld, auto&& body) {
         constexpr int D = decltype(dc)::value;
+#ifdef NMPC_FULL_RECORD_LOADS
+        constexpr int F = RS + 0 * decltype(fc)::value;  // A/B: whole records
+#else
+        constexpr int F = decltype(fc)::value;  // floats of the record prefix this sweep reads
+#endif
         const ptrdiff_t step = ld ? (ptrdiff_t)KS * dir : 0;
         float buf[D][RS];
         const float* p = tbase + (size_t)k0 * KS;
         int kl = k0;
-        rec_load<NQ>(p, buf[0]);
+        rec_load_prefix<F, RS>(p, buf[0]);
         sfor<1, D>([&](auto ic) {
             constexpr int i = decltype(ic)::value;
             p = (kl == k1) ? p : p + step;
             kl = (kl == k1) ? kl : kl + dir;
-            rec_load<NQ>(p, buf[i]);
+            rec_load_prefix<F, RS>(p, buf[i]);
         });
         for (int k = k0;; k += D * dir) {
             bool stop = false;
@@ -527,7 +565,7 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
                 }
                 p = (kl == k1) ? p : p + step;
                 kl = (kl == k1) ? kl : kl + dir;
-                rec_load<NQ>(p, buf[i]);
+                rec_load_prefix<F, RS>(p, buf[i]);
             });
             if (stop) break;
         }
@@ -765,7 +803,7 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
             if (pass > 0) {
                 // corrector rhs through the stored factorisation (backward)
                 float pvc = 0.0f;
-                sweepd(std::integral_constant<int, LIGHT_D>{}, N, 0, -1, ld, [&](int k, float (&rc)[RS]) {
+                sweepd(std::integral_constant<int, LIGHT_D>{}, std::integral_constant<int, R::NB>{}, N, 0, -1, ld, [&](int k, float (&rc)[RS]) {
                     const bool vu = is_u && k < N;
                     float ghat;
                     {  // branch-free: 0 on the kFar-sentinel slots (see P0)
@@ -801,7 +839,7 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
             if (pass == 1) STAMPC1();
             // forward: du from the stored factor, dz, bounded-variable directions, next-stage dx
             float dxs = 0.0f, amax = 1e30f, s1 = 0.0f, s2 = 0.0f;
-            sweepd(std::integral_constant<int, LIGHT_D>{}, 0, N, 1, ld, [&](int k, float (&rc)[RS]) {
+            sweepd(std::integral_constant<int, LIGHT_D>{}, std::integral_constant<int, R::NF>{}, 0, N, 1, ld, [&](int k, float (&rc)[RS]) {
                 const bool vu = is_u && k < N;
                 const bool vx = is_x && k >= 1;
                 const bool valid = vu || vx;
