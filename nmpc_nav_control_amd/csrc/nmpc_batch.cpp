@@ -109,8 +109,9 @@ hipError_t schedule(nmpc_batch* b, KArgs& a, hipStream_t s)
 {
     if (b->kernel != NMPC_KERNEL_TEAM) return hipSuccess;
     a.iter_key = b->iter_key;
+    a.dense = ((a.B + 3) / 4 > b->n_simd) ? 1 : 0;  // 4 teams per wave
     int layout = b->sched;
-    if (layout == NMPC_SCHED_AUTO) layout = ((a.B + 3) / 4 > b->n_simd) ? NMPC_SCHED_SORTED : NMPC_SCHED_OFF;
+    if (layout == NMPC_SCHED_AUTO) layout = a.dense ? NMPC_SCHED_SORTED : NMPC_SCHED_OFF;
     if (layout == NMPC_SCHED_OFF) return hipSuccess;
     a.order = b->order;
     return launch_team_order(b->iter_key, a.B, layout, b->sorted, b->order, s);

@@ -46,6 +46,7 @@ struct KArgs {
     // team placement (schedule.hip): team slot -> instance, or nullptr (slot i = instance i)
     const int* order;
     int* iter_key;  // [stride] resident: executed IPM iterations of the last solve, or nullptr
+    int dense;      // the launch has more waves than the device has SIMDs (selects the team kernel variant)
 };
 
 template <int NU>

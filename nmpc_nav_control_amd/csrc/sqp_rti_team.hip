@@ -57,15 +57,19 @@ __device__ unsigned long long g_stamps_c1[256][kStampIts];
 template <class M>
 struct TeamRec {
     static constexpr int NX = M::NX, NU = M::NU, NV = NX + NU, NGV = M::NGV;
-    // Field order = the light sweeps' needs first, so they load a prefix of the record: the forward sweeps read
-    // [0, NF), the corrector's backward sweep [0, NB); P1 reads and writes all RS floats.
+    // Field order: the fields P1 rewrites first (it stores only that prefix, [0, NP1)), then the rest the light
+    // sweeps read (they load the prefix [0, NL)), then the P1-only inputs. P1 reads all RS floats.
     static constexpr int TL = 0, TU = 1, LL = 2, LU = 3;  // slacks / multipliers of the box bound (bounded slots)
-    static constexpr int Z = 4, LB = 5, UB = 6, LR = 7;   // QP iterate, bounds relative to the SQP iterate, Luu^-1 rhs
-    static constexpr int LM = 8;                          // NU floats: row v of the stage factor, input columns
-    static constexpr int GV = LM + NU;                    // NGV floats: varying rows of column v of [B A]
-    static constexpr int DZA = GV + NGV, RU = DZA + 1;    // affine direction, u-stationarity residual
-    static constexpr int DZ = RU + 1, GR = RU + 2;        // combined direction, cost gradient (P1 only)
-    static constexpr int NF = DZA + 1, NB = RU + 1;       // prefixes read by the forward / backward light sweeps
+    static constexpr int Z = 4, LR = 5;                   // QP iterate, Luu^-1 rhs
+    static constexpr int LM = 6;                          // NU floats: row v of the stage factor, input columns
+    static constexpr int RU = LM + NU;                    // u-stationarity residual
+    static constexpr int NP1 = RU + 1;                    // prefix rewritten by P1
+    static constexpr int LB = NP1, UB = NP1 + 1;          // bounds relative to the SQP iterate
+    static constexpr int GV = UB + 1;                     // NGV floats: varying rows of column v of [B A]
+    static constexpr int DZA = GV + NGV;                  // affine direction
+    static constexpr int NL = DZA + 1;                    // prefix read by the light sweeps
+    static constexpr int DZ = NL, GR = NL + 1;            // combined direction, cost gradient (P1 only)
+    static constexpr int NF = NL, NB = NL;
     static constexpr int RS = (GR + 1 + 3) / 4 * 4;       // record floats (dwordx4 aligned)
     static constexpr int NQ = RS / 4;
     static_assert(NV <= 16, "a team holds at most 16 variables");
@@ -87,6 +91,9 @@ constexpr float kStatRelT = 1e-5f;
 constexpr float kCompMaxRatio = 30.0f;
 #ifndef LIGHT_D
 #define LIGHT_D 4  // record buffers of the light (solve-only) sweeps
+#endif
+#ifndef P1_D
+#define P1_D 2  // record buffers of the factorisation sweep (2: ping-pong; 3 measured no faster)
 #endif
 constexpr float kFar = 1e30f;  // sentinel bound / slack of unbounded slots (z + kFar - kFar == 0 in fp32)
 #ifdef NMPC_STAMPS
@@ -200,55 +207,87 @@ __device__ __forceinline__ void rk4_column(const float* x, const float* u, const
     }
 }
 
-template <int NQ>
-__device__ __forceinline__ void rec_load(const float* p, float (&v)[NQ * 4])
+// Record access. A lane's record is NQ quads of 4 floats, QS floats apart, in one of two stage-block layouts:
+//   slot-major [slot][RS] (QS = 4): a lane's record is contiguous;
+//   quad-major [quad][slot 0..15][4] (QS = 64): quad i of a team's 16 slots is 256 contiguous bytes, so a
+//     dwordx4 access of a team touches 2 cache lines instead of one per two slots.
+// Measured per model in same-box A/B runs (ms per tick): omni4 (15 slots, 80-B records) 2.17 slot-major ->
+// 1.74 quad-major; diff 1.55 -> 1.57 and tric 4.48 -> 4.62 (9 slots) favour slot-major. RQM picks quad-major for
+// teams of more than 12 slots (NMPC_SLOT_MAJOR / NMPC_QUAD_MAJOR force one layout for A/B runs).
+template <int NV>
+constexpr bool rec_quad_major()
 {
-    const float4* q = reinterpret_cast<const float4*>(p);
-#pragma unroll
-    for (int i = 0; i < NQ; i++) {
-        const float4 t = q[i];
-        v[4 * i + 0] = t.x;
-        v[4 * i + 1] = t.y;
-        v[4 * i + 2] = t.z;
-        v[4 * i + 3] = t.w;
-    }
+#if defined(NMPC_SLOT_MAJOR)
+    return false;
+#elif defined(NMPC_QUAD_MAJOR)
+    return true;
+#else
+    return NV > 12;
+#endif
 }
+template <int RS, bool QM>
+constexpr int rec_qs() { return QM ? 64 : 4; }  // floats between a lane's consecutive quads
+template <int RS, bool QM>
+constexpr int rec_lane() { return QM ? 4 : RS; }  // floats between the records of consecutive slots
+template <int RS, bool QM>
+constexpr int rec_off(int f) { return (f / 4) * rec_qs<RS, QM>() + f % 4; }  // offset of field f in a lane's record
 
 // the first NF floats of a record: NF/4 dwordx4 loads and one dword, dwordx2 or dwordx3 load for the rest
-template <int NF, int RS>
+template <int NF, int RS, bool QM>
 __device__ __forceinline__ void rec_load_prefix(const float* p, float (&v)[RS])
 {
     static_assert(NF <= RS, "prefix longer than the record");
-    const float4* q = reinterpret_cast<const float4*>(p);
+    constexpr int QS = rec_qs<RS, QM>();
 #pragma unroll
     for (int i = 0; i < NF / 4; i++) {
-        const float4 t = q[i];
+        const float4 t = *reinterpret_cast<const float4*>(p + i * QS);
         v[4 * i + 0] = t.x;
         v[4 * i + 1] = t.y;
         v[4 * i + 2] = t.z;
         v[4 * i + 3] = t.w;
     }
     constexpr int o = NF / 4 * 4, rem = NF % 4;
+    const float* pr = p + (NF / 4) * QS;
     if constexpr (rem == 1) {
-        v[o] = p[o];
+        v[o] = pr[0];
     } else if constexpr (rem == 2) {
-        const float2 t = *reinterpret_cast<const float2*>(p + o);
+        const float2 t = *reinterpret_cast<const float2*>(pr);
         v[o] = t.x;
         v[o + 1] = t.y;
     } else if constexpr (rem == 3) {
-        const float3 t = *reinterpret_cast<const float3*>(p + o);
+        const float3 t = *reinterpret_cast<const float3*>(pr);
         v[o] = t.x;
         v[o + 1] = t.y;
         v[o + 2] = t.z;
     }
 }
 
-template <int NQ>
-__device__ __forceinline__ void rec_store(float* p, const float (&v)[NQ * 4])
+template <int RS, bool QM>
+__device__ __forceinline__ void rec_load(const float* p, float (&v)[RS])
 {
-    float4* q = reinterpret_cast<float4*>(p);
+    rec_load_prefix<RS, RS, QM>(p, v);
+}
+
+// floats [F0, NF) of a record, F0 a multiple of 4 (the fields P1 rewrites)
+template <int NF, int RS, bool QM, int F0 = 0>
+__device__ __forceinline__ void rec_store_prefix(float* p, const float (&v)[RS])
+{
+    static_assert(F0 % 4 == 0, "range starts on a quad");
+    constexpr int QS = rec_qs<RS, QM>();
 #pragma unroll
-    for (int i = 0; i < NQ; i++) q[i] = make_float4(v[4 * i + 0], v[4 * i + 1], v[4 * i + 2], v[4 * i + 3]);
+    for (int i = F0 / 4; i < NF / 4; i++)
+        *reinterpret_cast<float4*>(p + i * QS) = make_float4(v[4 * i + 0], v[4 * i + 1], v[4 * i + 2], v[4 * i + 3]);
+    constexpr int o = NF / 4 * 4, rem = NF % 4;
+    float* pr = p + (NF / 4) * QS;
+    if constexpr (rem == 1) pr[0] = v[o];
+    else if constexpr (rem == 2) *reinterpret_cast<float2*>(pr) = make_float2(v[o], v[o + 1]);
+    else if constexpr (rem == 3) *reinterpret_cast<float3*>(pr) = make_float3(v[o], v[o + 1], v[o + 2]);
+}
+
+template <int RS, bool QM>
+__device__ __forceinline__ void rec_store(float* p, const float (&v)[RS])
+{
+    rec_store_prefix<RS, RS, QM>(p, v);
 }
 
 // Newton directions of one bounded variable (lower slack tl / multiplier ll, upper tu / lu) for a step dz with
@@ -272,11 +311,15 @@ __device__ __forceinline__ float step_bound_r(float amax, float v, float dv)
     return (dv < 0.0f) ? fminf(amax, -v * frcp(dv)) : amax;
 }
 
-template <class M>
+// MS: store the slack / multiplier quad only where a bound lives (launches with more waves than SIMDs, where the
+// record traffic shows: tric N=60 B=8192 4.47 -> 4.39 ms; with one wave per SIMD the exec-mask switches cost
+// more than the bytes save: diff N=40 B=4096 1.555 -> 1.566 ms)
+template <class M, bool MS>
 __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int mode)
 {
     using R = TeamRec<M>;
-    constexpr int NX = M::NX, NU = M::NU, NV = R::NV, NGV = R::NGV, RS = R::RS, NQ = R::NQ;
+    constexpr int NX = M::NX, NU = M::NU, NV = R::NV, NGV = R::NGV, RS = R::RS;
+    constexpr bool QM = rec_quad_major<NV>();
     const int gt = blockIdx.x * blockDim.x + threadIdx.x;
     const int team = gt >> 4;
     const int r = gt & 15;
@@ -303,7 +346,7 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
     // this lane's record of stage k: tbase + k * 16 * RS
     // idle slots (r >= NV) alias slot 0's record: their (unpredicated) loads then read valid data and touch no
     // extra cache lines; they never store
-    float* const tbase = a.scratch + ((size_t)team * (N + 1) * 16 + (lv ? r : 0)) * RS;
+    float* const tbase = a.scratch + (size_t)team * (N + 1) * 16 * RS + (lv ? r : 0) * rec_lane<RS, QM>();
     constexpr int KS = 16 * RS;
 
 #define XB(k, j) a.xbar[((size_t)(k) * NX + (j)) * S + inst]
@@ -463,7 +506,7 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
         }
 #pragma unroll
         for (int i = 0; i < NGV; i++) rec[R::GV + i] = (k < N && lv) ? g[i] : 0.0f;
-        if (lv) rec_store<NQ>(tbase + (size_t)k * KS, rec);
+        if (lv) rec_store<RS, QM>(tbase + (size_t)k * KS, rec);
         // dynamics-feasible initial states: dx_{k+1} = A dx_k + b_k (inputs start at du = 0, dx_0 = x0 - xbar_0);
         // row i of [B A] dz: NGV row sums over the columns + the constant rows held in grow
         if (k < N) {
@@ -520,14 +563,14 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
         const ptrdiff_t step = ld ? (ptrdiff_t)KS * dir : 0;
         const float* p = tbase + (size_t)k0 * KS;
         float ra[RS], rb[RS];
-        rec_load<NQ>(p, ra);
+        rec_load<RS, QM>(p, ra);
         for (int k = k0;; k += 2 * dir) {
             const float* p1 = (k == k1) ? p : p + step;
-            rec_load<NQ>(p1, rb);
+            rec_load<RS, QM>(p1, rb);
             body(k, ra);
             if (k == k1) break;
             const float* p2 = (k + dir == k1) ? p1 : p1 + step;
-            rec_load<NQ>(p2, ra);
+            rec_load<RS, QM>(p2, ra);
             body(k + dir, rb);
             if (k + dir == k1) break;
             p = p2;
@@ -546,12 +589,12 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
         float buf[D][RS];
         const float* p = tbase + (size_t)k0 * KS;
         int kl = k0;
-        rec_load_prefix<F, RS>(p, buf[0]);
+        rec_load_prefix<F, RS, QM>(p, buf[0]);
         sfor<1, D>([&](auto ic) {
             constexpr int i = decltype(ic)::value;
             p = (kl == k1) ? p : p + step;
             kl = (kl == k1) ? kl : kl + dir;
-            rec_load_prefix<F, RS>(p, buf[i]);
+            rec_load_prefix<F, RS, QM>(p, buf[i]);
         });
         for (int k = k0;; k += D * dir) {
             bool stop = false;
@@ -565,7 +608,7 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
                 }
                 p = (kl == k1) ? p : p + step;
                 kl = (kl == k1) ? kl : kl + dir;
-                rec_load_prefix<F, RS>(p, buf[i]);
+                rec_load_prefix<F, RS, QM>(p, buf[i]);
             });
             if (stop) break;
         }
@@ -586,7 +629,14 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
         bool fail = false;
         const bool act = lv && !done;
         const float a_upd = (it > 0 && !done) ? alpha : 0.0f;
+        // P1_D record buffers: the heavy sweep's next records are in flight for P1_D - 1 stage bodies (at four
+        // waves per CU a record load from the Infinity Cache takes about one stage body)
+#if P1_D > 2
+        sweepd(std::integral_constant<int, P1_D>{}, std::integral_constant<int, RS>{}, N, 0, -1, act,
+               [&](int k, float (&rc)[RS]) {
+#else
         sweep(N, 0, -1, act, [&](int k, float (&rc)[RS]) {
+#endif
             STAMPF(0);
             const bool vu = is_u && k < N;
             const bool vx = is_x && k >= 1;
@@ -738,7 +788,18 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
             }
             piv = pi_new;
             STAMPF(6);
-            if (act) rec_store<NQ>(tbase + (size_t)k * KS, rc);
+#ifdef NMPC_FULL_RECORD_STORES
+            if (act) rec_store<RS, QM>(tbase + (size_t)k * KS, rc);
+#else
+            if constexpr (MS) {
+                // slack / multiplier quad only where a bound lives (elsewhere it holds the constant sentinel)
+                static_assert(R::TL == 0 && R::LU == 3, "bound quad first");
+                if (act && bnd) rec_store_prefix<4, RS, QM>(tbase + (size_t)k * KS, rc);
+                if (act) rec_store_prefix<R::NP1, RS, QM, 4>(tbase + (size_t)k * KS, rc);
+            } else {
+                if (act) rec_store_prefix<R::NP1, RS, QM>(tbase + (size_t)k * KS, rc);
+            }
+#endif
             STAMPF(7);
         });
         if (it < kStampItsC) STAMP(2 + 4 * it);
@@ -830,7 +891,7 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
                             if (r == j) my_lr = lrj;
                             y -= Lmj * lrj;
                         });
-                        if (ld && is_u) tbase[(size_t)k * KS + R::LR] = my_lr;
+                        if (ld && is_u) tbase[(size_t)k * KS + rec_off<RS, QM>(R::LR)] = my_lr;
                         rc[R::LR] = my_lr;
                         pvc = is_x ? y : 0.0f;
                     }
@@ -890,7 +951,7 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
                         s2 += d.dll * d.dtl + d.dlu * d.dtu;
                     }
                 }
-                if (ld && valid) tbase[(size_t)k * KS + (pass == 0 ? R::DZA : R::DZ)] = dz;
+                if (ld && valid) tbase[(size_t)k * KS + (pass == 0 ? rec_off<RS, QM>(R::DZA) : rec_off<RS, QM>(R::DZ))] = dz;
                 if (k < N) dxs = dyn(rc, valid ? dz : 0.0f);
             });
             amax = row_min16(lv ? amax : 1e30f);
@@ -914,7 +975,7 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
     // ---- full SQP step + outputs ----------------------------------------------------------------------
     if (status == 0) {
         for (int k = 0; k <= N; k++) {
-            const float z = lv ? tbase[(size_t)k * KS + R::Z] : 0.0f;
+            const float z = lv ? tbase[(size_t)k * KS + rec_off<RS, QM>(R::Z)] : 0.0f;
             if (is_x) {
                 const float nv = (k == 0) ? x0_lane : XB(k, xi) + z;
                 XB(k, xi) = nv;
@@ -973,7 +1034,10 @@ hipError_t launch_sqp_rti_team(const KParams& P, const KArgs& a, int mode, hipSt
     const int block = 256;  // 16 teams
     const long long threads = (long long)a.B * 16;
     const int grid = (int)((threads + block - 1) / block);
-    hipLaunchKernelGGL(k_sqp_rti_team<M>, dim3(grid), dim3(block), 0, stream, P, a, mode);
+    if (a.dense)
+        hipLaunchKernelGGL((k_sqp_rti_team<M, true>), dim3(grid), dim3(block), 0, stream, P, a, mode);
+    else
+        hipLaunchKernelGGL((k_sqp_rti_team<M, false>), dim3(grid), dim3(block), 0, stream, P, a, mode);
     return hipGetLastError();
 }
 
