@@ -149,7 +149,7 @@ class Emu:
                 np.einsum("bij,bj->bi", Q["B"][:, k], dz[:, k, :nu])
         return dz, ok
 
-    def solve(self, polish=None, verbose=False, single=None, start=None):
+    def solve(self, polish=None, verbose=False, single=None, start=None, eta_scale=1.0, lag2=None):
         """Run the IPM on every robot. polish: None or dict(mu=threshold, rho=..., tol=...) -- after the
         residual test of an iteration whose mu is below the threshold, try the active-set polish; a robot whose
         polish passes its KKT test stops there. Returns per-robot iterations, polish attempts, solutions."""
@@ -218,8 +218,14 @@ class Emu:
             if single is not None:  # one direction per iteration, centring sigma from a rule (no predictor)
                 sg = single(mu, alpha_prev, it)
                 smu = (sg * mu)[:, None, None] + 0 * z
-                dz, _ = self.riccati(sig, rhs(smu, smu))
-                d = dirs(dz, smu, smu)
+                tgl_, tgu_ = smu, smu
+                if lag2 is not None and it > 0:  # lagged second-order term from the previous direction
+                    A_ = (lag2 * alpha_prev)[:, None, None]
+                    tgl_ = smu - A_ * d_prev[2] * d_prev[0]
+                    tgu_ = smu - A_ * d_prev[3] * d_prev[1]
+                dz, _ = self.riccati(sig, rhs(tgl_, tgu_))
+                d = dirs(dz, tgl_, tgu_)
+                d_prev = d
                 am = np.minimum.reduce([amax(tl, d[0]), amax(tu, d[1]), amax(ll, d[2]), amax(lu, d[3])])
                 alpha = np.minimum(1.0, self.tau * am)
                 alpha_prev = alpha
@@ -238,8 +244,8 @@ class Emu:
             s = np.clip(np.where(mu > 0, mu_aff / mu, 0.0), 0, None)
             sigma = np.minimum(s ** 3, 1.0)
             smu = (sigma * mu)[:, None, None]
-            tgl = smu - A_ * da[2] * da[0]
-            tgu = smu - A_ * da[3] * da[1]
+            tgl = smu - eta_scale * A_ * da[2] * da[0]  # eta_scale 0: no second-order correction
+            tgu = smu - eta_scale * A_ * da[3] * da[1]
             dz, _ = self.riccati(sig, rhs(tgl, tgu))
             d = dirs(dz, tgl, tgu)
             am = np.minimum.reduce([amax(tl, d[0]), amax(tu, d[1]), amax(ll, d[2]), amax(lu, d[3])])
