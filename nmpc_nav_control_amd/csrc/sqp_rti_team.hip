@@ -899,7 +899,12 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
             }
             if (pass == 1) STAMPC1();
             // forward: du from the stored factor, dz, bounded-variable directions, next-stage dx
-            float dxs = 0.0f, amax = 1e30f, s1 = 0.0f, s2 = 0.0f;
+            float amax = 1e30f, s1 = 0.0f, s2 = 0.0f;
+            // CORR 0: affine pass, 1: corrector / safeguard pass (compile-time bodies), 2: one body, runtime pass
+            auto fwd = [&](auto cc) {
+            constexpr int CORR = decltype(cc)::value;
+            const bool corr = (CORR == 2) ? (pass > 0) : (CORR == 1);
+            float dxs = 0.0f;
             sweepd(std::integral_constant<int, LIGHT_D>{}, std::integral_constant<int, R::NF>{}, 0, N, 1, ld, [&](int k, float (&rc)[RS]) {
                 const bool vu = is_u && k < N;
                 const bool vx = is_x && k >= 1;
@@ -936,7 +941,7 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
                     const float rl = z - rc[R::LB] - tl, rr = rc[R::UB] - z - tu;
                     const float itl = frcp(tl), itu = frcp(tu);
                     float tgl = 0.0f, tgu = 0.0f;
-                    if (pass > 0) {
+                    if (corr) {
                         const BoundDir da = bound_dir(rc[R::DZA], rl, rr, tl, tu, ll, lu, itl, itu, 0.0f, 0.0f);
                         tgl = sigma_mu - eta * da.dll * da.dtl;
                         tgu = sigma_mu - eta * da.dlu * da.dtu;
@@ -946,14 +951,21 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
                     amax = step_bound_r(amax, tu, d.dtu);
                     amax = step_bound_r(amax, ll, d.dll);
                     amax = step_bound_r(amax, lu, d.dlu);
-                    if (pass == 0) {  // dll = dlu = 0 on sentinel slots at zero targets
+                    if (!corr) {  // dll = dlu = 0 on sentinel slots at zero targets
                         s1 += ll * d.dtl + tl * d.dll + lu * d.dtu + tu * d.dlu;
                         s2 += d.dll * d.dtl + d.dlu * d.dtu;
                     }
                 }
-                if (ld && valid) tbase[(size_t)k * KS + (pass == 0 ? rec_off<RS, QM>(R::DZA) : rec_off<RS, QM>(R::DZ))] = dz;
+                if (ld && valid) tbase[(size_t)k * KS + (!corr ? rec_off<RS, QM>(R::DZA) : rec_off<RS, QM>(R::DZ))] = dz;
                 if (k < N) dxs = dyn(rc, valid ? dz : 0.0f);
             });
+            };
+#ifdef NMPC_FSPEC
+            if (pass == 0) fwd(std::integral_constant<int, 0>{});
+            else fwd(std::integral_constant<int, 1>{});
+#else
+            fwd(std::integral_constant<int, 2>{});
+#endif
             amax = row_min16(lv ? amax : 1e30f);
             if (pass == 0) {
                 s1 = row_sum16(lv ? s1 : 0.0f);
