@@ -95,6 +95,21 @@ constexpr float kCompMaxRatio = 30.0f;
 #ifndef P1_D
 #define P1_D 2  // record buffers of the factorisation sweep (2: ping-pong; 3 measured no faster)
 #endif
+#ifndef NMPC_RING_KB
+#define NMPC_RING_KB 20  // 1-KB quad slots of each wave's LDS record ring
+#endif
+#if !defined(NMPC_LDS_RING) && !defined(NMPC_REG_SWEEPS)
+#define NMPC_REG_SWEEPS  // LDS record rings are opt-in (-DNMPC_LDS_RING) until measured on the GPU
+#endif
+#ifdef NMPC_REG_SWEEPS
+#define LIGHT_SWEEP sweepd
+#define LIGHT_DEPTH LIGHT_D
+#define LIGHT_Q(F) (F)
+#else
+#define LIGHT_SWEEP sweepl
+#define LIGHT_DEPTH LDR
+#define LIGHT_Q(F) (((F) + 3) / 4)
+#endif
 constexpr float kFar = 1e30f;  // sentinel bound / slack of unbounded slots (z + kFar - kFar == 0 in fp32)
 #ifdef NMPC_STAMPS
 constexpr int kStampItsC = kStampIts;
@@ -268,6 +283,26 @@ __device__ __forceinline__ void rec_load(const float* p, float (&v)[RS])
     rec_load_prefix<RS, RS, QM>(p, v);
 }
 
+// ---- LDS record rings ----------------------------------------------------------------
+// global_load_lds_dwordx4 moves quad q of every lane's record of a stage straight into a per-wave LDS slot
+// (wave-uniform base + lane * 16 B, no VGPR destination), the stage body reads its quads with ds_read_b128.
+// The DMAs are inline asm, outside the compiler's s_waitcnt bookkeeping: ring_wait<N>() retires a stage by count.
+__device__ __forceinline__ void glds16(const float* gsrc, uint32_t lds_byte_addr)
+{
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(gsrc), "s"(lds_byte_addr)
+                 : "memory");
+}
+template <int N>
+__device__ __forceinline__ void ring_wait()
+{
+    static_assert(N >= 0 && N < 64, "vmcnt is 6 bits");
+    asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
+}
+__device__ __forceinline__ void lds_retire() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
 // floats [F0, NF) of a record, F0 a multiple of 4 (the fields P1 rewrites)
 template <int NF, int RS, bool QM, int F0 = 0>
 __device__ __forceinline__ void rec_store_prefix(float* p, const float (&v)[RS])
@@ -348,6 +383,18 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
     // extra cache lines; they never store
     float* const tbase = a.scratch + (size_t)team * (N + 1) * 16 * RS + (lv ? r : 0) * rec_lane<RS, QM>();
     constexpr int KS = 16 * RS;
+#ifndef NMPC_REG_SWEEPS
+    // per-wave LDS record ring of RING 1-KB quad slots (20: 80 KB per 4-wave block, so two blocks of any model
+    // share a CU), used in turn by the P1 and the light sweeps
+    constexpr int LQ = (R::NL + 3) / 4;  // quads the light sweeps read
+    constexpr int RING = NMPC_RING_KB;
+    constexpr int LDR = RING / LQ;       // light-sweep ring stages (diff, tric: 5; omni4: 4)
+    constexpr int P1R = RING / R::NQ;    // P1 ring stages (diff: 5; omni4, tric: 4)
+    static_assert(LDR >= 2 && P1R >= 2, "ring too small");
+    __shared__ float4 lring[4][RING][64];
+    const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
+    const uint32_t ring0 = __builtin_amdgcn_readfirstlane((uint32_t)reinterpret_cast<uintptr_t>(&lring[wv][0][0]));
+#endif
 
 #define XB(k, j) a.xbar[((size_t)(k) * NX + (j)) * S + inst]
 #define UBAR(k, j) a.ubar[((size_t)(k) * NU + (j)) * S + inst]
@@ -613,6 +660,49 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
             if (stop) break;
         }
     };
+#ifndef NMPC_REG_SWEEPS
+    // LDS-ring sweep over k = k0, k0 + dir, ..., k1: D ring stages of NQL quads, D - 1 stages in flight while a
+    // body runs; at the top of body k stage k + (D-1)*dir goes into the slot the previous body read, then the wait
+    // retires stage k. Lanes that do not sweep re-read one fixed record; past k1 the source stays on k1.
+    auto sweepl = [&](auto dc, auto qc, int k0, int k1, int dir, bool ld, auto&& body) {
+        constexpr int D = decltype(dc)::value, NQL = decltype(qc)::value;
+        static_assert(D * NQL <= RING, "ring too small");
+        const ptrdiff_t step = ld ? (ptrdiff_t)KS * dir : 0;
+        const float* p = tbase + (size_t)k0 * KS;
+        int kl = k0;
+        auto issue = [&](int slot) {
+            const uint32_t base = ring0 + (uint32_t)(slot * NQL) * 1024u;
+            sfor<0, NQL>([&](auto qq) {
+                constexpr int q = decltype(qq)::value;
+                glds16(p + rec_off<RS, QM>(4 * q), base + (uint32_t)q * 1024u);
+            });
+            p = (kl == k1) ? p : p + step;
+            kl = (kl == k1) ? kl : kl + dir;
+        };
+        lds_retire();
+        sfor<0, D - 1>([&](auto ic) { issue(decltype(ic)::value); });
+        int slot = 0;
+        for (int k = k0;; k += dir) {
+            lds_retire();
+            issue(slot == 0 ? D - 1 : slot - 1);
+            ring_wait<(D - 1) * NQL>();
+            float rc[RS];
+            sfor<0, NQL>([&](auto qq) {
+                constexpr int q = decltype(qq)::value;
+                const float4 t = lring[wv][slot * NQL + q][ln];
+                rc[4 * q + 0] = t.x;
+                rc[4 * q + 1] = t.y;
+                rc[4 * q + 2] = t.z;
+                rc[4 * q + 3] = t.w;
+            });
+#pragma unroll
+            for (int f = 4 * NQL; f < RS; f++) rc[f] = 0.0f;
+            body(k, rc);
+            if (k == k1) break;
+            slot = (slot + 1 == D) ? 0 : slot + 1;
+        }
+    };
+#endif
     // ---- interior-point iterations ----------------------------------------------------------------------
     int status = 0, it_done = 0;
     bool done = false;
@@ -631,11 +721,14 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
         const float a_upd = (it > 0 && !done) ? alpha : 0.0f;
         // P1_D record buffers: the heavy sweep's next records are in flight for P1_D - 1 stage bodies (at four
         // waves per CU a record load from the Infinity Cache takes about one stage body)
-#if P1_D > 2
+#if defined(NMPC_REG_SWEEPS) && P1_D > 2
         sweepd(std::integral_constant<int, P1_D>{}, std::integral_constant<int, RS>{}, N, 0, -1, act,
                [&](int k, float (&rc)[RS]) {
-#else
+#elif defined(NMPC_REG_SWEEPS)
         sweep(N, 0, -1, act, [&](int k, float (&rc)[RS]) {
+#else
+        sweepl(std::integral_constant<int, P1R>{}, std::integral_constant<int, R::NQ>{}, N, 0, -1, act,
+               [&](int k, float (&rc)[RS]) {
 #endif
             STAMPF(0);
             const bool vu = is_u && k < N;
@@ -864,7 +957,7 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
             if (pass > 0) {
                 // corrector rhs through the stored factorisation (backward)
                 float pvc = 0.0f;
-                sweepd(std::integral_constant<int, LIGHT_D>{}, std::integral_constant<int, R::NB>{}, N, 0, -1, ld, [&](int k, float (&rc)[RS]) {
+                LIGHT_SWEEP(std::integral_constant<int, LIGHT_DEPTH>{}, std::integral_constant<int, LIGHT_Q(R::NB)>{}, N, 0, -1, ld, [&](int k, float (&rc)[RS]) {
                     const bool vu = is_u && k < N;
                     float ghat;
                     {  // branch-free: 0 on the kFar-sentinel slots (see P0)
@@ -905,7 +998,7 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
             constexpr int CORR = decltype(cc)::value;
             const bool corr = (CORR == 2) ? (pass > 0) : (CORR == 1);
             float dxs = 0.0f;
-            sweepd(std::integral_constant<int, LIGHT_D>{}, std::integral_constant<int, R::NF>{}, 0, N, 1, ld, [&](int k, float (&rc)[RS]) {
+            LIGHT_SWEEP(std::integral_constant<int, LIGHT_DEPTH>{}, std::integral_constant<int, LIGHT_Q(R::NF)>{}, 0, N, 1, ld, [&](int k, float (&rc)[RS]) {
                 const bool vu = is_u && k < N;
                 const bool vx = is_x && k >= 1;
                 const bool valid = vu || vx;
@@ -984,6 +1077,9 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
         if (it < kStampItsC) STAMP(5 + 4 * it);
     }
 
+#ifndef NMPC_REG_SWEEPS
+    ring_wait<0>();  // no LDS-DMA outlives the sweeps
+#endif
     // ---- full SQP step + outputs ----------------------------------------------------------------------
     if (status == 0) {
         for (int k = 0; k <= N; k++) {
