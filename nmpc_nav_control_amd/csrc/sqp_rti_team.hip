@@ -1053,7 +1053,8 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
                 if (k < N) dxs = dyn(rc, valid ? dz : 0.0f);
             });
             };
-#ifdef NMPC_FSPEC
+#ifndef NMPC_NO_FSPEC
+            // one compiled body per pass kind: same-box A/B diff metric 1.553 -> 1.526 ms, tric 4.382 -> 4.363 ms
             if (pass == 0) fwd(std::integral_constant<int, 0>{});
             else fwd(std::integral_constant<int, 1>{});
 #else
