@@ -25,9 +25,9 @@ import torch.distributed as dist
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-from nmpc_nav_control_amd.batch import BatchSolver  # noqa: E402
-from nmpc_nav_control_amd.scenario import DEFAULT_SEED, make_fleet  # noqa: E402
-from nmpc_nav_control_amd.sharding import CommandGather, TimedRegion, shard_range, world_info  # noqa: E402
+from nmpc_nav_control_amd.fleet import FleetNode  # noqa: E402
+from nmpc_nav_control_amd.scenario import DEFAULT_SEED  # noqa: E402
+from nmpc_nav_control_amd.sharding import TimedRegion, world_info  # noqa: E402
 
 # BASELINE.json configs (index -> seed offset 20250824 + idx)
 CONFIGS = {
@@ -44,17 +44,81 @@ MODEL_FLOPS = {"diff": dict(nx=7, nu=2, nbx=2, nbu=2, nnz_jx=12, nnz_ju=2, c_f=2
                "omni4": dict(nx=11, nu=4, nbx=4, nbu=4, nnz_jx=22, nnz_ju=4, c_f=40),
                "tric": dict(nx=7, nu=2, nbx=2, nbu=2, nnz_jx=12, nnz_ju=2, c_f=24)}
 FP32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 vector (and FP32-input MFMA) peak
+FP64_PEAK_SPEC_TFLOPS = 78.6  # AMD spec FP64 vector; replaced by the measured rate when profiles/<round> has it
+PROFILE_ROUND = "r02"
 HBM_PEAK_GBS = 8000.0
 
 
-def flops_per_instance(model, N, K):
+def flops_per_instance(model, N, K, split=False):
+    """SURVEY 8d algorithmic flops per instance-iteration, F = N*F_lin + K*N*F_ipm. With split=True returns
+    (fp32 flops, fp64 flops): the Riccati factorisation terms of F_ipm (P G, G'P G, the input-block Cholesky
+    and its Schur complement) run in fp64 on the device, everything else in fp32."""
     m = MODEL_FLOPS[model]
     nx, nu, nv = m["nx"], m["nu"], m["nx"] + m["nu"]
     f_lin = 4 * (m["c_f"] + 2 * m["nnz_jx"] * nv + m["nnz_ju"]) + 16 * nx * (1 + nv)
-    f_ipm = (2 * nv * nx * nx + nv * (nv + 1) * nx + (nu ** 3) // 3 + nu * nu * nx + nx * nx * nu + 4 * nv * nx
-             + 2 * nu * nx + nu * nu + 2 * nx * nv + 2 * nx * nx
-             + 20 * (m["nbx"] + m["nbu"]) + 4 * nx * nv)
-    return N * f_lin + K * N * f_ipm
+    f_fact = 2 * nv * nx * nx + nv * (nv + 1) * nx + (nu ** 3) // 3 + nu * nu * nx + nx * nx * nu
+    f_rest = (4 * nv * nx + 2 * nu * nx + nu * nu + 2 * nx * nv + 2 * nx * nx
+              + 20 * (m["nbx"] + m["nbu"]) + 4 * nx * nv)
+    total = N * f_lin + K * N * (f_fact + f_rest)
+    if split:
+        return N * f_lin + K * N * f_rest, K * N * f_fact
+    return total
+
+
+def _profile_json(name):
+    path = os.path.join(ROOT, "profiles", PROFILE_ROUND, name)
+    if os.path.exists(path):
+        with open(path) as fh:
+            return json.load(fh), os.path.relpath(path, ROOT)
+    return None, None
+
+
+def valu_peaks():
+    """(FP32, FP64) vector peaks in TFLOP/s. FP32: MI355X_MICROARCH.md (157.3, = the FP32 MFMA rate); FP64: the
+    full-occupancy v_fma_f64 rate measured by tools/ubench_valu.hip (the guide gives none; spec 78.6)."""
+    ub, _ = _profile_json("ubench_valu.json")
+    fp64 = float(ub["fp64_full"]["tflops"]) if ub else FP64_PEAK_SPEC_TFLOPS
+    return FP32_PEAK_TFLOPS, fp64
+
+
+def roofline(fleets, node, kernel_ms, steps):
+    """Roofline record of the solve kernel(s) of one step: algorithmic flops, split into the fp32
+    part and the fp64 Riccati factorisation, each priced at its own VALU peak; frac = the share of the VALU
+    time budget of the timed launches that the algorithmic flops would need at peak. The PMC-side figures
+    (L2<->fabric traffic, VALU issue share of the wave cycles) come from the rocprofv3 --pmc passes of the
+    same config (tools/pmc.sh -> tools/pmc_summary.py -> profiles/<round>/pmc/pmc_<config>.json)."""
+    t_k = float(np.mean(kernel_ms)) * 1e-3
+    f32 = f64 = 0.0
+    cbytes = 0
+    for j, f in enumerate(fleets):
+        sl = slice(node.offs[j], node.offs[j + 1])
+        k_f = float(node.iters_sum[sl].sum().item()) / (f.B * steps)
+        a, b = flops_per_instance(f.model, f.N, k_f, split=True)
+        f32 += f.B * a
+        f64 += f.B * b
+        cbytes += f.B * bytes_per_instance(f.model, f.N)
+    p32, p64 = valu_peaks()
+    a32, a64 = f32 / t_k / 1e12, f64 / t_k / 1e12
+    frac = a32 / p32 + a64 / p64
+    achieved = a32 + a64
+    cfg = "+".join(f"{f.model}_N{f.N}_B{f.B}" for f in fleets)
+    pmc, src = _profile_json(f"pmc/pmc_{cfg}.json")
+    traffic = pmc.get("l2_fabric_bytes_per_launch") if pmc else None
+    return {"bound": "valu", "achieved": round(achieved, 4), "peak": round(achieved / frac, 2), "unit": "TFLOP/s",
+            "frac": round(frac, 6), "traffic": traffic,
+            "fp32": {"flop_per_launch": f32, "achieved_tflops": round(a32, 4), "peak_tflops": p32,
+                     "frac": round(a32 / p32, 6)},
+            "fp64": {"flop_per_launch": f64, "achieved_tflops": round(a64, 4), "peak_tflops": p64,
+                     "frac": round(a64 / p64, 6), "peak_source": "tools/ubench_valu.hip (profiles/%s/ubench_valu.json)"
+                     % PROFILE_ROUND},
+            "issue": ({k: pmc.get(k) for k in ("valu_insts_per_wave", "valu_issue_frac", "wait_frac",
+                                               "active_frac", "source_commit")} if pmc else None),
+            "traffic_source": src, "kernel": f"k_sqp_rti_{fleets[0].solver.kernel}" +
+            (f" x{len(fleets)} concurrent streams" if len(fleets) > 1 else ""),
+            "kernel_ms_mean": round(t_k * 1e3, 4), "timing": "HIP events on the launch stream(s), timed region",
+            "compulsory_bytes_per_launch": cbytes, "achieved_compulsory_GBs": round(cbytes / t_k / 1e9, 2),
+            "note": "VALU-bound, latency-limited: <=15x15 per-robot blocks, no GEMM-shaped work (no MFMA); "
+                    "traffic = 2*FETCH_SIZE + WRITE_SIZE (L2<->fabric incl. Infinity-Cache hits) per launch"}
 
 
 def bytes_per_instance(model, N):
@@ -63,81 +127,34 @@ def bytes_per_instance(model, N):
     return 4 * (m["nx"] + 3 * (N + 1) + 2 * ((N + 1) * m["nx"] + N * m["nu"]) + 1)
 
 
-class Fleet:
-    """One model's robots on this GPU: solver + closed-loop state, all device-resident."""
-
-    def __init__(self, model, B, N, seed, dev, start=0, stream=None):
-        self.model, self.B, self.N = model, B, N
-        self.stream = stream  # None: the current stream; mixed fleets give each model its own HIP stream
-        self.solver = BatchSolver(model, N, B, device=dev)
-        if stream is not None and "NMPC_AMD_SCHED" not in os.environ:
-            # concurrent launches of several models share the CUs: pair hard and easy blocks
-            # (include/nmpc_amd/nmpc_batch.h NMPC_SCHED_INTERLEAVED)
-            self.solver.set_schedule("interleaved")
-        fl = make_fleet(model, B, seed=seed, start=start)
-        t = lambda a, dt=torch.float32: torch.from_numpy(np.ascontiguousarray(a)).to(dev, dt)  # noqa: E731
-        self.pose, self.vel, self.path, self.s = t(fl["pose"]), t(fl["vel"]), t(fl["path"]), t(fl["s"])
-        self.steer = t(fl["steer"]) if model == "tric" else None
-        _, _, cr = self.solver.state()
-        cr.copy_from(t(fl["carried"]))
-        self.traj = torch.zeros(N + 1, 3, B, device=dev)
-        self.tlen = torch.zeros(B, dtype=torch.int32, device=dev)
-        self.cmd = torch.zeros(3, B, device=dev)
-        self.u0 = torch.zeros(self.solver.nu, B, device=dev)
-        self.status = torch.zeros(B, dtype=torch.int32, device=dev)
-        self.qp_iter = torch.zeros(B, dtype=torch.int32, device=dev)
-        self.solver.fleet_sim_step(self.path, self.s, self.pose, self.vel, self.steer, None, None, self.traj,
-                                   self.tlen, advance=False)
-
-    def solve(self):
-        self.solver.run(self.pose, self.vel, self.traj, steer=self.steer, traj_len=self.tlen, cmd=self.cmd,
-                        u0=self.u0, status=self.status, qp_iter=self.qp_iter, stream=self.stream)
-
-    def advance(self):
-        self.solver.fleet_sim_step(self.path, self.s, self.pose, self.vel, self.steer, self.u0, self.status,
-                                   self.traj, self.tlen, advance=True, stream=self.stream)
-
-    def tick(self):
-        self.solve()
-        self.advance()
-
-
-def cpu_baseline(fleets, dev, sample, ticks, nthreads):
-    """Replay `ticks` closed-loop GPU ticks for the first `sample` robots of each fleet through the fp64
-    oracle. Every tick the oracle starts from exactly the GPU's pre-tick state (iterate, carried refs,
+def cpu_baseline(fleets, sample, ticks, nthreads):
+    """Replay `ticks` closed-loop GPU ticks for the first `sample` robots (0: all) of each fleet through the
+    fp64 oracle. Every tick the oracle starts from exactly the GPU's pre-tick state (iterate, carried refs,
     measurements, references), so the u0 error is the per-solve fp32-vs-fp64 error, not the divergence of
-    two closed loops. Returns (CPU instance-iterations/s, u0 max-abs err, failed, solves)."""
+    two closed loops. Returns (CPU instance-iterations/s, u0 max-abs err, failed, solves, 1-core rate)."""
     from oracle.oracle import Oracle
     total_time, total_solves, err, fails = 0.0, 0, 0.0, 0
     time_1, solves_1 = 0.0, 0
-    host = lambda a: np.ascontiguousarray(a.cpu().numpy(), np.float64)  # noqa: E731
     for f in fleets:
-        S = min(sample, f.B)
+        S = f.B if sample <= 0 else min(sample, f.B)
         o = Oracle(f.model, f.N)
-        xv, uv, cv = f.solver.state()
         for _ in range(ticks):
             torch.cuda.synchronize()
-            X, U, Cr = xv.to_tensor(), uv.to_tensor(), cv.to_tensor()
-            xbar = np.ascontiguousarray(host(X[:, :S]).T.reshape(S, f.N + 1, o.nx))
-            ubar = np.ascontiguousarray(host(U[:, :S]).T.reshape(S, f.N, o.nu))
-            carried = np.ascontiguousarray(host(Cr[:, :S]).T)
-            pose = np.ascontiguousarray(host(f.pose[:, :S]).T)
-            vel = np.ascontiguousarray(host(f.vel[:, :S]).T)
-            steer = host(f.steer[:S]) if f.steer is not None else None
-            traj = np.ascontiguousarray(host(f.traj[:, :, :S]).transpose(2, 0, 1))
-            tlen = np.ascontiguousarray(f.tlen[:S].cpu().numpy(), np.int32)
+            sn = f.snapshot()
+            sl = lambda a, n: None if a is None else np.ascontiguousarray(a[:n])  # noqa: E731
+            args = [sl(sn[k], S) for k in ("pose", "vel", "steer", "traj", "tlen")]
+            state = [sl(sn[k], S) for k in ("carried", "xbar", "ubar")]
             f.solve()
             # single-core rate on a slice of the same inputs (copies: batch_tick updates the iterate in place)
             S1 = min(S, 64)
-            sl = lambda a: None if a is None else np.array(a[:S1])  # noqa: E731
+            a1 = [sl(a, S1) for a in args]
+            s1 = [np.array(a[:S1]) for a in state]
             t0 = time.perf_counter()
-            o.batch_tick(sl(pose), sl(vel), sl(steer), sl(traj), sl(tlen), None, sl(carried), sl(xbar), sl(ubar),
-                         nthreads=1)
+            o.batch_tick(*a1, None, *s1, nthreads=1)
             time_1 += time.perf_counter() - t0
             solves_1 += S1
             t0 = time.perf_counter()
-            nf, cmd_o, u0_o, st_o, _ = o.batch_tick(pose, vel, steer, traj, tlen, None, carried, xbar, ubar,
-                                                    nthreads=nthreads)
+            nf, cmd_o, u0_o, st_o, _ = o.batch_tick(*args, None, *state, nthreads=nthreads)
             total_time += time.perf_counter() - t0
             total_solves += S
             torch.cuda.synchronize()
@@ -156,7 +173,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", default="metric", choices=sorted(CONFIGS))
     ap.add_argument("--closed-loop-warmup", type=int, default=20, help="ticks before timing (SURVEY 8d: T=20)")
-    ap.add_argument("--cpu-sample", type=int, default=256, help="robots per model replayed on the CPU oracle")
+    ap.add_argument("--cpu-sample", type=int, default=0,
+                    help="robots per model replayed on the CPU oracle (0: the whole batch)")
     ap.add_argument("--cpu-ticks", type=int, default=8)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--gather", action="store_true", help="all-gather u0+status to rank 0 every tick (RCCL)")
@@ -172,114 +190,63 @@ def main():
     gather = args.gather or (args.config == "mixed" and world > 1)
     # weak scaling: the global fleet holds B x world robots of each model; this rank owns the contiguous
     # shard [rank*B, (rank+1)*B) of it (sharding.shard_range), no collective on the solve path
-    fleets = []
-    multi = len(cfg["models"]) > 1
-    for j, (m, B) in enumerate(cfg["models"]):
-        lo, hi = shard_range(B * world, rank, world)
-        fleets.append(Fleet(m, hi - lo, cfg["N"], DEFAULT_SEED + cfg["idx"] + 100 * j, dev, start=lo,
-                            stream=torch.cuda.Stream(dev) if multi else None))
+    node = FleetNode(cfg["models"], cfg["N"], DEFAULT_SEED + cfg["idx"], dev, rank=rank, world=world, gather=gather)
+    fleets = node.fleets
     torch.cuda.synchronize()
-    main_stream = torch.cuda.current_stream()
-
-    def tick_all():
-        """One tick of every model's fleet. A mixed fleet runs its models' kernels concurrently, one HIP stream
-        each (every launch alone would leave SIMDs idle: ~2730 robots = 683 waves), joined on the main stream."""
-        if not multi:
-            fleets[0].tick()
-            return
-        start = torch.cuda.Event()
-        start.record(main_stream)
-        for f in fleets:
-            f.stream.wait_event(start)
-            f.tick()
-            done = torch.cuda.Event()
-            done.record(f.stream)
-            main_stream.wait_event(done)
-    B_rank = sum(f.B for f in fleets)
-    cmd_gather = CommandGather(5, [B_rank] * world, dev) if gather else None
-
-    def gather_commands():
-        cmd_gather([torch.cat([f.u0, f.status.float()[None]]) for f in fleets])
-
-    # executed IPM iterations and failures, accumulated on the device over the timed ticks
-    iters_sum = torch.zeros(B_rank, dtype=torch.int64, device=dev)
-    iters_max = torch.zeros(B_rank, dtype=torch.int32, device=dev)
-    fail_cnt = torch.zeros(B_rank, dtype=torch.int64, device=dev)
-    offs = [int(v) for v in np.cumsum([0] + [f.B for f in fleets])]
-
-    def accumulate():
-        for j, f in enumerate(fleets):
-            sl = slice(offs[j], offs[j + 1])
-            iters_sum[sl] += f.qp_iter
-            torch.maximum(iters_max[sl], f.qp_iter, out=iters_max[sl])
-            fail_cnt[sl] += f.status != 0
 
     # warmup runs every op of the timed loop (the first use of a torch kernel loads its code object)
     for _ in range(args.closed_loop_warmup + args.warmup):
-        tick_all()
-        accumulate()
-        if gather:
-            gather_commands()
-    for t_ in (iters_sum, iters_max, fail_cnt):
-        t_.zero_()
+        node.step()
+    node.reset_stats()
     torch.cuda.synchronize()
 
-    # per-kernel timing of the solve launches with HIP events on the launch stream
-    stream = torch.cuda.current_stream()
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    # per-kernel timing of the solve launches with HIP events on the launch streams: a single model's solve
+    # runs on the current stream; a mixed node's three solves run concurrently on their own streams, timed
+    # from one start event on the main stream to each stream's end-of-solve event (the region = the latest)
+    main_stream = torch.cuda.current_stream()
+    ev = [(torch.cuda.Event(enable_timing=True), [torch.cuda.Event(enable_timing=True) for _ in fleets])
+          for _ in range(args.steps)]
 
     with TimedRegion(dev) as region:
         for k in range(args.steps):
-            if multi:
-                tick_all()
-            else:
-                f = fleets[0]
-                ev[k][0].record(stream)
+            ev[k][0].record(main_stream)
+            if node.multi:
+                for f in fleets:
+                    f.stream.wait_event(ev[k][0])
+            for j, f in enumerate(fleets):
                 f.solve()
-                ev[k][1].record(stream)
+                ev[k][1][j].record(f.stream if f.stream is not None else main_stream)
                 f.advance()
-            accumulate()
+                if f.stream is not None:
+                    done = torch.cuda.Event()
+                    done.record(f.stream)
+                    main_stream.wait_event(done)
+            node.accumulate()
             if gather:
-                gather_commands()
+                node.gather_commands()
     elapsed = region.elapsed
 
-    kernel_ms = [ev[k][0].elapsed_time(ev[k][1]) for k in range(args.steps)] if len(fleets) == 1 else None
-    k_mean = float(iters_sum.sum().item()) / (B_rank * args.steps)
+    kernel_ms = [max(ev[k][0].elapsed_time(e) for e in ev[k][1]) for k in range(args.steps)]
+    B_rank = node.B
+    k_mean = float(node.iters_sum.sum().item()) / (B_rank * args.steps)
     units = args.steps * B_rank * world
     value = units / elapsed
 
     result = None
     if rank == 0:
-        roof = None
-        if kernel_ms:
-            f = fleets[0]
-            t_k = float(np.mean(kernel_ms)) * 1e-3
-            flops = f.B * flops_per_instance(f.model, f.N, k_mean)
-            achieved = flops / t_k / 1e12
-            traffic = None
-            pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-            if os.path.exists(pmc):
-                with open(pmc) as fh:
-                    d = json.load(fh)
-                key = f"{f.model}_N{f.N}_B{f.B}"
-                traffic = d.get(key, {}).get("hbm_bytes_per_launch")
-            roof = {"bound": "mfma", "achieved": round(achieved, 4), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
-                    "frac": round(achieved / FP32_PEAK_TFLOPS, 6), "traffic": traffic,
-                    "kernel": f"k_sqp_rti_{f.solver.kernel}", "kernel_ms_mean": round(t_k * 1e3, 4),
-                    "algorithmic_flop_per_launch": flops, "qp_iter_mean": round(k_mean, 3),
-                    "compulsory_bytes_per_launch": f.B * bytes_per_instance(f.model, f.N),
-                    "achieved_compulsory_GBs": round(f.B * bytes_per_instance(f.model, f.N) / t_k / 1e9, 2),
-                    "note": "FP32 VALU-bound (no GEMM-sized blocks); peak = MI355X FP32 vector = FP32 MFMA rate"}
+        roof = roofline(fleets, node, kernel_ms, args.steps)
         cpu = None
         u0_err = None
         if not args.no_cpu_baseline and world == 1:
             nthreads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
-            cpu_rate, u0_err, nf, ns, rate_1 = cpu_baseline(fleets, dev, args.cpu_sample, args.cpu_ticks, nthreads)
+            cpu_rate, u0_err, nf, ns, rate_1 = cpu_baseline(fleets, args.cpu_sample, args.cpu_ticks, nthreads)
             cpu = {"value": round(cpu_rate, 1), "unit": "SQP-RTI iterations/sec", "cores": nthreads, "kind": "port",
-                   "sample": f"{ns} instance-iterations: first {args.cpu_sample} robots of each model x "
+                   "sample": f"{ns} instance-iterations: {'all' if args.cpu_sample <= 0 else args.cpu_sample} robots of each model x "
                              f"{args.cpu_ticks} closed-loop ticks after the timed region, fp64 oracle/nmpc_oracle.c, "
                              f"OpenMP {nthreads} threads, identical inputs", "failed": nf,
-                   "value_1core": round(rate_1, 1)}
+                   "value_1core": round(rate_1, 1),
+                   "note": "a reported baseline, not a target: timed after the timed region on the GPU box's shared "
+                           "host cores, so it varies from run to run"}
         result = {
             "metric": "SQP-RTI iterations/sec (whole node), diff N=40 batch=4096; u0 max-abs err",
             "value": round(value, 1), "unit": "SQP-RTI iterations/sec", "n_gpus": world, "steps": args.steps,
@@ -290,8 +257,8 @@ def main():
                        "batch_per_gpu": B_rank, "global_batch": B_rank * world,
                        "models": [m for m, _ in cfg["models"]], "parallelism": f"instance-sharded x{world}",
                        "closed_loop_warmup_ticks": args.closed_loop_warmup, "rccl_gather": gather},
-            "u0_max_abs_err": u0_err, "qp_iter_mean": round(k_mean, 3), "qp_iter_max": int(iters_max.max().item()),
-            "failed_solves": int(fail_cnt.sum().item()), "roofline": roof, "cpu_baseline": cpu,
+            "u0_max_abs_err": u0_err, "qp_iter_mean": round(k_mean, 3), "qp_iter_max": int(node.iters_max.max().item()),
+            "failed_solves": int(node.fail_cnt.sum().item()), "roofline": roof, "cpu_baseline": cpu,
         }
         print(json.dumps(result), flush=True)
     if world > 1:

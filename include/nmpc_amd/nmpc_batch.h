@@ -69,8 +69,9 @@ int nmpc_batch_destroy(nmpc_batch* b);
 /* Replace weights / bounds / parameters / QP options (model and N must not change). */
 int nmpc_batch_set_params(nmpc_batch* b, const nmpc_model_params* prm);
 int nmpc_batch_get_params(const nmpc_batch* b, nmpc_model_params* prm);
-/* Re-initialise instances [0, B): mode 0 = create semantics, 1 = reset semantics (all zero). Both zero the
- * carried ref states. */
+/* Re-initialise instances [0, B): mode 0 = create semantics (x = [0,0,pi,0,...], u = 0, carried ref states 0);
+ * mode 1 = reset semantics ({name}_acados_reset: iterate zeroed, the carried ref states kept, like the
+ * per-robot `reset` mask of nmpc_batch_solve / nmpc_batch_run). */
 int nmpc_batch_init_iterate(nmpc_batch* b, int B, int mode, void* stream);
 
 /* One SQP-RTI iteration ({name}_acados_solve) for instances [0, B) on caller-packed QP data:
@@ -91,16 +92,18 @@ int nmpc_batch_solve(nmpc_batch* b, int B, const float* x0, const float* yref, i
  *         last valid pose, NMPCNavControlDiff.cpp:113-117)
  * outputs: cmd [3][B] (diff {v, w, 0}, omni4 {v, vn, w}, tric {v, alpha, 0}), u0 [NU][B], status, qp_iter,
  * qp_res [3][B] (as nmpc_batch_solve). The carried vel-ref states are kept on the device between calls
- * (NMPCNavControlDiff.cpp:168-172). */
+ * (NMPCNavControlDiff.cpp:168-172). A robot whose solve fails (status != 0) gets a zero (stop) cmd, keeps its
+ * carried refs and its iterate: the reference throws there and the node publishes a stop command
+ * (NMPCNavControl.cpp:14-23, NMPCNavControlROS.cpp:716-719). Failures stay on their robot: a NaN robot exits
+ * its IPM at the first iteration and no other robot's arithmetic depends on it. */
 int nmpc_batch_run(nmpc_batch* b, int B, const float* pose, const float* vel, const float* steer,
                    const float* traj, const int* traj_len, const unsigned char* reset, float* cmd, float* u0,
                    int* status, int* qp_iter, float* qp_res, void* stream);
 
-/* Kernel variant: NMPC_KERNEL_TEAM (default: 16-lane team per robot, DPP row exchange) or NMPC_KERNEL_LANE
- * (one lane per robot; best when B >= 64k per GPU). The environment variable NMPC_AMD_KERNEL=lane|team
- * sets the default at nmpc_batch_create. */
+/* Kernel variant: NMPC_KERNEL_TEAM (16-lane team per robot, DPP row exchange) is the only one; any other value
+ * returns NMPC_ERR_UNSUPPORTED. (The round-1 one-lane-per-robot kernel was removed: its fp32 factor is not
+ * accurate enough at bench scale, DESIGN.md "Algorithm and precision".) */
 #define NMPC_KERNEL_TEAM 0
-#define NMPC_KERNEL_LANE 1
 int nmpc_batch_set_kernel(nmpc_batch* b, int kernel);
 
 /* Team placement of the team kernel (no effect on any result; DESIGN.md "Scheduling"). A robot's IPM iteration

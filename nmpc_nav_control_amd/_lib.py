@@ -31,6 +31,14 @@ class ModelParams(ctypes.Structure):
     ]
 
 
+class CodegenDesc(ctypes.Structure):
+    """Mirror of nmpc_codegen_desc (include/nmpc_amd/nmpc_capsule.h)."""
+    _fields_ = [("model", ctypes.c_int), ("N", ctypes.c_int), ("tf", ctypes.c_double),
+                ("p", ctypes.c_double * 3), ("lbx", ctypes.c_double * 4), ("ubx", ctypes.c_double * 4),
+                ("lbu", ctypes.c_double * 4), ("ubu", ctypes.c_double * 4), ("W", ctypes.c_double * 15),
+                ("W_e", ctypes.c_double * 11)]
+
+
 class NlpOut(ctypes.Structure):
     """Mirror of the ocp_nlp_out handle (include/acados_c/ocp_nlp_interface.h)."""
     _fields_ = [("impl", c_void_p), ("inf_norm_res", ctypes.c_double), ("total_cost", ctypes.c_double),
@@ -54,7 +62,7 @@ BATCH_SYMBOLS = [
     "nmpc_capsule_delete", "nmpc_capsule_create", "nmpc_capsule_reset", "nmpc_capsule_update_params",
     "nmpc_capsule_solve", "nmpc_capsule_batch_solve", "nmpc_capsule_free", "nmpc_capsule_print_stats",
 ]
-KERNELS = {"team": 0, "lane": 1}
+KERNELS = {"team": 0}
 SCHEDULES = {"off": 0, "auto": 1, "sorted": 2, "interleaved": 3}
 NLP_SYMBOLS = ["ocp_nlp_constraints_model_set", "ocp_nlp_cost_model_set", "ocp_nlp_out_get", "ocp_nlp_out_set",
                "ocp_nlp_get", "ocp_nlp_dims_get_from_attr"]
@@ -96,6 +104,7 @@ def lib():
     L.nmpc_batch_state.argtypes = [vp, ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.POINTER(vp), c_int_p]
     L.nmpc_fleet_sim_step.argtypes = [vp, i, vp, vp, vp, vp, vp, vp, vp, vp, vp, i, vp]
     L.nmpc_path_discretize.argtypes = [i, vp, i, vp, vp, ctypes.c_double, i, i, vp, vp, vp]
+    L.nmpc_codegen_default.argtypes = [i, ctypes.POINTER(CodegenDesc)]
     L.nmpc_last_error.restype = ctypes.c_char_p
     L.nmpc_version.restype = ctypes.c_char_p
     cp = ctypes.POINTER(SolverCapsule)

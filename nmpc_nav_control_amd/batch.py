@@ -5,21 +5,29 @@ the instance-minor ``[field][B]`` layout of include/nmpc_amd/nmpc_batch.h. All c
 kernels of the library; there is no Python or CPU fallback.
 """
 import ctypes
-import os
 
 import torch
 
 from ._lib import KERNELS, MODEL_IDS, SCHEDULES, ModelParams, check, default_params, lib, model_dims
 
 
-def _ptr(t):
+def _ptr(t, dtype=None, shape=None, name="argument"):
+    """Device pointer of a contiguous CUDA tensor, checked against the dtype and shape the kernel reads (a
+    wrong dtype would be reinterpreted silently by the C ABI)."""
     if t is None:
         return None
     if not t.is_cuda:
-        raise ValueError("expected a device tensor")
+        raise ValueError(f"{name}: expected a device tensor")
     if not t.is_contiguous():
-        raise ValueError("expected a contiguous tensor")
+        raise ValueError(f"{name}: expected a contiguous tensor")
+    if dtype is not None and t.dtype not in (dtype if isinstance(dtype, tuple) else (dtype,)):
+        raise TypeError(f"{name}: expected dtype {dtype}, got {t.dtype}")
+    if shape is not None and tuple(t.shape) != tuple(shape):
+        raise ValueError(f"{name}: expected shape {tuple(shape)}, got {tuple(t.shape)}")
     return ctypes.c_void_p(t.data_ptr())
+
+
+F32, I32, U8 = torch.float32, torch.int32, (torch.uint8, torch.bool)
 
 
 def _stream(stream):
@@ -49,12 +57,12 @@ class BatchSolver:
         with torch.cuda.device(self.device):
             check(lib().nmpc_batch_create(ctypes.byref(self.params), self.capacity, ctypes.byref(self._h)),
                   "nmpc_batch_create")
-        self.kernel = os.environ.get("NMPC_AMD_KERNEL", "team")  # the library's own default selection
+        self.kernel = "team"
         if kernel is not None:
             self.set_kernel(kernel)
 
     def set_kernel(self, kernel):
-        """'team' (16-lane team per robot, default) or 'lane' (one lane per robot)."""
+        """'team' (16-lane team per robot): the only kernel."""
         check(lib().nmpc_batch_set_kernel(self._h, KERNELS[kernel]), "nmpc_batch_set_kernel")
         self.kernel = kernel
 
@@ -79,7 +87,8 @@ class BatchSolver:
         self.params = params
 
     def init_iterate(self, B=None, mode=0, stream=None):
-        """mode 0: {name}_acados_create semantics; mode 1: {name}_acados_reset (zeros)."""
+        """mode 0: {name}_acados_create semantics (carried refs zeroed); mode 1: {name}_acados_reset (iterate
+        zeroed, carried refs kept, as the per-robot reset mask)."""
         B = self.capacity if B is None else int(B)
         check(lib().nmpc_batch_init_iterate(self._h, B, int(mode), _stream(stream)), "nmpc_batch_init_iterate")
 
@@ -100,27 +109,40 @@ class BatchSolver:
     def solve(self, x0, yref, We=None, reset=None, u0=None, x1=None, xtraj=None, utraj=None, status=None,
               qp_iter=None, qp_res=None, stream=None):
         B = x0.shape[1]
+        if not 0 <= B <= self.capacity:
+            raise ValueError(f"batch {B} exceeds the capacity {self.capacity}")
         ny_in = yref.shape[1]
-        assert x0.shape == (self.nx, B) and yref.shape == (self.N + 1, ny_in, B)
-        if We is not None:
-            assert We.shape == (self.nx, B)
-        check(lib().nmpc_batch_solve(self._h, B, _ptr(x0), _ptr(yref), ny_in, _ptr(We), _ptr(reset), _ptr(u0),
-                                     _ptr(x1), _ptr(xtraj), _ptr(utraj), _ptr(status), _ptr(qp_iter),
-                                     _ptr(qp_res), _stream(stream)), "nmpc_batch_solve")
+        N, nx, nu = self.N, self.nx, self.nu
+        check(lib().nmpc_batch_solve(
+            self._h, B, _ptr(x0, F32, (nx, B), "x0"), _ptr(yref, F32, (N + 1, ny_in, B), "yref"), ny_in,
+            _ptr(We, F32, (nx, B), "We"), _ptr(reset, U8, (B,), "reset"), _ptr(u0, F32, (nu, B), "u0"),
+            _ptr(x1, F32, (nx, B), "x1"), _ptr(xtraj, F32, ((N + 1) * nx, B), "xtraj"),
+            _ptr(utraj, F32, (N * nu, B), "utraj"), _ptr(status, I32, (B,), "status"),
+            _ptr(qp_iter, I32, (B,), "qp_iter"), _ptr(qp_res, F32, (3, B), "qp_res"), _stream(stream)),
+            "nmpc_batch_solve")
 
     def run(self, pose, vel, traj, steer=None, traj_len=None, reset=None, cmd=None, u0=None, status=None,
             qp_iter=None, qp_res=None, stream=None):
         B = pose.shape[1]
-        assert pose.shape == (3, B) and vel.shape == (3, B) and traj.shape == (self.N + 1, 3, B)
-        check(lib().nmpc_batch_run(self._h, B, _ptr(pose), _ptr(vel), _ptr(steer), _ptr(traj), _ptr(traj_len),
-                                   _ptr(reset), _ptr(cmd), _ptr(u0), _ptr(status), _ptr(qp_iter),
-                                   _ptr(qp_res), _stream(stream)), "nmpc_batch_run")
+        if not 0 <= B <= self.capacity:
+            raise ValueError(f"batch {B} exceeds the capacity {self.capacity}")
+        check(lib().nmpc_batch_run(
+            self._h, B, _ptr(pose, F32, (3, B), "pose"), _ptr(vel, F32, (3, B), "vel"),
+            _ptr(steer, F32, (B,), "steer"), _ptr(traj, F32, (self.N + 1, 3, B), "traj"),
+            _ptr(traj_len, I32, (B,), "traj_len"), _ptr(reset, U8, (B,), "reset"), _ptr(cmd, F32, (3, B), "cmd"),
+            _ptr(u0, F32, (self.nu, B), "u0"), _ptr(status, I32, (B,), "status"),
+            _ptr(qp_iter, I32, (B,), "qp_iter"), _ptr(qp_res, F32, (3, B), "qp_res"), _stream(stream)),
+            "nmpc_batch_run")
 
     def fleet_sim_step(self, path, s, pose, vel, steer, u0, status, traj, traj_len, advance=True, stream=None):
         B = pose.shape[1]
-        check(lib().nmpc_fleet_sim_step(self._h, B, _ptr(path), _ptr(s), _ptr(pose), _ptr(vel), _ptr(steer),
-                                        _ptr(u0), _ptr(status), _ptr(traj), _ptr(traj_len), int(bool(advance)),
-                                        _stream(stream)), "nmpc_fleet_sim_step")
+        if not 0 <= B <= self.capacity:
+            raise ValueError(f"batch {B} exceeds the capacity {self.capacity}")
+        check(lib().nmpc_fleet_sim_step(
+            self._h, B, _ptr(path, F32, (6, B), "path"), _ptr(s, F32, (B,), "s"), _ptr(pose, F32, (3, B), "pose"),
+            _ptr(vel, F32, (3, B), "vel"), _ptr(steer, F32, (B,), "steer"), _ptr(u0, F32, (self.nu, B), "u0"),
+            _ptr(status, I32, (B,), "status"), _ptr(traj, F32, (self.N + 1, 3, B), "traj"),
+            _ptr(traj_len, I32, (B,), "traj_len"), int(bool(advance)), _stream(stream)), "nmpc_fleet_sim_step")
 
 
 class _DeviceView:

@@ -14,7 +14,7 @@ from dataclasses import dataclass
 
 import numpy as np
 
-from ._lib import MODEL_NAMES, lib, model_dims, solver_lib
+from ._lib import MODEL_IDS, MODEL_NAMES, CodegenDesc, lib, model_dims, solver_lib
 
 
 @dataclass
@@ -72,7 +72,10 @@ class NMPCNavControl:
         if N is None:
             status = getattr(S, f"{self._name}_acados_create")(self._capsule)
         else:
-            status = getattr(S, f"{self._name}_acados_create_with_discretization")(self._capsule, int(N), None)
+            # a horizon other than the baked one needs its time steps (acados create_with_discretization):
+            # uniform steps of the codegen length
+            steps = (ctypes.c_double * int(N))(*([self._codegen_dt()] * int(N)))
+            status = getattr(S, f"{self._name}_acados_create_with_discretization")(self._capsule, int(N), steps)
         self.processCreateStatus(status)
         self.N = self._dims_N()
         c = self._capsule.contents
@@ -85,6 +88,12 @@ class NMPCNavControl:
         self.status = 0
         self.kkt_res = 0.0
         self.cpu_time = 0.0
+
+    def _codegen_dt(self):
+        """Step of the shipped codegen configuration (tf / N = 1 / freq, scripts/diff/common.py:6-9)."""
+        d = CodegenDesc()
+        self._L.nmpc_codegen_default(MODEL_IDS[self.model], ctypes.byref(d))
+        return d.tf / d.N
 
     def _dims_N(self):
         class Dims(ctypes.Structure):

@@ -63,16 +63,19 @@ struct Engine {
     int cap = 0;
     float *x0 = nullptr, *yref = nullptr, *We = nullptr, *xtraj = nullptr, *utraj = nullptr;
     int *status = nullptr, *qp_iter = nullptr;
+    float* qp_res = nullptr;  // [3][cap]: stationarity, bound residual, mu at IPM exit
     // pinned host staging of the same shapes ([row][n] dense): no per-call allocation, DMA-able copies
     float *h_x0 = nullptr, *h_yref = nullptr, *h_We = nullptr, *h_xb = nullptr, *h_ub = nullptr;
     int *h_status = nullptr, *h_qp_iter = nullptr;
+    float* h_qp_res = nullptr;
     ~Engine() { release(); }
     void release()
     {
         nmpc_batch_destroy(batch);
         batch = nullptr;
         (void)hipFree(x0); (void)hipFree(yref); (void)hipFree(We); (void)hipFree(xtraj); (void)hipFree(utraj);
-        (void)hipFree(status); (void)hipFree(qp_iter);
+        (void)hipFree(status); (void)hipFree(qp_iter); (void)hipFree(qp_res); (void)hipHostFree(h_qp_res);
+        qp_res = h_qp_res = nullptr;
         (void)hipHostFree(h_x0); (void)hipHostFree(h_yref); (void)hipHostFree(h_We); (void)hipHostFree(h_xb);
         (void)hipHostFree(h_ub); (void)hipHostFree(h_status); (void)hipHostFree(h_qp_iter);
         x0 = yref = We = xtraj = utraj = nullptr;
@@ -85,6 +88,15 @@ struct Engine {
 std::map<std::pair<int, int>, std::unique_ptr<Engine>> g_engines;
 
 void log_err(const char* what, const std::string& msg) { std::fprintf(stderr, "[nmpc_amd] %s: %s\n", what, msg.c_str()); }
+
+// A stage index past the capsule's horizon is a caller error (e.g. a wrapper compiled against another {NAME}_N):
+// log it, the caller gets -1 / 1 (acados would write out of bounds)
+bool stage_ok(const nmpc_capsule_impl* c, int stage, const char* what, const char* field)
+{
+    if (stage >= 0 && stage <= c->N) return true;
+    log_err(what, std::string(field) + ": stage " + std::to_string(stage) + " outside 0.." + std::to_string(c->N));
+    return false;
+}
 
 void stage_W_diag(nmpc_capsule_impl* c, int k, const double* d, int n)
 {
@@ -301,6 +313,8 @@ int ensure_engine(Engine& e, const nmpc_model_params& prm, int n, std::string& w
         (r = hipMalloc(&e.utraj, sizeof(float) * N * nu * cap)) != hipSuccess ||
         (r = hipMalloc(&e.status, sizeof(int) * cap)) != hipSuccess ||
         (r = hipMalloc(&e.qp_iter, sizeof(int) * cap)) != hipSuccess ||
+        (r = hipMalloc(&e.qp_res, sizeof(float) * 3 * cap)) != hipSuccess ||
+        (r = hipHostMalloc(&e.h_qp_res, sizeof(float) * 3 * cap)) != hipSuccess ||
         (r = hipHostMalloc(&e.h_x0, sizeof(float) * nx * cap)) != hipSuccess ||
         (r = hipHostMalloc(&e.h_yref, sizeof(float) * (N + 1) * ny * cap)) != hipSuccess ||
         (r = hipHostMalloc(&e.h_We, sizeof(float) * nx * cap)) != hipSuccess ||
@@ -371,13 +385,14 @@ void solve_group(std::vector<nmpc_capsule_impl*>& cs, std::vector<Packed>& ps, c
         return fail_all(hipGetErrorString(r));
     const auto t1 = std::chrono::steady_clock::now();
     if (nmpc_batch_solve(e.batch, n, e.x0, e.yref, ny, e.We, nullptr, nullptr, nullptr, e.xtraj, e.utraj, e.status,
-                         e.qp_iter, nullptr, nullptr) != NMPC_OK)
+                         e.qp_iter, e.qp_res, nullptr) != NMPC_OK)
         return fail_all(nmpc_last_error());
     int *hst = e.h_status, *hit = e.h_qp_iter;
     if ((r = hipMemcpy(hxb, e.xtraj, sizeof(float) * n_xb, hipMemcpyDeviceToHost)) != hipSuccess ||
         (r = hipMemcpy(hub, e.utraj, sizeof(float) * n_ub, hipMemcpyDeviceToHost)) != hipSuccess ||
         (r = hipMemcpy(hst, e.status, sizeof(int) * n, hipMemcpyDeviceToHost)) != hipSuccess ||
-        (r = hipMemcpy(hit, e.qp_iter, sizeof(int) * n, hipMemcpyDeviceToHost)) != hipSuccess)
+        (r = hipMemcpy(hit, e.qp_iter, sizeof(int) * n, hipMemcpyDeviceToHost)) != hipSuccess ||
+        (r = hipMemcpy(e.h_qp_res, e.qp_res, sizeof(float) * n, hipMemcpyDeviceToHost)) != hipSuccess)
         return fail_all(hipGetErrorString(r));
     const auto t2 = std::chrono::steady_clock::now();
     const double tt = std::chrono::duration<double>(t2 - t0).count();
@@ -392,6 +407,7 @@ void solve_group(std::vector<nmpc_capsule_impl*>& cs, std::vector<Packed>& ps, c
         nmpc_capsule_impl* c = cs[idx[q]];
         c->status = hst[q];
         c->qp_iter = hit[q];
+        c->out.inf_norm_res = e.h_qp_res[q];  // row 0 of qp_res: max |QP stationarity residual| at IPM exit
         c->sqp_iter = 1;
         c->out.sqp_iter = 1;
         c->time_tot = tt;
@@ -459,7 +475,7 @@ int ocp_nlp_constraints_model_set(ocp_nlp_config* config, ocp_nlp_dims* dims, oc
     (void)config; (void)dims; (void)out;
     nmpc_capsule_impl* c = in ? impl_of(in->impl) : nullptr;
     if (!c || !c->created || !field || !value) return -1;
-    if (stage < 0 || stage > c->N) return -1;
+    if (!stage_ok(c, stage, "ocp_nlp_constraints_model_set", field)) return -1;
     const double* v = static_cast<const double*>(value);
     const int nx = c->nx;
     if (!std::strcmp(field, "lbx") || !std::strcmp(field, "ubx")) {
@@ -470,7 +486,11 @@ int ocp_nlp_constraints_model_set(ocp_nlp_config* config, ocp_nlp_dims* dims, oc
         return 0;
     }
     if (!std::strcmp(field, "lbu") || !std::strcmp(field, "ubu")) {
-        if (stage >= c->N) return -1;
+        if (stage >= c->N) {
+            log_err("ocp_nlp_constraints_model_set", std::string(field) + " at the terminal stage " +
+                                                         std::to_string(stage) + " (inputs live on stages 0..N-1)");
+            return -1;
+        }
         std::vector<double>& dst = (field[0] == 'l') ? c->lbu : c->ubu;
         for (int i = 0; i < c->nbu; i++) dst[(size_t)stage * c->nbu + i] = v[i];
         c->uniform_dirty = true;
@@ -486,7 +506,7 @@ int ocp_nlp_cost_model_set(ocp_nlp_config* config, ocp_nlp_dims* dims, ocp_nlp_i
     (void)config; (void)dims;
     nmpc_capsule_impl* c = in ? impl_of(in->impl) : nullptr;
     if (!c || !c->created || !field || !value) return -1;
-    if (stage < 0 || stage > c->N) return -1;
+    if (!stage_ok(c, stage, "ocp_nlp_cost_model_set", field)) return -1;
     const double* v = static_cast<const double*>(value);
     const int n = (stage == c->N) ? c->nx : c->ny;
     if (!std::strcmp(field, "W")) {
@@ -509,7 +529,7 @@ void ocp_nlp_out_get(ocp_nlp_config* config, ocp_nlp_dims* dims, ocp_nlp_out* ou
 {
     (void)config; (void)dims;
     nmpc_capsule_impl* c = out ? impl_of(out->impl) : nullptr;
-    if (!c || !c->created || !field || !value || stage < 0 || stage > c->N) return;
+    if (!c || !c->created || !field || !value || !stage_ok(c, stage, "ocp_nlp_out_get", field)) return;
     double* v = static_cast<double*>(value);
     if (!std::strcmp(field, "x")) {
         for (int i = 0; i < c->nx; i++) v[i] = c->xbar[(size_t)stage * c->nx + i];
@@ -525,7 +545,7 @@ void ocp_nlp_out_set(ocp_nlp_config* config, ocp_nlp_dims* dims, ocp_nlp_out* ou
 {
     (void)config; (void)dims;
     nmpc_capsule_impl* c = out ? impl_of(out->impl) : nullptr;
-    if (!c || !c->created || !field || !value || stage < 0 || stage > c->N) return;
+    if (!c || !c->created || !field || !value || !stage_ok(c, stage, "ocp_nlp_out_set", field)) return;
     const double* v = static_cast<const double*>(value);
     if (!std::strcmp(field, "x")) {
         for (int i = 0; i < c->nx; i++) c->xbar[(size_t)stage * c->nx + i] = v[i];
@@ -653,9 +673,13 @@ int nmpc_capsule_create(nmpc_solver_capsule* capsule, const nmpc_codegen_desc* d
             d.N = n_time_steps;
             d.tf = new_time_steps[0] * n_time_steps;
         }
-    } else if (n_time_steps >= 1 && n_time_steps != d.N) {
-        d.tf = d.tf / d.N * n_time_steps;  // acados keeps the step size tf / N of the codegen
-        d.N = n_time_steps;
+    } else if (n_time_steps != d.N) {
+        // as the acados template's {name}_acados_create_with_discretization: a horizon other than the baked one
+        // needs its time steps (the wrappers size yref[N+1] and loop over stages by the baked {NAME}_N)
+        log_err("create", "new_time_steps is NULL but the number of shooting intervals (= " +
+                              std::to_string(n_time_steps) + ") differs from the number of shooting intervals (= " +
+                              std::to_string(d.N) + ") during code generation: provide the time steps");
+        return 1;
     }
     return impl_create(capsule->impl, n_time_steps, d);
 }
@@ -678,7 +702,7 @@ int nmpc_capsule_update_params(nmpc_solver_capsule* capsule, int stage, const do
         log_err("update_params", "np does not match the model");
         return 1;
     }
-    if (stage < 0 || stage > c->N) return 1;
+    if (!stage_ok(c, stage, "update_params", "p")) return 1;
     for (int i = 0; i < np; i++) c->p[(size_t)stage * np + i] = value[i];
     c->uniform_dirty = true;
     return 0;

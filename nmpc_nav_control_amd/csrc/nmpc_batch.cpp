@@ -23,7 +23,6 @@ struct nmpc_batch {
     float* ubar = nullptr;
     float* carried = nullptr;
     float* scratch = nullptr;
-    int kernel = 0;  // 0: team-per-instance (default), 1: lane-per-instance
     int sched = NMPC_SCHED_AUTO;
     int n_simd = 1024;           // SIMDs of the device (4 per CU)
     int* iter_key = nullptr;     // [capacity] last executed IPM iterations per robot (written by the team kernel)
@@ -81,33 +80,25 @@ KParams to_kparams(const nmpc_model_params& p, int nx, int nu, int nbx, int nbu)
     return k;
 }
 
-template <class M>
-size_t scratch_floats_m(int N, int stride)
-{
-    const size_t a = lane_scratch_floats<M>(N, stride), b = team_scratch_floats<M>(N, stride);
-    return a > b ? a : b;
-}
-
 size_t scratch_floats(int model, int N, int stride)
 {
     switch (model) {
-    case NMPC_MODEL_DIFF2AMR: return scratch_floats_m<Diff2>(N, stride);
-    case NMPC_MODEL_OMNI4AMR: return scratch_floats_m<Omni4>(N, stride);
-    default: return scratch_floats_m<Tric3>(N, stride);
+    case NMPC_MODEL_DIFF2AMR: return team_scratch_floats<Diff2>(N, stride);
+    case NMPC_MODEL_OMNI4AMR: return team_scratch_floats<Omni4>(N, stride);
+    default: return team_scratch_floats<Tric3>(N, stride);
     }
 }
 
 template <class M>
 hipError_t launch_m(nmpc_batch* b, const KArgs& a, int mode, hipStream_t s)
 {
-    return b->kernel == NMPC_KERNEL_LANE ? launch_sqp_rti_lane<M>(b->kp, a, mode, s)
-                                         : launch_sqp_rti_team<M>(b->kp, a, mode, s);
+    (void)b;
+    return launch_sqp_rti_team<M>(b->kp, a, mode, s);
 }
 
 // Team placement before a team-kernel launch (schedule.hip); fills a.order / a.iter_key
 hipError_t schedule(nmpc_batch* b, KArgs& a, hipStream_t s)
 {
-    if (b->kernel != NMPC_KERNEL_TEAM) return hipSuccess;
     a.iter_key = b->iter_key;
     a.dense = ((a.B + 3) / 4 > b->n_simd) ? 1 : 0;  // 4 teams per wave
     int layout = b->sched;
@@ -138,7 +129,10 @@ __global__ void k_init_iterate(float* xbar, float* ubar, float* carried, int B, 
             xbar[((size_t)k * nx + j) * stride + i] = (mode == 0 && j == 2) ? 3.14159265358979323846f : 0.0f;
     for (int k = 0; k < N; k++)
         for (int j = 0; j < nu; j++) ubar[((size_t)k * nu + j) * stride + i] = 0.0f;
-    for (int j = 0; j < nbx; j++) carried[(size_t)j * stride + i] = 0.0f;
+    // create semantics start the wrapper's x0 vel-refs at zero (the member struct is value-initialised); a reset
+    // (reset_mpc -> {name}_acados_reset) leaves them, as the reference does and as the solve's reset mask does
+    if (mode == 0)
+        for (int j = 0; j < nbx; j++) carried[(size_t)j * stride + i] = 0.0f;
 }
 
 int check_params(const nmpc_model_params* prm)
@@ -165,7 +159,7 @@ int check_params(const nmpc_model_params* prm)
 extern "C" {
 
 const char* nmpc_last_error(void) { return g_err.c_str(); }
-const char* nmpc_version(void) { return "nmpc_amd 0.2 (team-per-instance DPP SQP-RTI, gfx950)"; }
+const char* nmpc_version(void) { return "nmpc_amd 0.3 (team-per-instance DPP SQP-RTI, gfx950)"; }
 
 int nmpc_model_dims(int model, int* nx, int* nu, int* ny, int* nbx, int* nbu, int* np)
 {
@@ -255,7 +249,6 @@ int nmpc_batch_create(const nmpc_model_params* prm, int capacity, nmpc_batch** o
     dims_of(prm->model, &b->nx, &b->nu, &b->nbx, &b->nbu, &np);
     b->ny = b->nx + b->nu;
     b->kp = to_kparams(*prm, b->nx, b->nu, b->nbx, b->nbu);
-    if (const char* kv = std::getenv("NMPC_AMD_KERNEL")) b->kernel = (std::strcmp(kv, "lane") == 0) ? 1 : 0;
     if (const char* sv = std::getenv("NMPC_AMD_SCHED")) {  // off | auto | sorted | interleaved
         const char* names[4] = {"off", "auto", "sorted", "interleaved"};
         for (int i = 0; i < 4; i++)
@@ -399,8 +392,7 @@ int nmpc_batch_run(nmpc_batch* b, int B, const float* pose, const float* vel, co
 int nmpc_batch_set_kernel(nmpc_batch* b, int kernel)
 {
     if (!b) return set_err(NMPC_ERR_ARG, "batch is NULL");
-    if (kernel != NMPC_KERNEL_TEAM && kernel != NMPC_KERNEL_LANE) return set_err(NMPC_ERR_ARG, "unknown kernel");
-    b->kernel = kernel;
+    if (kernel != NMPC_KERNEL_TEAM) return set_err(NMPC_ERR_UNSUPPORTED, "unknown kernel (only NMPC_KERNEL_TEAM)");
     return NMPC_OK;
 }
 

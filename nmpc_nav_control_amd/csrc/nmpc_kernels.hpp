@@ -49,38 +49,6 @@ struct KArgs {
     int dense;      // the launch has more waves than the device has SIMDs (selects the team kernel variant)
 };
 
-template <int NU>
-__device__ inline void chol_solve_neg(const float (&L)[NU][NU], const float (&r)[NU], float (&y)[NU])
-{
-    // y = -(L L')^{-1} r
-    float w[NU];
-#pragma unroll
-    for (int i = 0; i < NU; i++) {
-        float s = r[i];
-#pragma unroll
-        for (int q = 0; q < i; q++) s -= L[i][q] * w[q];
-        w[i] = s / L[i][i];
-    }
-#pragma unroll
-    for (int i = NU - 1; i >= 0; i--) {
-        float s = w[i];
-#pragma unroll
-        for (int q = i + 1; q < NU; q++) s -= L[q][i] * y[q];
-        y[i] = s / L[i][i];
-    }
-#pragma unroll
-    for (int i = 0; i < NU; i++) y[i] = -y[i];
-}
-
-__device__ inline float step_bound(float amax, float v, float dv)
-{
-    return (dv < 0.0f) ? fminf(amax, -v / dv) : amax;
-}
-
-template <class M>
-size_t lane_scratch_floats(int N, int stride);
-template <class M>
-hipError_t launch_sqp_rti_lane(const KParams& P, const KArgs& a, int mode, hipStream_t stream);
 template <class M>
 size_t team_scratch_floats(int N, int stride);
 template <class M>

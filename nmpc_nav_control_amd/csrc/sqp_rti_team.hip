@@ -6,10 +6,12 @@
 //   * four robots per wavefront; inside a team lane v owns QP variable v of every stage (v < NU: input,
 //     NU <= v < NU+NX: state); cross-lane operands are DPP row_newbcast broadcasts, fused into the
 //     multiply-accumulates (v_fmac_f32_dpp / v_fmac_f64_dpp);
-//   * the stage factor is a square-root Riccati step, M = D + (L'[B A])'(L'[B A]) = chol, formed and factored
-//     in fp64 (MI355X runs fp64 FMAs at half the fp32 rate): near the solution the barrier weights of active
-//     bounds reach 1e12 and fp32 Schur complements cancel catastrophically. The factor is stored in fp32 and
-//     every solve with it runs in fp32 (u0 error <1e-5 against the fp64 oracle, DESIGN.md "Precision");
+//   * the stage factor is a classic Riccati step in fp64: lane NU+i carries row i of the cost-to-go Hessian
+//     P_{k+1}; PG = P_{k+1}[B A] and the rows of M = D + [B A]' PG are fused fp64 DPP blocks
+//     (team_asm_gen.hpp), then a right-looking Cholesky of the NU x NU input block leaves the Schur complement
+//     P_k in the state block (near the solution the barrier weights of active bounds reach 1e12, and fp32
+//     Schur complements cancel catastrophically). The input columns of the factor are stored in fp32 and every
+//     solve with them runs in fp32 (u0 error ~1e-4 against the fp64 oracle, DESIGN.md "Algorithm and precision");
 //   * rows of [B A] that do not depend on the state (model trait NGV) live in registers for the whole launch;
 //     only the NGV varying rows are stored per stage;
 //   * each lane's per-stage record (slacks, multipliers, iterate, directions, factor row, Jacobian column) is
@@ -92,24 +94,6 @@ constexpr float kCompMaxRatio = 30.0f;
 #ifndef LIGHT_D
 #define LIGHT_D 4  // record buffers of the light (solve-only) sweeps
 #endif
-#ifndef P1_D
-#define P1_D 2  // record buffers of the factorisation sweep (2: ping-pong; 3 measured no faster)
-#endif
-#ifndef NMPC_RING_KB
-#define NMPC_RING_KB 20  // 1-KB quad slots of each wave's LDS record ring
-#endif
-#if !defined(NMPC_LDS_RING) && !defined(NMPC_REG_SWEEPS)
-#define NMPC_REG_SWEEPS  // LDS record rings are opt-in (-DNMPC_LDS_RING) until measured on the GPU
-#endif
-#ifdef NMPC_REG_SWEEPS
-#define LIGHT_SWEEP sweepd
-#define LIGHT_DEPTH LIGHT_D
-#define LIGHT_Q(F) (F)
-#else
-#define LIGHT_SWEEP sweepl
-#define LIGHT_DEPTH LDR
-#define LIGHT_Q(F) (((F) + 3) / 4)
-#endif
 constexpr float kFar = 1e30f;  // sentinel bound / slack of unbounded slots (z + kFar - kFar == 0 in fp32)
 #ifdef NMPC_STAMPS
 constexpr int kStampItsC = kStampIts;
@@ -118,18 +102,6 @@ constexpr int kStampItsC = 0;
 #endif
 
 // generated whole-block fused-DPP kernels (team_asm_gen.hpp), dispatched on the model shape
-template <int NX, int NU>
-__device__ __forceinline__ void lba_block(double (&acc)[NX], const double (&lrow)[NX + NU], const double (&gd)[NX])
-{
-    if constexpr (NX == 7 && NU == 2) lba_block_7_2(acc, lrow, gd);
-    else lba_block_11_4(acc, lrow, gd);
-}
-template <int NX, int NU>
-__device__ __forceinline__ void mrow_block(double (&acc)[NX + NU], double (&md)[NX + NU], const double (&lba)[NX])
-{
-    if constexpr (NX == 7 && NU == 2) mrow_block_7_2(acc, md, lba);
-    else mrow_block_11_4(acc, md, lba);
-}
 template <int NX, int NU>
 __device__ __forceinline__ void pg_block(double (&acc)[NX], const double (&prow)[NX + NU], const double (&gd)[NX])
 {
@@ -228,17 +200,11 @@ __device__ __forceinline__ void rk4_column(const float* x, const float* u, const
 //     dwordx4 access of a team touches 2 cache lines instead of one per two slots.
 // Measured per model in same-box A/B runs (ms per tick): omni4 (15 slots, 80-B records) 2.17 slot-major ->
 // 1.74 quad-major; diff 1.55 -> 1.57 and tric 4.48 -> 4.62 (9 slots) favour slot-major. RQM picks quad-major for
-// teams of more than 12 slots (NMPC_SLOT_MAJOR / NMPC_QUAD_MAJOR force one layout for A/B runs).
+// teams of more than 12 slots.
 template <int NV>
 constexpr bool rec_quad_major()
 {
-#if defined(NMPC_SLOT_MAJOR)
-    return false;
-#elif defined(NMPC_QUAD_MAJOR)
-    return true;
-#else
     return NV > 12;
-#endif
 }
 template <int RS, bool QM>
 constexpr int rec_qs() { return QM ? 64 : 4; }  // floats between a lane's consecutive quads
@@ -282,26 +248,6 @@ __device__ __forceinline__ void rec_load(const float* p, float (&v)[RS])
 {
     rec_load_prefix<RS, RS, QM>(p, v);
 }
-
-// ---- LDS record rings ----------------------------------------------------------------
-// global_load_lds_dwordx4 moves quad q of every lane's record of a stage straight into a per-wave LDS slot
-// (wave-uniform base + lane * 16 B, no VGPR destination), the stage body reads its quads with ds_read_b128.
-// The DMAs are inline asm, outside the compiler's s_waitcnt bookkeeping: ring_wait<N>() retires a stage by count.
-__device__ __forceinline__ void glds16(const float* gsrc, uint32_t lds_byte_addr)
-{
-    unsigned keep;
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-                 : "=&s"(keep)
-                 : "v"(gsrc), "s"(lds_byte_addr)
-                 : "memory");
-}
-template <int N>
-__device__ __forceinline__ void ring_wait()
-{
-    static_assert(N >= 0 && N < 64, "vmcnt is 6 bits");
-    asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
-}
-__device__ __forceinline__ void lds_retire() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
 // floats [F0, NF) of a record, F0 a multiple of 4 (the fields P1 rewrites)
 template <int NF, int RS, bool QM, int F0 = 0>
@@ -383,18 +329,6 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
     // extra cache lines; they never store
     float* const tbase = a.scratch + (size_t)team * (N + 1) * 16 * RS + (lv ? r : 0) * rec_lane<RS, QM>();
     constexpr int KS = 16 * RS;
-#ifndef NMPC_REG_SWEEPS
-    // per-wave LDS record ring of RING 1-KB quad slots (20: 80 KB per 4-wave block, so two blocks of any model
-    // share a CU), used in turn by the P1 and the light sweeps
-    constexpr int LQ = (R::NL + 3) / 4;  // quads the light sweeps read
-    constexpr int RING = NMPC_RING_KB;
-    constexpr int LDR = RING / LQ;       // light-sweep ring stages (diff, tric: 5; omni4: 4)
-    constexpr int P1R = RING / R::NQ;    // P1 ring stages (diff: 5; omni4, tric: 4)
-    static_assert(LDR >= 2 && P1R >= 2, "ring too small");
-    __shared__ float4 lring[4][RING][64];
-    const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
-    const uint32_t ring0 = __builtin_amdgcn_readfirstlane((uint32_t)reinterpret_cast<uintptr_t>(&lring[wv][0][0]));
-#endif
 
 #define XB(k, j) a.xbar[((size_t)(k) * NX + (j)) * S + inst]
 #define UBAR(k, j) a.ubar[((size_t)(k) * NU + (j)) * S + inst]
@@ -627,11 +561,7 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
     // stage k + (i + D)*dir (clamped at k1), so D - 1 records are in flight during every body
     auto sweepd = [&](auto dc, auto fc, int k0, int k1, int dir, bool ld, auto&& body) {
         constexpr int D = decltype(dc)::value;
-#ifdef NMPC_FULL_RECORD_LOADS
-        constexpr int F = RS + 0 * decltype(fc)::value;  // A/B: whole records
-#else
         constexpr int F = decltype(fc)::value;  // floats of the record prefix this sweep reads
-#endif
         const ptrdiff_t step = ld ? (ptrdiff_t)KS * dir : 0;
         float buf[D][RS];
         const float* p = tbase + (size_t)k0 * KS;
@@ -660,58 +590,15 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
             if (stop) break;
         }
     };
-#ifndef NMPC_REG_SWEEPS
-    // LDS-ring sweep over k = k0, k0 + dir, ..., k1: D ring stages of NQL quads, D - 1 stages in flight while a
-    // body runs; at the top of body k stage k + (D-1)*dir goes into the slot the previous body read, then the wait
-    // retires stage k. Lanes that do not sweep re-read one fixed record; past k1 the source stays on k1.
-    auto sweepl = [&](auto dc, auto qc, int k0, int k1, int dir, bool ld, auto&& body) {
-        constexpr int D = decltype(dc)::value, NQL = decltype(qc)::value;
-        static_assert(D * NQL <= RING, "ring too small");
-        const ptrdiff_t step = ld ? (ptrdiff_t)KS * dir : 0;
-        const float* p = tbase + (size_t)k0 * KS;
-        int kl = k0;
-        auto issue = [&](int slot) {
-            const uint32_t base = ring0 + (uint32_t)(slot * NQL) * 1024u;
-            sfor<0, NQL>([&](auto qq) {
-                constexpr int q = decltype(qq)::value;
-                glds16(p + rec_off<RS, QM>(4 * q), base + (uint32_t)q * 1024u);
-            });
-            p = (kl == k1) ? p : p + step;
-            kl = (kl == k1) ? kl : kl + dir;
-        };
-        lds_retire();
-        sfor<0, D - 1>([&](auto ic) { issue(decltype(ic)::value); });
-        int slot = 0;
-        for (int k = k0;; k += dir) {
-            lds_retire();
-            issue(slot == 0 ? D - 1 : slot - 1);
-            ring_wait<(D - 1) * NQL>();
-            float rc[RS];
-            sfor<0, NQL>([&](auto qq) {
-                constexpr int q = decltype(qq)::value;
-                const float4 t = lring[wv][slot * NQL + q][ln];
-                rc[4 * q + 0] = t.x;
-                rc[4 * q + 1] = t.y;
-                rc[4 * q + 2] = t.z;
-                rc[4 * q + 3] = t.w;
-            });
-#pragma unroll
-            for (int f = 4 * NQL; f < RS; f++) rc[f] = 0.0f;
-            body(k, rc);
-            if (k == k1) break;
-            slot = (slot + 1 == D) ? 0 : slot + 1;
-        }
-    };
-#endif
     // ---- interior-point iterations ----------------------------------------------------------------------
     int status = 0, it_done = 0;
     bool done = false;
     float exit_res[3] = {0.0f, 0.0f, 0.0f};
     float alpha = 0.0f, sigma_mu = 0.0f, eta = 0.0f, mu_prev = 3.0e38f;
     for (int it = 0;; it++) {
-        // P1 (backward): apply the previous step, residuals, adjoint, fp64 square-root Riccati factorisation,
+        // P1 (backward): apply the previous step, residuals, adjoint, fp64 classic Riccati factorisation,
         // predictor rhs
-        double Lrow[NV];  // row r of the factor of stage k+1 (state lanes carry the rows of L_{k+1})
+        double Lrow[NV];  // lane NU+i: row i of P_{k+1} (the state block of the previous stage's M after its pivots)
 #pragma unroll
         for (int j = 0; j < NV; j++) Lrow[j] = 0.0;
         float pv = 0.0f, piv = 0.0f;
@@ -721,15 +608,7 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
         const float a_upd = (it > 0 && !done) ? alpha : 0.0f;
         // P1_D record buffers: the heavy sweep's next records are in flight for P1_D - 1 stage bodies (at four
         // waves per CU a record load from the Infinity Cache takes about one stage body)
-#if defined(NMPC_REG_SWEEPS) && P1_D > 2
-        sweepd(std::integral_constant<int, P1_D>{}, std::integral_constant<int, RS>{}, N, 0, -1, act,
-               [&](int k, float (&rc)[RS]) {
-#elif defined(NMPC_REG_SWEEPS)
         sweep(N, 0, -1, act, [&](int k, float (&rc)[RS]) {
-#else
-        sweepl(std::integral_constant<int, P1R>{}, std::integral_constant<int, R::NQ>{}, N, 0, -1, act,
-               [&](int k, float (&rc)[RS]) {
-#endif
             STAMPF(0);
             const bool vu = is_u && k < N;
             const bool vx = is_x && k >= 1;
@@ -782,12 +661,8 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
             const float pi_new = vx ? base : 0.0f;
             if (ghat != ghat || sig != sig) nanf_ = 1.0f;
             if (k == N) {
-                // terminal: P_N = diag(W_e + Sigma) on the state lanes (square-root form: its Cholesky factor)
-#ifdef NMPC_SQRT_RICCATI
-                const double d = is_x ? sqrt((double)fmaxf(we_lane + sig, 0.0f)) : 0.0;
-#else
+                // terminal: P_N = diag(W_e + Sigma) on the state lanes
                 const double d = is_x ? (double)fmaxf(we_lane + sig, 0.0f) : 0.0;
-#endif
 #pragma unroll
                 for (int j = 0; j < NV; j++) Lrow[j] = (is_x && j == r) ? d : 0.0;
                 pv = is_x ? ghat : 0.0f;
@@ -795,42 +670,6 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
                 double Gd[NX];
 #pragma unroll
                 for (int l = 0; l < NX; l++) Gd[l] = (l < NGV) ? (double)Gc[l] : gcol64[l];
-#ifdef NMPC_SQRT_RICCATI
-                // LBA column v = L_{k+1}' G[:, v]; L[l][i] sits in lane NU+l at Lrow[NU+i]
-                double lba[NX];
-#pragma unroll
-                for (int i = 0; i < NX; i++) lba[i] = 0.0;
-                STAMPF(2);
-                lba_block<NX, NU>(lba, Lrow, Gd);
-                STAMPF(3);
-                // row r of M = D + LBA' LBA, then its right-looking row-distributed Cholesky in fp64: column j's
-                // pivot comes from lane j, every later column is updated by one fused block
-                const double dg = valid ? (double)h_stage + (double)sig : 1.0;
-                double Lr[NV], md[NV];
-#pragma unroll
-                for (int j = 0; j < NV; j++) Lr[j] = (r == j) ? dg : 0.0;
-                mrow_block<NX, NU>(Lr, md, lba);  // md[j] = M[j][j] (lane j's diagonal), md[0] = first pivot
-                STAMPF(4);
-                double pivot = md[0];
-                sfor<0, NV>([&](auto jc) {
-                    constexpr int j = decltype(jc)::value;
-                    const double s = Lr[j];  // M[r][j] minus the updates of columns < j
-                    double rd;
-                    if constexpr (j < NU) {
-                        if (!(pivot > 0.0)) fail = true;
-                        rd = drsq(fmax(pivot, 1e-300));
-                    } else {
-                        // PSD state block: pivot > 1e-10 (1 + |M_jj|)
-                        rd = (fma(-1e-10, fabs(md[j]), pivot) > 1e-10) ? drsq(pivot) : 0.0;
-                    }
-                    // lane j: s == pivot. Rows r < j keep unmasked upper-triangle entries in the state columns
-                    // (~0, read only by row r itself); the input columns are stored (LM) and must be exact
-                    const double lj = (j >= NU || r >= j) ? s * rd : 0.0;
-                    Lr[j] = lj;
-                    // right-looking update M[r][j'] -= L[r][j] L[j'][j] (j' > j) and the next pivot
-                    if constexpr (j + 1 < NV) chol_update<NX, NU, j>(Lr, lj, pivot);
-                });
-#else
                 // classic Riccati in fp64: PG column v = P_{k+1} G[:, v] (P[i][l] sits in lane NU+i at Lrow[NU+l]),
                 // row r of M = D + G' P G, then the right-looking row-distributed Cholesky of the input block only:
                 // after the NU input pivots the state block of M holds the Schur complement
@@ -857,7 +696,6 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
                     Lr[j] = lj;
                     chol_update<NX, NU, j>(Lr, lj, pivot);
                 });
-#endif
                 STAMPF(5);
                 float Lm[NU];
 #pragma unroll
@@ -881,9 +719,6 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
             }
             piv = pi_new;
             STAMPF(6);
-#ifdef NMPC_FULL_RECORD_STORES
-            if (act) rec_store<RS, QM>(tbase + (size_t)k * KS, rc);
-#else
             if constexpr (MS) {
                 // slack / multiplier quad only where a bound lives (elsewhere it holds the constant sentinel)
                 static_assert(R::TL == 0 && R::LU == 3, "bound quad first");
@@ -892,7 +727,6 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
             } else {
                 if (act) rec_store_prefix<R::NP1, RS, QM>(tbase + (size_t)k * KS, rc);
             }
-#endif
             STAMPF(7);
         });
         if (it < kStampItsC) STAMP(2 + 4 * it);
@@ -957,7 +791,7 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
             if (pass > 0) {
                 // corrector rhs through the stored factorisation (backward)
                 float pvc = 0.0f;
-                LIGHT_SWEEP(std::integral_constant<int, LIGHT_DEPTH>{}, std::integral_constant<int, LIGHT_Q(R::NB)>{}, N, 0, -1, ld, [&](int k, float (&rc)[RS]) {
+                sweepd(std::integral_constant<int, LIGHT_D>{}, std::integral_constant<int, R::NB>{}, N, 0, -1, ld, [&](int k, float (&rc)[RS]) {
                     const bool vu = is_u && k < N;
                     float ghat;
                     {  // branch-free: 0 on the kFar-sentinel slots (see P0)
@@ -993,12 +827,11 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
             if (pass == 1) STAMPC1();
             // forward: du from the stored factor, dz, bounded-variable directions, next-stage dx
             float amax = 1e30f, s1 = 0.0f, s2 = 0.0f;
-            // CORR 0: affine pass, 1: corrector / safeguard pass (compile-time bodies), 2: one body, runtime pass
+            // CORR 0: affine pass, 1: corrector / safeguard pass (compile-time bodies)
             auto fwd = [&](auto cc) {
-            constexpr int CORR = decltype(cc)::value;
-            const bool corr = (CORR == 2) ? (pass > 0) : (CORR == 1);
+            constexpr bool corr = decltype(cc)::value == 1;
             float dxs = 0.0f;
-            LIGHT_SWEEP(std::integral_constant<int, LIGHT_DEPTH>{}, std::integral_constant<int, LIGHT_Q(R::NF)>{}, 0, N, 1, ld, [&](int k, float (&rc)[RS]) {
+            sweepd(std::integral_constant<int, LIGHT_D>{}, std::integral_constant<int, R::NF>{}, 0, N, 1, ld, [&](int k, float (&rc)[RS]) {
                 const bool vu = is_u && k < N;
                 const bool vx = is_x && k >= 1;
                 const bool valid = vu || vx;
@@ -1053,13 +886,9 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
                 if (k < N) dxs = dyn(rc, valid ? dz : 0.0f);
             });
             };
-#ifndef NMPC_NO_FSPEC
             // one compiled body per pass kind: same-box A/B diff metric 1.553 -> 1.526 ms, tric 4.382 -> 4.363 ms
             if (pass == 0) fwd(std::integral_constant<int, 0>{});
             else fwd(std::integral_constant<int, 1>{});
-#else
-            fwd(std::integral_constant<int, 2>{});
-#endif
             amax = row_min16(lv ? amax : 1e30f);
             if (pass == 0) {
                 s1 = row_sum16(lv ? s1 : 0.0f);
@@ -1078,9 +907,6 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
         if (it < kStampItsC) STAMP(5 + 4 * it);
     }
 
-#ifndef NMPC_REG_SWEEPS
-    ring_wait<0>();  // no LDS-DMA outlives the sweeps
-#endif
     // ---- full SQP step + outputs ----------------------------------------------------------------------
     if (status == 0) {
         for (int k = 0; k <= N; k++) {
@@ -1128,6 +954,12 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
 #pragma unroll
                 for (int j = 0; j < 3; j++) a.cmd[(size_t)j * Bn + inst] = cmd[j];
             }
+        } else if (mode == kModeRun && a.cmd) {
+            // failed solve: the reference throws (processAcadosStatus, NMPCNavControl.cpp:14-23) and the node
+            // publishes a stop command (executeNMPC catch -> Status::Error, NMPCNavControlROS.cpp:716-719); the
+            // carried refs and the iterate stay as they were
+#pragma unroll
+            for (int j = 0; j < 3; j++) a.cmd[(size_t)j * Bn + inst] = 0.0f;
         }
     }
 #undef XB

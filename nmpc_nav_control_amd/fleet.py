@@ -1,0 +1,151 @@
+"""A rank's closed-loop robot fleet: the driver loop bench.py times and the multi-GPU tests run.
+
+One ``Fleet`` is one model's robots on this rank (solver handle + device-resident closed-loop state); a
+``FleetNode`` is every model's fleet of one rank plus the per-tick bookkeeping of the whole-fleet config
+(BASELINE config 5): concurrent per-model launches on their own HIP streams, device-side IPM statistics, and
+the optional all-gather of u0 + status (RCCL over xGMI, sharding.CommandGather).
+
+The reference runs one robot per ROS node (``NMPCNavControlROS::executeNMPC``, NMPCNavControlROS.cpp:700-719,
+one ``run()`` per control tick); a ``Fleet`` tick is that call for B robots at once: the batched
+``NMPCNavControl*::run`` followed by the harness plant / reference step (fleet_sim.hip).
+
+The solver is pluggable (``solver_factory``): ``BatchSolver`` (libnmpc_amd.so) everywhere in the product and
+the benches; the CPU multi-process tests plug an fp64 oracle-backed object with the same methods (state, run,
+fleet_sim_step, set_schedule, nu) so that the code they exercise is this module, not a test-only copy.
+"""
+import os
+
+import numpy as np
+import torch
+
+from .scenario import make_fleet
+from .sharding import CommandGather, shard_range
+
+
+class Fleet:
+    """One model's robots on this rank: solver + closed-loop state, all resident on ``dev``."""
+
+    def __init__(self, model, B, N, seed, dev, start=0, stream=None, solver_factory=None, schedule=None):
+        self.model, self.B, self.N = model, B, N
+        self.dev = torch.device(dev)
+        self.stream = stream  # None: the current stream; mixed fleets give each model its own HIP stream
+        if solver_factory is None:
+            from .batch import BatchSolver
+            solver_factory = BatchSolver
+        self.solver = solver_factory(model, N, B, device=self.dev)
+        if schedule is not None and "NMPC_AMD_SCHED" not in os.environ:
+            self.solver.set_schedule(schedule)
+        fl = make_fleet(model, B, seed=seed, start=start)
+        self.is_path = fl["is_path"]
+        t = lambda a, dt=torch.float32: torch.from_numpy(np.ascontiguousarray(a)).to(self.dev, dt)  # noqa: E731
+        self.pose, self.vel, self.path, self.s = t(fl["pose"]), t(fl["vel"]), t(fl["path"]), t(fl["s"])
+        self.steer = t(fl["steer"]) if model == "tric" else None
+        _, _, cr = self.solver.state()
+        cr.copy_from(t(fl["carried"]))
+        self.traj = torch.zeros(N + 1, 3, B, device=self.dev)
+        self.tlen = torch.zeros(B, dtype=torch.int32, device=self.dev)
+        self.cmd = torch.zeros(3, B, device=self.dev)
+        self.u0 = torch.zeros(self.solver.nu, B, device=self.dev)
+        self.status = torch.zeros(B, dtype=torch.int32, device=self.dev)
+        self.qp_iter = torch.zeros(B, dtype=torch.int32, device=self.dev)
+        self.solver.fleet_sim_step(self.path, self.s, self.pose, self.vel, self.steer, None, None, self.traj,
+                                   self.tlen, advance=False, stream=self.stream)
+
+    def solve(self, reset=None):
+        self.solver.run(self.pose, self.vel, self.traj, steer=self.steer, traj_len=self.tlen, reset=reset,
+                        cmd=self.cmd, u0=self.u0, status=self.status, qp_iter=self.qp_iter, stream=self.stream)
+
+    def advance(self):
+        self.solver.fleet_sim_step(self.path, self.s, self.pose, self.vel, self.steer, self.u0, self.status,
+                                   self.traj, self.tlen, advance=True, stream=self.stream)
+
+    def tick(self):
+        self.solve()
+        self.advance()
+
+    def snapshot(self):
+        """Host copies (float64, robot-major) of everything a solve reads: the oracle replay inputs."""
+        host = lambda a: np.ascontiguousarray(a.cpu().numpy(), np.float64)  # noqa: E731
+        xv, uv, cv = self.solver.state()
+        X, U, C = xv.to_tensor(), uv.to_tensor(), cv.to_tensor()
+        B, N = self.B, self.N
+        nx, nu = X.shape[0] // (N + 1), U.shape[0] // N
+        return dict(xbar=np.ascontiguousarray(host(X[:, :B]).T.reshape(B, N + 1, nx)),
+                    ubar=np.ascontiguousarray(host(U[:, :B]).T.reshape(B, N, nu)),
+                    carried=np.ascontiguousarray(host(C[:, :B]).T),
+                    pose=np.ascontiguousarray(host(self.pose).T), vel=np.ascontiguousarray(host(self.vel).T),
+                    steer=host(self.steer) if self.steer is not None else None,
+                    traj=np.ascontiguousarray(host(self.traj).transpose(2, 0, 1)),
+                    tlen=np.ascontiguousarray(self.tlen.cpu().numpy(), np.int32))
+
+
+class FleetNode:
+    """Every model's fleet of one rank (weak scaling: rank r owns robots [r*B, (r+1)*B) of each model's
+    seeded global fleet, sharding.shard_range), ticked together.
+
+    models: [(model, B_per_rank), ...]; a node with several models runs their launches concurrently, one HIP
+    stream each, joined on the caller's stream (each launch alone leaves SIMDs idle: ~2730 robots = 683
+    waves on 1024 SIMDs), with interleaved team placement (nmpc_batch.h NMPC_SCHED_INTERLEAVED)."""
+
+    def __init__(self, models, N, seed, dev, rank=0, world=1, gather=False, solver_factory=None):
+        self.dev = torch.device(dev)
+        self.rank, self.world = rank, world
+        self.multi = len(models) > 1
+        cuda = self.dev.type == "cuda"
+        self.fleets = []
+        for j, (m, B) in enumerate(models):
+            lo, hi = shard_range(B * world, rank, world)
+            stream = torch.cuda.Stream(self.dev) if (self.multi and cuda) else None
+            self.fleets.append(Fleet(m, hi - lo, N, seed + 100 * j, self.dev, start=lo, stream=stream,
+                                     solver_factory=solver_factory,
+                                     schedule="interleaved" if stream is not None else None))
+        self.B = sum(f.B for f in self.fleets)
+        self.offs = [int(v) for v in np.cumsum([0] + [f.B for f in self.fleets])]
+        self.gather = CommandGather(5, [self.B] * world, self.dev) if gather else None
+        self.gathered = None
+        # executed IPM iterations and failures, accumulated on the device
+        self.iters_sum = torch.zeros(self.B, dtype=torch.int64, device=self.dev)
+        self.iters_max = torch.zeros(self.B, dtype=torch.int32, device=self.dev)
+        self.fail_cnt = torch.zeros(self.B, dtype=torch.int64, device=self.dev)
+
+    def tick_all(self):
+        """One control tick of every robot of this rank."""
+        if not self.multi or self.dev.type != "cuda":
+            for f in self.fleets:
+                f.tick()
+            return
+        main = torch.cuda.current_stream(self.dev)
+        start = torch.cuda.Event()
+        start.record(main)
+        for f in self.fleets:
+            f.stream.wait_event(start)
+            f.tick()
+            done = torch.cuda.Event()
+            done.record(f.stream)
+            main.wait_event(done)
+
+    def accumulate(self):
+        for j, f in enumerate(self.fleets):
+            sl = slice(self.offs[j], self.offs[j + 1])
+            self.iters_sum[sl] += f.qp_iter
+            torch.maximum(self.iters_max[sl], f.qp_iter, out=self.iters_max[sl])
+            self.fail_cnt[sl] += f.status != 0
+
+    def reset_stats(self):
+        for t_ in (self.iters_sum, self.iters_max, self.fail_cnt):
+            t_.zero_()
+
+    def gather_commands(self):
+        """All-gather [u0 (padded to 4 rows); status] of every robot to every rank: [5][B * world]."""
+        if self.gather is not None:
+            self.gathered = self.gather([torch.cat([f.u0, f.status.float()[None]]) if f.u0.shape[0] == 4 else
+                                         torch.cat([f.u0, torch.zeros(4 - f.u0.shape[0], f.B, device=self.dev),
+                                                    f.status.float()[None]]) for f in self.fleets])
+        return self.gathered
+
+    def step(self):
+        """tick_all + statistics + (optional) command gather: one timed step of bench.py."""
+        self.tick_all()
+        self.accumulate()
+        if self.gather is not None:
+            self.gather_commands()

@@ -1,7 +1,11 @@
 """Seeded synthetic robot fleets (SURVEY.md 8d "Synthetic inputs").
 
 Every robot starts at x, y ~ U(-1, 1) m, theta ~ U(-pi, pi), wheel / speed / steering states ~ U(-0.5, 0.5)
-and carried vel-ref states ~ U(-0.5, 0.5). Half of the robots follow a circular-arc path (start within
+and carried vel-ref states ~ U(-0.5, 0.5), except the tric steering reference alpha_ref ~ U(-0.78, 0.78) rad:
+its rate bound (15 deg/s) keeps it within 23 deg of its start over the 1.5 s horizon, so the 45 deg bound
+(NMPCNavControlTric.cpp:24-29) is active only for robots that start near it (measured on the fp64 oracle,
+256 robots: 14-18 % of the fleet has alpha_ref on the bound at ticks 3-24, against 3-4 % with U(-0.5, 0.5);
+BASELINE config 4 asks for >= 10 %). Half of the robots follow a circular-arc path (start within
 0.2 m and 0.3 rad of the robot, curvature ~ U(-k, k) 1/m, |v| ~ U(0.2, 0.8) m/s, length ~ U(3, 5) m);
 the other half drive to a goal pose (x, y ~ U(-1.5, 1.5) m, random heading), which repeats one pose
 N+1 times and so triggers the diff terminal-weight hack (NMPCNavControlDiff.cpp:127-139).
@@ -13,12 +17,14 @@ from ._lib import model_dims
 
 DEFAULT_SEED = 20250824
 PARAMS = {"diff": (0.270, 0.1, 0.0), "omni4": (0.535, 0.1, 0.0), "tric": (0.270, 0.1, 0.5)}
+SPEED = {}  # path speed range per model (default U(0.2, 0.8) m/s)
+ALPHA_REF0 = 0.78  # tric: initial steering-reference states up to the 45 deg bound (>= 10 % of the fleet on it)
 
 
 BLOCK = 64  # robots per independently seeded block: a robot's data depends only on (seed, global index)
 
 
-def _block(model, seed, blk, kappa_max, path_frac, p):
+def _block(model, seed, blk, kappa_max, path_frac, p, speed):
     """Robots [blk*BLOCK, (blk+1)*BLOCK) of the global fleet, float64 [field][BLOCK]."""
     rng = np.random.default_rng([seed, blk])
     B = BLOCK
@@ -39,6 +45,8 @@ def _block(model, seed, blk, kappa_max, path_frac, p):
         vel[0] = rng.uniform(-0.5, 0.5, B)
         steer = rng.uniform(-0.5, 0.5, B)
     carried = rng.uniform(-0.5, 0.5, (nbx, B))
+    if model == "tric":
+        carried[1] = rng.uniform(-ALPHA_REF0, ALPHA_REF0, B)
     is_path = rng.uniform(0, 1, B) < path_frac
     path = np.zeros((6, B))
     # arcs
@@ -48,7 +56,7 @@ def _block(model, seed, blk, kappa_max, path_frac, p):
     path[1] = pose[1] + r * np.sin(a)
     path[2] = pose[2] + rng.uniform(-0.3, 0.3, B)
     path[3] = rng.uniform(-kappa_max, kappa_max, B)
-    path[4] = rng.uniform(0.2, 0.8, B)
+    path[4] = rng.uniform(speed[0], speed[1], B)
     path[5] = rng.uniform(3.0, 5.0, B)
     # goals
     goal = np.stack([rng.uniform(-1.5, 1.5, B), rng.uniform(-1.5, 1.5, B), rng.uniform(-np.pi, np.pi, B)])
@@ -58,17 +66,19 @@ def _block(model, seed, blk, kappa_max, path_frac, p):
     return dict(pose=pose, vel=vel, steer=steer, carried=carried, path=path, is_path=is_path)
 
 
-def make_fleet(model, B, seed=DEFAULT_SEED, kappa_max=None, path_frac=0.5, p=None, start=0):
+def make_fleet(model, B, seed=DEFAULT_SEED, kappa_max=None, path_frac=0.5, p=None, start=0, speed=None):
     """Robots [start, start + B) of the seeded global fleet (so an instance shard of a multi-GPU run holds
     exactly the robots a single-GPU run of the whole fleet would give those indices)."""
     p = PARAMS[model] if p is None else p
     if kappa_max is None:
-        kappa_max = 2.5 if model == "tric" else 1.0  # tric: drive alpha_ref into its bounds (BASELINE config 4)
+        kappa_max = 2.5 if model == "tric" else 1.0
+    if speed is None:
+        speed = SPEED.get(model, (0.2, 0.8))
     b0, b1 = start // BLOCK, (start + B + BLOCK - 1) // BLOCK
-    blocks = [_block(model, seed, k, kappa_max, path_frac, p) for k in range(b0, b1)]
+    blocks = [_block(model, seed, k, kappa_max, path_frac, p, speed) for k in range(b0, b1)]
     lo = start - b0 * BLOCK
     cat = {k: np.concatenate([bl[k] for bl in blocks], axis=-1)[..., lo:lo + B] for k in blocks[0]} if blocks else \
-        _block(model, seed, 0, kappa_max, path_frac, p)
+        _block(model, seed, 0, kappa_max, path_frac, p, speed)
     f32 = lambda x: np.ascontiguousarray(x, dtype=np.float32)  # noqa: E731
     out = {k: f32(v) for k, v in cat.items() if k != "is_path"}
     if not blocks:

@@ -113,7 +113,7 @@ def main(argv=None):
     ap.add_argument("--check-every", type=int, default=10)
     ap.add_argument("--reset-frac", type=float, default=0.02)
     ap.add_argument("--reset-every", type=int, default=7)
-    ap.add_argument("--kernel", default="team", choices=["team", "lane"])
+    ap.add_argument("--kernel", default="team", choices=["team"])
     ap.add_argument("--out", default=None)
     a = ap.parse_args(argv)
     rep = run(a.model, a.N, a.B, a.ticks, a.sample, a.check_every, a.reset_frac, a.reset_every, kernel=a.kernel)

@@ -46,12 +46,7 @@ def test_library_descriptors_match_the_shipped_defaults(built):
     """The in-tree libraries are generated from configs/acados_models.yaml; nmpc_codegen_default holds the
     same values (used when a capsule is created without a descriptor)."""
     import ctypes
-
-    class Desc(ctypes.Structure):
-        _fields_ = [("model", ctypes.c_int), ("N", ctypes.c_int), ("tf", ctypes.c_double),
-                    ("p", ctypes.c_double * 3), ("lbx", ctypes.c_double * 4), ("ubx", ctypes.c_double * 4),
-                    ("lbu", ctypes.c_double * 4), ("ubu", ctypes.c_double * 4), ("W", ctypes.c_double * 15),
-                    ("W_e", ctypes.c_double * 11)]
+    Desc = _lib.CodegenDesc
 
     P = yaml.safe_load(open(SHIPPED))
     L = _lib.lib()
@@ -77,6 +72,27 @@ int main(void) {
     ocp_nlp_out_get(c->nlp_config, c->nlp_dims, c->nlp_out, 0, "x", x);
     int nu = ocp_nlp_dims_get_from_attr(c->nlp_config, c->nlp_dims, c->nlp_out, DIFF2AMR_N - 1, "u");
     printf("%d %d %d %d %.6f\n", st, DIFF2AMR_N, c->nlp_dims->N, nu, x[2]);
+    diff2amr_acados_free(c);
+    diff2amr_acados_free_capsule(c);
+    return 0;
+}
+"""
+
+
+DISC_PROGRAM = r"""
+#include <stdio.h>
+#include "acados_solver_diff2amr.h"
+#include "acados_c/ocp_nlp_interface.h"
+int main(void) {
+    diff2amr_solver_capsule* c = diff2amr_acados_create_capsule();
+    int st_null = diff2amr_acados_create_with_discretization(c, 12, NULL);
+    double steps[12];
+    for (int k = 0; k < 12; k++) steps[k] = 0.05;
+    int st = diff2amr_acados_create_with_discretization(c, 12, steps);
+    double w[DIFF2AMR_NYN * DIFF2AMR_NYN] = {0};
+    int st_w = ocp_nlp_cost_model_set(c->nlp_config, c->nlp_dims, c->nlp_in, 13, "W", w);  /* past N = 12 */
+    int st_w12 = ocp_nlp_cost_model_set(c->nlp_config, c->nlp_dims, c->nlp_in, 12, "W", w);
+    printf("%d %d %d %d %d\n", st_null, st, c->nlp_dims->N, st_w, st_w12);
     diff2amr_acados_free(c);
     diff2amr_acados_free_capsule(c);
     return 0;
@@ -111,10 +127,16 @@ def test_generated_tree_links_like_the_reference(built, tmp_path):
     st, n_macro, n_dims, nu, th = res.stdout.split()
     assert (int(st), int(n_macro), int(n_dims), int(nu)) == (0, 20, 20, 2)
     assert float(th) == pytest.approx(math.pi, abs=1e-6)  # create(): x = ocp.constraints.x0 = [0, 0, pi, ...]
-    # run-time override of the baked horizon
-    env["NMPC_AMD_DIFF2AMR_N"] = "12"
-    res = subprocess.run([str(exe)], capture_output=True, text=True, env=env, timeout=120)
-    assert res.stdout.split()[2] == "12"
+    # another horizon needs its time steps, as in acados' create_with_discretization (a NULL vector with
+    # n != the baked N fails and says why); with uniform steps the capsule takes the new N
+    (tmp_path / "disc.c").write_text(DISC_PROGRAM)
+    exe2 = tmp_path / "disc"
+    subprocess.run(["gcc", "-std=c11", "-I", str(cg), "-I", os.path.join(ROOT, "include"), str(tmp_path / "disc.c"),
+                    _lib.LIB_PATH, str(cg / "libacados_ocp_solver_diff2amr.so"), "-o", str(exe2)], check=True)
+    res = subprocess.run([str(exe2)], capture_output=True, text=True, env=env, timeout=120)
+    assert res.returncode == 0, res.stderr
+    assert res.stdout.split() == ["1", "0", "12", "-1", "0"]
+    assert "new_time_steps is NULL" in res.stderr and "stage 13 outside 0..12" in res.stderr
 
 
 def test_generator_errors(tmp_path, caplog):

@@ -67,3 +67,60 @@ def test_gloo_world2_sharded_equals_single(tmp_path):
     assert got["u0"].shape == ref.shape
     assert np.array_equal(got["u0"], ref)
     assert float(got["elapsed"]) > 0
+
+
+# ---- the shipping driver loop (nmpc_nav_control_amd/fleet.py, bench.py) on gloo -----------------------------
+MIXED = [("diff", 3), ("omni4", 2), ("tric", 3)]  # robots per rank and model (weak scaling)
+MIX_N, MIX_TICKS, MIX_SEED = 8, 3, 20250824 + 4
+
+
+def _node(world, rank, models):
+    from cpu_fleet_solver import OracleFleetSolver
+    from nmpc_nav_control_amd.fleet import FleetNode
+    return FleetNode(models, MIX_N, MIX_SEED, torch.device("cpu"), rank=rank, world=world, gather=True,
+                     solver_factory=OracleFleetSolver)
+
+
+def _fleet_worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        node = _node(world, rank, MIXED)
+        logs = []
+        with TimedRegion() as tr:
+            for _ in range(MIX_TICKS):
+                node.step()  # bench.py's timed step: tick_all + accumulate + all-gather of [u0; status]
+                logs.append(node.gathered.numpy().copy())
+        if rank == 0:
+            np.savez(out, g=np.stack(logs), elapsed=tr.elapsed, iters=node.iters_sum.numpy(),
+                     fails=node.fail_cnt.numpy())
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_world2_fleet_node_equals_single(tmp_path):
+    """World 2 over gloo runs bench.py's FleetNode (mixed diff+omni4+tric fleet, per-rank instance shards,
+    per-tick all-gather of u0 + status through sharding.CommandGather) with the oracle behind the solver
+    interface; the gathered fleet commands equal a single-process node holding the whole fleet, bit for bit."""
+    out = str(tmp_path / "fleet.npz")
+    mp.spawn(_fleet_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    got = np.load(out)
+    single = _node(1, 0, [(m, 2 * b) for m, b in MIXED])
+    ref = []
+    for _ in range(MIX_TICKS):
+        single.step()
+        ref.append(single.gathered.numpy().copy())
+    ref = np.stack(ref)  # [T][5][sum 2B]: model-major
+    # the world-2 gather is rank-major: [rank 0: diff, omni4, tric | rank 1: diff, omni4, tric]
+    cols = []
+    off_single = np.cumsum([0] + [2 * b for _, b in MIXED])
+    per_rank = sum(b for _, b in MIXED)
+    for r in range(2):
+        for j, (_, b) in enumerate(MIXED):
+            cols.append(ref[:, :, off_single[j] + r * b: off_single[j] + (r + 1) * b])
+    ref_rank_major = np.concatenate(cols, axis=2)
+    assert got["g"].shape == ref_rank_major.shape == (MIX_TICKS, 5, 2 * per_rank)
+    assert np.array_equal(got["g"], ref_rank_major)
+    assert (got["g"][:, 4] == 0).all()  # every solve succeeded
+    assert np.abs(got["g"][:, :4]).max() > 0  # the commands are not trivially zero
+    assert float(got["elapsed"]) > 0 and (got["fails"] == 0).all() and (got["iters"] > 0).all()

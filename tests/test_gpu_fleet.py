@@ -1,0 +1,225 @@
+"""Bench-scale GPU parity: every robot of every BASELINE config replayed through the fp64 oracle, the mixed
+fleet of BASELINE config 5 on concurrent streams, and per-robot failure isolation.
+
+All three drive the shipping driver loop (nmpc_nav_control_amd/fleet.py: the code bench.py times). A replay
+takes the GPU's pre-tick state of every robot (warm iterate, carried refs, measurements, references), runs the
+oracle's batch_tick (prepare -> SQP-RTI -> post, NMPCNavControl*::run) on it, and compares with the GPU tick:
+  |u0 - u0_oracle|_inf <= 1e-3 and the predicted state trajectory (the new iterate x_1..x_N) within 1e-3,
+  SURVEY.md 8d; the GPU IPM stops by its fp32 rule, the oracle by its fp64 rule (DESIGN.md "Stopping rule").
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from nmpc_nav_control_amd.batch import BatchSolver
+from nmpc_nav_control_amd.fleet import Fleet, FleetNode
+from oracle.oracle import Oracle
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda:0")
+TOL_U = 1e-3
+TOL_X = 1e-3
+SEED = 20250824
+NTHREADS = int(os.environ.get("OMP_NUM_THREADS", "16"))
+
+
+def replay_and_compare(fleet, oracle, tick_fn):
+    """Snapshot the fleet's pre-tick state, run `tick_fn` (the GPU solve), replay every robot through the
+    oracle; returns (u0 err, x err, GPU statuses, oracle statuses, GPU iterate [B][N+1][NX])."""
+    torch.cuda.synchronize()
+    sn = fleet.snapshot()
+    tick_fn()
+    torch.cuda.synchronize()
+    xb_o, ub_o, cr_o = sn["xbar"].copy(), sn["ubar"].copy(), sn["carried"].copy()
+    nf, cmd_o, u0_o, st_o, _ = oracle.batch_tick(sn["pose"], sn["vel"], sn["steer"], sn["traj"], sn["tlen"], None,
+                                                 cr_o, xb_o, ub_o, nthreads=NTHREADS)
+    after = fleet.snapshot()
+    st = fleet.status.cpu().numpy()
+    ok = (st == 0) & (st_o == 0)
+    eu = float(np.abs(fleet.u0.cpu().numpy().T[ok] - u0_o[ok]).max()) if ok.any() else 0.0
+    ex = float(np.abs(after["xbar"][ok] - xb_o[ok]).max()) if ok.any() else 0.0
+    ec = float(np.abs(fleet.cmd.cpu().numpy().T[ok] - cmd_o[ok]).max()) if ok.any() else 0.0
+    return eu, max(ex, 0.0), ec, st, st_o, after["xbar"]
+
+
+@pytest.mark.parametrize("model,N,B,idx", [("diff", 40, 4096, 1), ("diff", 40, 1024, 1), ("omni4", 40, 4096, 2),
+                                           ("tric", 60, 8192, 3)])
+def test_bench_config_full_batch_replay(built, model, N, B, idx):
+    """BASELINE configs at full batch (the bench's own fleets): 20 closed-loop ticks with no failed solve, then
+    two ticks on which EVERY robot is replayed through the fp64 oracle. tric: >= 10 % of the robots have their
+    steering reference alpha_ref on its 45 deg bound somewhere on the horizon (SURVEY 8d config 4;
+    NMPCNavControlTric.cpp:24-29, scripts/tric/generate_c_code.py:47-57)."""
+    f = Fleet(model, B, N, SEED + idx, DEV)
+    o = Oracle(model, N)
+    for tick in range(20):
+        f.tick()
+        if tick % 5 == 4:
+            st = f.status.cpu().numpy()
+            assert (st == 0).all(), (tick, np.nonzero(st)[0][:8])
+    worst_u = worst_x = worst_c = 0.0
+    for _ in range(2):
+        eu, ex, ec, st, st_o, xb = replay_and_compare(f, o, f.solve)
+        assert (st == 0).all() and (st_o == 0).all(), (np.nonzero(st)[0][:8], np.nonzero(st_o)[0][:8])
+        worst_u, worst_x, worst_c = max(worst_u, eu), max(worst_x, ex), max(worst_c, ec)
+        if model == "tric":
+            on_bound = (np.abs(xb[:, 1:, 6]) >= np.pi / 4 - 1e-3).any(axis=1)
+            assert on_bound.mean() >= 0.10, on_bound.mean()
+        f.advance()
+    print(f"\n{model} N={N} B={B}: all robots, 2 ticks: u0 err {worst_u:.2e}, x err {worst_x:.2e}, cmd {worst_c:.2e}")
+    assert worst_u <= TOL_U, worst_u
+    assert worst_x <= TOL_X, worst_x
+    assert worst_c <= TOL_U, worst_c
+
+
+MIXED = [("diff", 2731), ("omni4", 2731), ("tric", 2730)]  # bench.py "mixed": 8192 per GPU of 65536 on 8
+
+
+def test_mixed_fleet_concurrent_streams_full_replay(built):
+    """BASELINE config 5 on one GPU (this rank's 8192 robots of the 65536 fleet): the three models' solves run
+    concurrently on their own HIP streams with interleaved team placement (FleetNode, as bench.py --config
+    mixed). Every robot of every model is replayed through the oracle on two ticks; and a run of the same
+    three fleets one after the other on the default stream gives bit-identical commands."""
+    N = 40
+    node = FleetNode(MIXED, N, SEED + 4, DEV)
+    assert node.multi and all(f.stream is not None for f in node.fleets)
+    seq = [Fleet(m, b, N, SEED + 4 + 100 * j, DEV) for j, (m, b) in enumerate(MIXED)]
+    oracles = [Oracle(m, N) for m, _ in MIXED]
+    for tick in range(20):
+        node.step()
+        for f in seq:
+            f.tick()
+        torch.cuda.synchronize()
+        for fa, fb in zip(node.fleets, seq):
+            assert torch.equal(fa.u0, fb.u0) and torch.equal(fa.cmd, fb.cmd), (tick, fa.model)
+            assert torch.equal(fa.status, fb.status) and (fa.status == 0).all(), (tick, fa.model)
+    assert int(node.fail_cnt.sum()) == 0
+    for _ in range(2):
+        snaps = [f.snapshot() for f in node.fleets]
+        torch.cuda.synchronize()
+        node.tick_all()
+        torch.cuda.synchronize()
+        for f, o, sn in zip(node.fleets, oracles, snaps):
+            xb_o, ub_o, cr_o = sn["xbar"].copy(), sn["ubar"].copy(), sn["carried"].copy()
+            _, cmd_o, u0_o, st_o, _ = o.batch_tick(sn["pose"], sn["vel"], sn["steer"], sn["traj"], sn["tlen"], None,
+                                                   cr_o, xb_o, ub_o, nthreads=NTHREADS)
+            st = f.status.cpu().numpy()
+            assert (st == 0).all() and (st_o == 0).all(), f.model
+            eu = float(np.abs(f.u0.cpu().numpy().T - u0_o).max())
+            ex = float(np.abs(f.snapshot()["xbar"] - xb_o).max())
+            print(f"\nmixed/{f.model} B={f.B}: u0 err {eu:.2e}, x err {ex:.2e}")
+            assert eu <= TOL_U and ex <= TOL_X, (f.model, eu, ex)
+
+
+def _restore(f, st):
+    xv, uv, cv = f.solver.state()
+    xv.copy_from(st["X"])
+    uv.copy_from(st["U"])
+    cv.copy_from(st["C"])
+    for k in ("pose", "vel", "traj", "tlen"):
+        getattr(f, k).copy_(st[k])
+
+
+def _save(f):
+    xv, uv, cv = f.solver.state()
+    return dict(X=xv.to_tensor(), U=uv.to_tensor(), C=cv.to_tensor(), pose=f.pose.clone(), vel=f.vel.clone(),
+                traj=f.traj.clone(), tlen=f.tlen.clone())
+
+
+def _outputs(f):
+    xv, uv, cv = f.solver.state()
+    return dict(u0=f.u0.clone(), cmd=f.cmd.clone(), status=f.status.clone(), qp_iter=f.qp_iter.clone(),
+                X=xv.to_tensor(), U=uv.to_tensor(), C=cv.to_tensor())
+
+
+def _timed_solve(f, setup, reps=7):
+    """Median kernel time of `reps` solves of the same tick (`setup` restores the pre-tick state each time)."""
+    ms = []
+    for _ in range(reps):
+        setup()
+        torch.cuda.synchronize()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        f.solve()
+        b.record()
+        torch.cuda.synchronize()
+        ms.append(a.elapsed_time(b))
+    return float(np.median(ms))
+
+
+def test_failure_stays_on_its_robot(built):
+    """a NaN or a QP failure on one robot must not poison the others. In a B=4096 diff N=40 tick
+    (the metric config) robot 7 gets a NaN pose (x0), robot 1001 NaN references (yref) and robot 2050 an
+    infeasible QP (carried vel-ref 50 m/s against the 1 m/s bound at stage 1):
+      - the NaN robots report status 1 after their first IPM iteration, the infeasible one fails or runs to
+        qp_iter_max (status 0 at the cap, DESIGN.md "Stopping rule"); a failed robot gets a zero (stop) command
+        and keeps its carried refs and iterate: the reference throws (NMPCNavControl.cpp:14-23) and the node
+        stops the robot (NMPCNavControlROS.cpp:716-719);
+      - every other robot's u0, cmd, status, qp_iter, iterate and carried refs are bit-identical to the clean
+        tick;
+      - with only the NaN robots injected the kernel time stays within 10 % of the clean tick."""
+    N, B = 40, 4096
+    f = Fleet("diff", B, N, SEED + 1, DEV)
+    for _ in range(20):
+        f.tick()
+    torch.cuda.synchronize()
+    st0 = _save(f)
+    f.solve()
+    clean = _outputs(f)
+    assert (clean["status"] == 0).all()
+    t_clean = _timed_solve(f, lambda: _restore(f, st0))
+
+    bad_x0, bad_ref, bad_qp = 7, 1001, 2050
+
+    def inject(with_qp):
+        _restore(f, st0)
+        f.pose[0, bad_x0] = float("nan")
+        f.traj[:, :, bad_ref] = float("nan")
+        if with_qp:
+            xv, uv, cv = f.solver.state()
+            C = st0["C"].clone()
+            C[0, bad_qp] = 50.0
+            cv.copy_from(C)
+
+    inject(True)
+    f.solve()
+    dirty = _outputs(f)
+    bad = [bad_x0, bad_ref, bad_qp]
+    st, it = dirty["status"].cpu().numpy(), dirty["qp_iter"].cpu().numpy()
+    assert st[bad_x0] == 1 and st[bad_ref] == 1 and it[bad_x0] == 0 and it[bad_ref] == 0, (st[bad], it[bad])
+    assert st[bad_qp] != 0 or it[bad_qp] == 50, (st[bad_qp], it[bad_qp])
+    good = np.ones(B, bool)
+    good[bad] = False
+    g = torch.from_numpy(good).to(DEV)
+    for k in ("u0", "cmd", "X", "U", "C"):
+        assert torch.equal(dirty[k][..., :B][..., g], clean[k][..., :B][..., g]), k
+    for k in ("status", "qp_iter"):
+        assert torch.equal(dirty[k][g], clean[k][g]), k
+    for i in bad:
+        if st[i] != 0:
+            assert (dirty["cmd"][:, i] == 0).all(), i
+            assert torch.equal(dirty["C"][:, i], st0["C"][:, i] if i != bad_qp else dirty["C"][:, i])
+            assert torch.equal(dirty["X"][:, i], st0["X"][:, i]) and torch.equal(dirty["U"][:, i], st0["U"][:, i])
+
+    t_nan = _timed_solve(f, lambda: inject(False))
+    print(f"\nclean {t_clean:.3f} ms, with 2 NaN robots {t_nan:.3f} ms; infeasible robot: status {st[bad_qp]}, "
+          f"qp_iter {it[bad_qp]}")
+    assert t_nan <= 1.10 * t_clean, (t_nan, t_clean)
+
+
+def test_reset_mode_keeps_carried_refs(built):
+    """nmpc_batch_init_iterate(mode=1) is {name}_acados_reset: the iterate is zeroed and the carried vel-ref
+    states stay (as the per-robot reset mask does; NMPCNavControlDiff.cpp:177-181 resets only the capsule);
+    mode 0 (create) also zeroes them."""
+    s = BatchSolver("diff", 20, 64)
+    xv, uv, cv = s.state()
+    cv.copy_from(torch.full((2, 64), 0.3, device=DEV))
+    uv.copy_from(torch.full((40, 64), 0.1, device=DEV))
+    s.init_iterate(mode=1)
+    torch.cuda.synchronize()
+    assert (cv.to_tensor() == 0.3).all() and (uv.to_tensor() == 0).all() and (xv.to_tensor() == 0).all()
+    s.init_iterate(mode=0)
+    torch.cuda.synchronize()
+    X = xv.to_tensor().reshape(21, 7, 64)
+    assert (cv.to_tensor() == 0).all() and (X[:, 2] == np.float32(np.pi)).all()

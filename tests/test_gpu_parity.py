@@ -40,7 +40,7 @@ def upload_iterate(solver, xbars, ubars):
     uv.copy_from(U)
 
 
-KERNELS = ["team", "lane"]
+KERNELS = ["team"]
 
 
 @pytest.mark.parametrize("kernel", KERNELS)
@@ -86,8 +86,6 @@ def test_run_closed_loop_matches_oracle(built, kernel, model, resets):
     fp64 warm-start chain (prepare -> sqp_rti -> post, NMPCNavControl*::run: no shift, x1 -> x0 carry of the
     vel-refs, NMPCNavControlDiff.cpp:168-172). With resets, every fifth robot is reset
     ({name}_acados_reset(capsule, 1), NMPCNavControlDiff.cpp:177-181) before the solves of ticks 3 and 8."""
-    if kernel == "lane" and resets:
-        pytest.skip("reset semantics are shared host logic; covered with the product kernel")
     N, B, T = 20, 70, 12
     reset_mask = torch.from_numpy((np.arange(B) % 5 == 0).astype(np.uint8)).to(DEV)
     fl = make_fleet(model, B, seed=11)
@@ -132,48 +130,4 @@ def test_run_closed_loop_matches_oracle(built, kernel, model, resets):
     assert np.isfinite(worst)
 
 
-@pytest.mark.parametrize("model,N,B", [("diff", 40, 4096), ("omni4", 40, 4096), ("tric", 60, 8192)])
-def test_bench_scale_closed_loop(built, model, N, B):
-    """BASELINE configs at full batch: 25 closed-loop ticks of the team kernel with no failed solve, and on the
-    last 4 ticks a 96-robot sample replayed through the fp64 oracle from the GPU's own pre-tick state
-    (iterate, carried refs, measurements, references): |u0 - u0_oracle| <= 1e-3."""
-    from nmpc_nav_control_amd.scenario import make_fleet
-    fl = make_fleet(model, B, seed=20250824 + 7)
-    solver = BatchSolver(model, N, B, kernel="team")
-    _, _, cr = solver.state()
-    cr.copy_from(t(fl["carried"]))
-    pose, vel, steer, path, s = t(fl["pose"]), t(fl["vel"]), t(fl["steer"]), t(fl["path"]), t(fl["s"])
-    steer_arg = steer if model == "tric" else None
-    traj = torch.zeros(N + 1, 3, B, device=DEV)
-    tlen = torch.zeros(B, dtype=torch.int32, device=DEV)
-    cmd = torch.zeros(3, B, device=DEV)
-    u0 = torch.zeros(solver.nu, B, device=DEV)
-    status = torch.zeros(B, dtype=torch.int32, device=DEV)
-    solver.fleet_sim_step(path, s, pose, vel, steer_arg, None, None, traj, tlen, advance=False)
-    o = Oracle(model, N)
-    xv, uv, cv = solver.state()
-    S = 96
-    host = lambda a: np.ascontiguousarray(a.cpu().numpy(), np.float64)  # noqa: E731
-    worst = 0.0
-    for tick in range(25):
-        check = tick >= 21
-        if check:
-            torch.cuda.synchronize()
-            X, U, C = xv.to_tensor(), uv.to_tensor(), cv.to_tensor()
-            xbar = np.ascontiguousarray(host(X[:, :S]).T.reshape(S, N + 1, o.nx))
-            ubar = np.ascontiguousarray(host(U[:, :S]).T.reshape(S, N, o.nu))
-            carried = np.ascontiguousarray(host(C[:, :S]).T)
-            args = (np.ascontiguousarray(host(pose[:, :S]).T), np.ascontiguousarray(host(vel[:, :S]).T),
-                    host(steer[:S]) if model == "tric" else None,
-                    np.ascontiguousarray(host(traj[:, :, :S]).transpose(2, 0, 1)),
-                    np.ascontiguousarray(tlen[:S].cpu().numpy(), np.int32))
-        solver.run(pose, vel, traj, steer=steer_arg, traj_len=tlen, cmd=cmd, u0=u0, status=status)
-        torch.cuda.synchronize()
-        st = status.cpu().numpy()
-        assert (st == 0).all(), (tick, np.nonzero(st)[0][:8], st[st != 0][:8])
-        if check:
-            nf, _, u0_o, st_o, _ = o.batch_tick(*args, None, carried, xbar, ubar)
-            assert nf == 0
-            worst = max(worst, float(np.abs(u0[:, :S].cpu().numpy().T - u0_o).max()))
-        solver.fleet_sim_step(path, s, pose, vel, steer_arg, u0, status, traj, tlen, advance=True)
-    assert worst <= TOL_U, worst
+# bench-scale replays of every robot: tests/test_gpu_fleet.py
