@@ -150,3 +150,26 @@ def test_generator_errors(tmp_path, caplog):
     empty.write_text(yaml.safe_dump({"other": 1}))
     assert gen.main([str(empty), "--out", str(tmp_path / "o2")]) == 0
     assert "No parameters found in YAML file to generate the 'diff' libraries." in caplog.text
+
+
+def test_descriptors_pinned_to_the_reference_loader():
+    """tools/generate_solver_libs.load_parameters against the reference's own scripts/*/common.py
+    load_parameters, evaluated on the shipped codegen yaml and variations of it (fixture made by
+    tests/golden/make_codegen_descriptors.py): N, TF, parameters, bounds (tric angles in radians) and the
+    W = blkdiag(Q, R), W_e = QN that generate_c_code.py bakes, bit for bit."""
+    fx = json.load(open(os.path.join(ROOT, "tests", "golden", "codegen_descriptors.json")))
+    assert len(fx["cases"]) == 16
+    pkeys = {"diff": ["DIST_B", "TAU_V"], "omni4": ["L1_PLUS_L2", "TAU_V"], "tric": ["DIST_D", "TAU_V", "TAU_A"]}
+    for case in fx["cases"]:
+        g, ref = case["geometry"], case["load_parameters"]
+        d = gen.load_parameters(g, case["params"])
+        assert d["N"] == ref["N"] and d["tf"] == ref["TF"], (g, case["params"])
+        assert d["p"] == [ref[k] for k in pkeys[g]]
+        assert d["W"] == ref["Q_diag"] + ref["R_diag"] and d["W_e"] == ref["QN_diag"]
+        nb = {"diff": 2, "omni4": 4, "tric": 1}[g]
+        assert d["ubx"][:nb] == [ref["V_MAX"]] * nb and d["lbx"][:nb] == [-ref["V_MAX"]] * nb
+        if g == "tric":
+            assert (d["lbx"][1], d["ubx"][1]) == (ref["ALPHA_MIN"], ref["ALPHA_MAX"])
+            assert (d["lbu"], d["ubu"]) == ([-ref["A_MAX"], -ref["DALPHA_MAX"]], [ref["A_MAX"], ref["DALPHA_MAX"]])
+        else:
+            assert d["lbu"] == [-ref["A_MAX"]] * nb and d["ubu"] == [ref["A_MAX"]] * nb

@@ -1,17 +1,26 @@
-"""Summarise rocprofv3 --pmc passes of tools/pmc.sh into per-dispatch averages per kernel, and write the
-L2-fabric traffic of the solve kernel into profiles/pmc_traffic.json (read by bench.py's roofline.traffic).
+"""Summarise the rocprofv3 --pmc passes of tools/pmc.sh into per-dispatch averages per kernel and write the
+solve kernel's record to profiles/<round>/pmc/pmc_<config>.json (read by bench.py's roofline: traffic and
+issue figures).
 
-usage: python tools/pmc_summary.py gpurun_out/<tag> <key e.g. diff_N40_B4096> [--write]
+usage: python tools/pmc_summary.py gpurun_out/<tag> <config key, e.g. diff_N40_B4096> [--round r02] [--write]
 
-traffic = 2 x FETCH_SIZE + WRITE_SIZE (KB -> bytes): MI355X_MICROARCH.md "HBM": on gfx950 FETCH_SIZE tallies
-128-B requests at 64 B (x2 for wide reads); both counters sit at the L2 memory side, so Infinity-Cache (MALL)
-hits are included -- this is L2-miss traffic, an upper bound on HBM bytes.
+Figures per launch of the solve kernel (for a mixed fleet: the sum over its per-model launches of one step):
+  l2_fabric_bytes_per_launch = 2 x FETCH_SIZE + WRITE_SIZE (KB -> bytes). MI355X_MICROARCH.md "HBM": on gfx950
+      FETCH_SIZE tallies 128-B requests at 64 B (x2 for wide reads); both counters sit at the L2's memory side,
+      so Infinity-Cache (MALL) hits are included: L2-miss traffic, an upper bound on HBM bytes.
+  valu_insts_per_wave = SQ_INSTS_VALU / SQ_WAVES.
+  valu_issue_frac = SQ_INSTS_VALU / SQ_WAVE_CYCLES: SQ_WAVE_CYCLES counts quad-cycles (MI355X_MICROARCH.md
+      "s_memtime tick vs SQ PMC units") and one wave issues at most one VALU instruction per quad-cycle
+      (4 cycles, row "vector-instruction ISSUE cost"), so this is the share of the waves' lifetime spent
+      issuing VALU at the one-wave minimum cost (fp64 FMAs measure 4.6 cycles, DPP forms 5.6: a lower bound).
+  wait_frac / active_frac = SQ_WAIT_ANY / SQ_ACTIVE_INST_ANY over SQ_WAVE_CYCLES (disjoint buckets).
 """
 import csv
 import glob
 import json
 import os
 import re
+import subprocess
 import sys
 from collections import defaultdict
 
@@ -25,33 +34,54 @@ def load(prefix):
             for row in csv.DictReader(fh):
                 m = re.search(r"\b(k_\w+)", row["Kernel_Name"])
                 name = m.group(1) if m else row["Kernel_Name"][:60]
+                # one model's kernel template: keep the model in the name (mixed fleets launch three)
+                t = re.search(r"k_sqp_rti_team<nmpc::(\w+)", row["Kernel_Name"])
+                if t:
+                    name = f"k_sqp_rti_team<{t.group(1)}>"
                 acc[name][row["Counter_Name"]].append(float(row["Counter_Value"]))
     return {k: {c: sum(v) / len(v) for c, v in d.items()} for k, d in acc.items()}
 
 
 def main():
     prefix, key = sys.argv[1], sys.argv[2]
+    rnd = sys.argv[sys.argv.index("--round") + 1] if "--round" in sys.argv else "r02"
     summ = load(prefix)
     for k, d in sorted(summ.items()):
         print(k)
         for c, v in sorted(d.items()):
             print(f"   {c:24s} {v:16.4g}")
-    solve = [k for k in summ if "k_sqp_rti" in k]
+    solve = sorted(k for k in summ if "k_sqp_rti" in k)
     if not solve:
         sys.exit("no solve kernel in the counters")
-    d = summ[solve[0]]
-    traffic = 2 * d.get("FETCH_SIZE", 0.0) * 1024 + d.get("WRITE_SIZE", 0.0) * 1024
-    rec = {"kernel": solve[0], "hbm_bytes_per_launch": traffic, "fetch_size_kb": d.get("FETCH_SIZE"),
-           "write_size_kb": d.get("WRITE_SIZE"), "tcc_hit": d.get("TCC_HIT_sum"), "tcc_miss": d.get("TCC_MISS_sum"),
-           "source": os.path.basename(prefix.rstrip("/")),
-           "note": "2*FETCH_SIZE + WRITE_SIZE per dispatch (L2-miss traffic incl. MALL hits)"}
+    tot = defaultdict(float)
+    for k in solve:
+        for c, v in summ[k].items():
+            tot[c] += v
+    fetch, write = tot.get("FETCH_SIZE", 0.0), tot.get("WRITE_SIZE", 0.0)
+    cyc = tot.get("SQ_WAVE_CYCLES", 0.0)
+    hit, miss = tot.get("TCC_HIT_sum", 0.0), tot.get("TCC_MISS_sum", 0.0)
+    try:
+        commit = subprocess.run(["git", "-C", ROOT, "rev-parse", "--short", "HEAD"], capture_output=True,
+                                text=True).stdout.strip()
+    except OSError:
+        commit = None
+    rec = {"kernels": solve, "config": key, "l2_fabric_bytes_per_launch": 2 * fetch * 1024 + write * 1024,
+           "fetch_size_kb": fetch, "write_size_kb": write,
+           "tcc_hit_rate": hit / (hit + miss) if hit + miss > 0 else None,
+           "valu_insts_per_wave": tot["SQ_INSTS_VALU"] / tot["SQ_WAVES"] if tot.get("SQ_WAVES") else None,
+           "valu_issue_frac": tot["SQ_INSTS_VALU"] / cyc if cyc else None,
+           "wait_frac": tot["SQ_WAIT_ANY"] / cyc if cyc else None,
+           "active_frac": tot["SQ_ACTIVE_INST_ANY"] / cyc if cyc else None,
+           "salu_insts_per_wave": tot["SQ_INSTS_SALU"] / tot["SQ_WAVES"] if tot.get("SQ_WAVES") else None,
+           "source": os.path.basename(prefix.rstrip("/")), "source_commit": commit,
+           "note": "per launch (mixed: summed over the per-model launches of one step); "
+                   "traffic = 2*FETCH_SIZE + WRITE_SIZE (L2<->fabric incl. Infinity-Cache hits)"}
     print(json.dumps(rec, indent=1))
     if "--write" in sys.argv:
-        out = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-        data = json.load(open(out)) if os.path.exists(out) else {}
-        data[key] = rec
-        with open(out, "w") as fh:
-            json.dump(data, fh, indent=1)
+        out_dir = os.path.join(ROOT, "profiles", rnd, "pmc")
+        os.makedirs(out_dir, exist_ok=True)
+        with open(os.path.join(out_dir, f"pmc_{key}.json"), "w") as fh:
+            json.dump(rec, fh, indent=1)
 
 
 if __name__ == "__main__":
