@@ -121,6 +121,7 @@ int nmpc_batch_set_kernel(nmpc_batch* b, int kernel);
 #define NMPC_SCHED_AUTO 1
 #define NMPC_SCHED_SORTED 2
 #define NMPC_SCHED_INTERLEAVED 3
+#define NMPC_SCHED_SPREAD 4 /* the hardest 4 robots per block in its first wave, easy CU-mates (schedule.hip) */
 int nmpc_batch_set_schedule(nmpc_batch* b, int mode);
 
 /* Device pointers of the resident state: xbar [(N+1)*NX][stride], ubar [N*NU][stride],

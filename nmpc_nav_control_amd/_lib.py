@@ -63,7 +63,7 @@ BATCH_SYMBOLS = [
     "nmpc_capsule_solve", "nmpc_capsule_batch_solve", "nmpc_capsule_free", "nmpc_capsule_print_stats",
 ]
 KERNELS = {"team": 0}
-SCHEDULES = {"off": 0, "auto": 1, "sorted": 2, "interleaved": 3}
+SCHEDULES = {"off": 0, "auto": 1, "sorted": 2, "interleaved": 3, "spread": 4}
 NLP_SYMBOLS = ["ocp_nlp_constraints_model_set", "ocp_nlp_cost_model_set", "ocp_nlp_out_get", "ocp_nlp_out_set",
                "ocp_nlp_get", "ocp_nlp_dims_get_from_attr"]
 CAPSULE_SUFFIXES = ["create_capsule", "free_capsule", "create", "create_with_discretization", "reset",

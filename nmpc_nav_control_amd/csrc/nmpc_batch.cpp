@@ -250,8 +250,8 @@ int nmpc_batch_create(const nmpc_model_params* prm, int capacity, nmpc_batch** o
     b->ny = b->nx + b->nu;
     b->kp = to_kparams(*prm, b->nx, b->nu, b->nbx, b->nbu);
     if (const char* sv = std::getenv("NMPC_AMD_SCHED")) {  // off | auto | sorted | interleaved
-        const char* names[4] = {"off", "auto", "sorted", "interleaved"};
-        for (int i = 0; i < 4; i++)
+        const char* names[5] = {"off", "auto", "sorted", "interleaved", "spread"};
+        for (int i = 0; i < 5; i++)
             if (std::strcmp(sv, names[i]) == 0) b->sched = i;
     }
     const int N = prm->N;
@@ -399,7 +399,7 @@ int nmpc_batch_set_kernel(nmpc_batch* b, int kernel)
 int nmpc_batch_set_schedule(nmpc_batch* b, int mode)
 {
     if (!b) return set_err(NMPC_ERR_ARG, "batch is NULL");
-    if (mode < NMPC_SCHED_OFF || mode > NMPC_SCHED_INTERLEAVED) return set_err(NMPC_ERR_ARG, "unknown schedule");
+    if (mode < NMPC_SCHED_OFF || mode > NMPC_SCHED_SPREAD) return set_err(NMPC_ERR_ARG, "unknown schedule");
     b->sched = mode;
     return NMPC_OK;
 }

@@ -8,7 +8,11 @@
 //   sorted      slot s <- rank s: waves hold robots of like difficulty, the hard half of the blocks is
 //               dispatched first;
 //   interleaved even blocks take ranks from the hard end, odd blocks from the easy end, so neighbouring
-//               blocks (which share CUs) pair a hard block with an easy one.
+//               blocks (which share CUs) pair a hard block with an easy one;
+//   spread      the first wave of every block (one block = one CU at one wave per SIMD) takes the 4 x blocks
+//               hardest robots, the other three waves the rest in order: the kernel ends with the slowest
+//               wave, and a hard wave whose CU-mates finish early runs its last iterations alone on the CU
+//               (memory pipeline and L1 no longer shared).
 // Every robot keeps its own arithmetic whatever slot it lands in, so the order changes no result.
 #include "nmpc_kernels.hpp"
 
@@ -68,6 +72,17 @@ __global__ __launch_bounds__(kOrderThreads) void k_team_order(const int* __restr
     if (layout == NMPC_SCHED_SORTED) return;
     __threadfence_block();
     __syncthreads();
+    if (layout == NMPC_SCHED_SPREAD) {
+        // wave-0 slots (s % 16 < 4) of block j take ranks 4 j .. 4 j + 3; every other slot follows in slot
+        // order after the n0 wave-0 slots (only the last block can be partial)
+        const int nb = (B + 15) >> 4;
+        const int n0 = 4 * (nb - 1) + min(4, B - 16 * (nb - 1));
+        for (int sl = t; sl < B; sl += kOrderThreads) {
+            const int j = sl >> 4, w = sl & 15;
+            order[sl] = sorted[(w < 4) ? 4 * j + w : n0 + sl - 4 * (j + 1)];
+        }
+        return;
+    }
     // interleaved: slot s in block j = s / 16 (16 teams per block); even blocks count up from the hardest
     // rank, odd blocks down from the easiest (only the last block can be partial, so both runs are dense)
     for (int sl = t; sl < B; sl += kOrderThreads) {

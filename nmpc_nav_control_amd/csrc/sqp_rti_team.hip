@@ -59,22 +59,28 @@ __device__ unsigned long long g_stamps_c1[256][kStampIts];
 template <class M>
 struct TeamRec {
     static constexpr int NX = M::NX, NU = M::NU, NV = NX + NU, NGV = M::NGV;
-    // Field order: the fields P1 rewrites first (it stores only that prefix, [0, NP1)), then the rest the light
-    // sweeps read (they load the prefix [0, NL)), then the P1-only inputs. P1 reads all RS floats.
-    static constexpr int TL = 0, TU = 1, LL = 2, LU = 3;  // slacks / multipliers of the box bound (bounded slots)
-    static constexpr int Z = 4, LR = 5;                   // QP iterate, Luu^-1 rhs
-    static constexpr int LM = 6;                          // NU floats: row v of the stage factor, input columns
-    static constexpr int RU = LM + NU;                    // u-stationarity residual
-    static constexpr int NP1 = RU + 1;                    // prefix rewritten by P1
-    static constexpr int LB = NP1, UB = NP1 + 1;          // bounds relative to the SQP iterate
-    static constexpr int GV = UB + 1;                     // NGV floats: varying rows of column v of [B A]
-    static constexpr int DZA = GV + NGV;                  // affine direction
-    static constexpr int NL = DZA + 1;                    // prefix read by the light sweeps
-    static constexpr int DZ = NL, GR = NL + 1;            // combined direction, cost gradient (P1 only)
+    // Field order: P1's write-only outputs first (LR, LM, RU: P1 never loads them, so no record load is issued
+    // into registers P1 overwrites), then the bound quad, the iterate and the rest the light sweeps read
+    // (prefix [0, NL)), then the P1-only inputs (DZ, GR). P1 loads [P1L0, P1L1) and stores [0, P1S1).
+    // Same-box A/B against the round-1 order (P1 rewrote a prefix it also loaded, and the compiler reused the
+    // dead lanes of those loads, waiting on them): kernel ms diff N=40 B=4096 1.430 -> 1.404, omni4 1.664 ->
+    // 1.655 (profiles/r02/ab/abwb.txt)
+    static constexpr int LR = 0, LM = 1, RU = LM + NU;   // Luu^-1 rhs, row v of the input columns, u residual
+    static constexpr int Z = (NU == 2) ? 8 : 6, DZA = Z + 1 + ((NU == 2) ? 2 : 0);  // iterate, affine direction
+    static constexpr int TL = (NU == 2) ? 4 : 8, TU = TL + 1, LL = TL + 2, LU = TL + 3;  // bound quad
+    static constexpr int LB = (NU == 2) ? 9 : 12, UB = LB + 1;  // bounds relative to the SQP iterate
+    static constexpr int GV = (NU == 2) ? 12 : 14;             // NGV floats: varying rows of column v of [B A]
+    static constexpr int NL = GV + NGV;                        // prefix read by the light sweeps
+    static constexpr int DZ = NL, GR = NL + 1;                 // combined direction, cost gradient (P1 only)
+    static constexpr int P1L0 = (NU == 2) ? TL : Z, P1L1 = GR + 1;  // P1 loads
+    static constexpr int P1S1 = 12;                                // P1 stores [0, P1S1)
+    static_assert(NU == 2 || NU == 4, "layouts for NU = 2 and 4");
+    static_assert(RU < ((NU == 2) ? TL : Z) && DZA < P1S1 && LU < P1S1 && Z < P1S1, "P1 store block");
     static constexpr int NF = NL, NB = NL;
     static constexpr int RS = (GR + 1 + 3) / 4 * 4;       // record floats (dwordx4 aligned)
     static constexpr int NQ = RS / 4;
     static_assert(NV <= 16, "a team holds at most 16 variables");
+    static_assert(TL % 4 == 0, "bound quad aligned");
 };
 
 template <class M>
@@ -92,7 +98,13 @@ constexpr float kStatRelT = 1e-5f;
 // curvature R dt (DESIGN.md "Stopping rule")
 constexpr float kCompMaxRatio = 30.0f;
 #ifndef LIGHT_D
-#define LIGHT_D 4  // record buffers of the light (solve-only) sweeps
+#define LIGHT_D 4  // record buffers of the forward light sweeps (F0, F1)
+#endif
+#ifndef LIGHT_DC
+#define LIGHT_DC LIGHT_D  // record buffers of the corrector backward sweep (C1)
+#endif
+#ifndef P1_D
+#define P1_D 2  // record buffers of the factorisation sweep (2: ping-pong)
 #endif
 constexpr float kFar = 1e30f;  // sentinel bound / slack of unbounded slots (z + kFar - kFar == 0 in fp32)
 #ifdef NMPC_STAMPS
@@ -213,62 +225,52 @@ constexpr int rec_lane() { return QM ? 4 : RS; }  // floats between the records 
 template <int RS, bool QM>
 constexpr int rec_off(int f) { return (f / 4) * rec_qs<RS, QM>() + f % 4; }  // offset of field f in a lane's record
 
-// the first NF floats of a record: NF/4 dwordx4 loads and one dword, dwordx2 or dwordx3 load for the rest
-template <int NF, int RS, bool QM>
-__device__ __forceinline__ void rec_load_prefix(const float* p, float (&v)[RS])
+
+// floats [F0, F1) of a record, one access per quad piece (a piece never crosses a quad)
+template <int F0, int F1, int RS, bool QM>
+__device__ __forceinline__ void rec_load_range(const float* p, float (&v)[RS])
 {
-    static_assert(NF <= RS, "prefix longer than the record");
     constexpr int QS = rec_qs<RS, QM>();
-#pragma unroll
-    for (int i = 0; i < NF / 4; i++) {
-        const float4 t = *reinterpret_cast<const float4*>(p + i * QS);
-        v[4 * i + 0] = t.x;
-        v[4 * i + 1] = t.y;
-        v[4 * i + 2] = t.z;
-        v[4 * i + 3] = t.w;
-    }
-    constexpr int o = NF / 4 * 4, rem = NF % 4;
-    const float* pr = p + (NF / 4) * QS;
-    if constexpr (rem == 1) {
-        v[o] = pr[0];
-    } else if constexpr (rem == 2) {
-        const float2 t = *reinterpret_cast<const float2*>(pr);
-        v[o] = t.x;
-        v[o + 1] = t.y;
-    } else if constexpr (rem == 3) {
-        const float3 t = *reinterpret_cast<const float3*>(pr);
-        v[o] = t.x;
-        v[o + 1] = t.y;
-        v[o + 2] = t.z;
-    }
+    sfor<F0 / 4, (F1 + 3) / 4>([&](auto qc) {
+        constexpr int q = decltype(qc)::value;
+        constexpr int a = (F0 > 4 * q) ? F0 : 4 * q, b = (F1 < 4 * q + 4) ? F1 : 4 * q + 4, L = b - a;
+        static_assert(L != 2 || a % 2 == 0, "dwordx2 piece 8-byte aligned");
+        const float* pq = p + q * QS + (a - 4 * q);
+        if constexpr (L == 4) {
+            const float4 t = *reinterpret_cast<const float4*>(pq);
+            v[a] = t.x; v[a + 1] = t.y; v[a + 2] = t.z; v[a + 3] = t.w;
+        } else if constexpr (L == 3) {
+            const float3 t = *reinterpret_cast<const float3*>(pq);
+            v[a] = t.x; v[a + 1] = t.y; v[a + 2] = t.z;
+        } else if constexpr (L == 2) {
+            const float2 t = *reinterpret_cast<const float2*>(pq);
+            v[a] = t.x; v[a + 1] = t.y;
+        } else {
+            v[a] = pq[0];
+        }
+    });
 }
 
-template <int RS, bool QM>
-__device__ __forceinline__ void rec_load(const float* p, float (&v)[RS])
+template <int F0, int F1, int RS, bool QM>
+__device__ __forceinline__ void rec_store_range(float* p, const float (&v)[RS])
 {
-    rec_load_prefix<RS, RS, QM>(p, v);
-}
-
-// floats [F0, NF) of a record, F0 a multiple of 4 (the fields P1 rewrites)
-template <int NF, int RS, bool QM, int F0 = 0>
-__device__ __forceinline__ void rec_store_prefix(float* p, const float (&v)[RS])
-{
-    static_assert(F0 % 4 == 0, "range starts on a quad");
     constexpr int QS = rec_qs<RS, QM>();
-#pragma unroll
-    for (int i = F0 / 4; i < NF / 4; i++)
-        *reinterpret_cast<float4*>(p + i * QS) = make_float4(v[4 * i + 0], v[4 * i + 1], v[4 * i + 2], v[4 * i + 3]);
-    constexpr int o = NF / 4 * 4, rem = NF % 4;
-    float* pr = p + (NF / 4) * QS;
-    if constexpr (rem == 1) pr[0] = v[o];
-    else if constexpr (rem == 2) *reinterpret_cast<float2*>(pr) = make_float2(v[o], v[o + 1]);
-    else if constexpr (rem == 3) *reinterpret_cast<float3*>(pr) = make_float3(v[o], v[o + 1], v[o + 2]);
+    sfor<F0 / 4, (F1 + 3) / 4>([&](auto qc) {
+        constexpr int q = decltype(qc)::value;
+        constexpr int a = (F0 > 4 * q) ? F0 : 4 * q, b = (F1 < 4 * q + 4) ? F1 : 4 * q + 4, L = b - a;
+        static_assert(L != 2 || a % 2 == 0, "dwordx2 piece 8-byte aligned");
+        float* pq = p + q * QS + (a - 4 * q);
+        if constexpr (L == 4) *reinterpret_cast<float4*>(pq) = make_float4(v[a], v[a + 1], v[a + 2], v[a + 3]);
+        else if constexpr (L == 3) *reinterpret_cast<float3*>(pq) = make_float3(v[a], v[a + 1], v[a + 2]);
+        else if constexpr (L == 2) *reinterpret_cast<float2*>(pq) = make_float2(v[a], v[a + 1]);
+        else pq[0] = v[a];
+    });
 }
 
 template <int RS, bool QM>
 __device__ __forceinline__ void rec_store(float* p, const float (&v)[RS])
 {
-    rec_store_prefix<RS, RS, QM>(p, v);
+    rec_store_range<0, RS, RS, QM>(p, v);
 }
 
 // Newton directions of one bounded variable (lower slack tl / multiplier ll, upper tu / lu) for a step dz with
@@ -287,9 +289,14 @@ __device__ __forceinline__ BoundDir bound_dir(float dz, float rl, float rr, floa
     return d;
 }
 
+// Largest step keeping v + a dv >= 0, folded into amax. t = -v / dv is a bound only for dv < 0 (v >= 0): then
+// t >= +0; for dv >= 0 it is <= -0, -inf or a NaN. As unsigned integers non-negative floats keep their order and
+// every negative float (and -0) is larger than +inf, so one unsigned min drops the non-bounds without a compare /
+// select (same-box A/B against the branch form: diff 1.403 -> 1.398 ms, tric 4.386 -> 4.358 ms)
 __device__ __forceinline__ float step_bound_r(float amax, float v, float dv)
 {
-    return (dv < 0.0f) ? fminf(amax, -v * frcp(dv)) : amax;
+    const float t = -v * frcp(dv);
+    return __uint_as_float(min(__float_as_uint(amax), __float_as_uint(t)));
 }
 
 // MS: store the slack / multiplier quad only where a bound lives (launches with more waves than SIMDs, where the
@@ -544,14 +551,14 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
         const ptrdiff_t step = ld ? (ptrdiff_t)KS * dir : 0;
         const float* p = tbase + (size_t)k0 * KS;
         float ra[RS], rb[RS];
-        rec_load<RS, QM>(p, ra);
+        rec_load_range<R::P1L0, R::P1L1, RS, QM>(p, ra);
         for (int k = k0;; k += 2 * dir) {
             const float* p1 = (k == k1) ? p : p + step;
-            rec_load<RS, QM>(p1, rb);
+            rec_load_range<R::P1L0, R::P1L1, RS, QM>(p1, rb);
             body(k, ra);
             if (k == k1) break;
             const float* p2 = (k + dir == k1) ? p1 : p1 + step;
-            rec_load<RS, QM>(p2, ra);
+            rec_load_range<R::P1L0, R::P1L1, RS, QM>(p2, ra);
             body(k + dir, rb);
             if (k + dir == k1) break;
             p = p2;
@@ -559,19 +566,19 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
     };
     // D buffers: buf[i] holds stage k + i*dir while the loop is at k; after body(k + i*dir) it is refilled with
     // stage k + (i + D)*dir (clamped at k1), so D - 1 records are in flight during every body
-    auto sweepd = [&](auto dc, auto fc, int k0, int k1, int dir, bool ld, auto&& body) {
+    auto sweepd = [&](auto dc, auto f0c, auto fc, int k0, int k1, int dir, bool ld, auto&& body) {
         constexpr int D = decltype(dc)::value;
-        constexpr int F = decltype(fc)::value;  // floats of the record prefix this sweep reads
+        constexpr int F0 = decltype(f0c)::value, F = decltype(fc)::value;  // floats [F0, F) this sweep reads
         const ptrdiff_t step = ld ? (ptrdiff_t)KS * dir : 0;
         float buf[D][RS];
         const float* p = tbase + (size_t)k0 * KS;
         int kl = k0;
-        rec_load_prefix<F, RS, QM>(p, buf[0]);
+        rec_load_range<F0, F, RS, QM>(p, buf[0]);
         sfor<1, D>([&](auto ic) {
             constexpr int i = decltype(ic)::value;
             p = (kl == k1) ? p : p + step;
             kl = (kl == k1) ? kl : kl + dir;
-            rec_load_prefix<F, RS, QM>(p, buf[i]);
+            rec_load_range<F0, F, RS, QM>(p, buf[i]);
         });
         for (int k = k0;; k += D * dir) {
             bool stop = false;
@@ -585,7 +592,7 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
                 }
                 p = (kl == k1) ? p : p + step;
                 kl = (kl == k1) ? kl : kl + dir;
-                rec_load_prefix<F, RS, QM>(p, buf[i]);
+                rec_load_range<F0, F, RS, QM>(p, buf[i]);
             });
             if (stop) break;
         }
@@ -608,7 +615,12 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
         const float a_upd = (it > 0 && !done) ? alpha : 0.0f;
         // P1_D record buffers: the heavy sweep's next records are in flight for P1_D - 1 stage bodies (at four
         // waves per CU a record load from the Infinity Cache takes about one stage body)
+#if P1_D > 2
+        sweepd(std::integral_constant<int, P1_D>{}, std::integral_constant<int, R::P1L0>{},
+               std::integral_constant<int, R::P1L1>{}, N, 0, -1, act, [&](int k, float (&rc)[RS]) {
+#else
         sweep(N, 0, -1, act, [&](int k, float (&rc)[RS]) {
+#endif
             STAMPF(0);
             const bool vu = is_u && k < N;
             const bool vx = is_x && k >= 1;
@@ -721,11 +733,13 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
             STAMPF(6);
             if constexpr (MS) {
                 // slack / multiplier quad only where a bound lives (elsewhere it holds the constant sentinel)
-                static_assert(R::TL == 0 && R::LU == 3, "bound quad first");
-                if (act && bnd) rec_store_prefix<4, RS, QM>(tbase + (size_t)k * KS, rc);
-                if (act) rec_store_prefix<R::NP1, RS, QM, 4>(tbase + (size_t)k * KS, rc);
+                if (act && bnd) rec_store_range<R::TL, R::TL + 4, RS, QM>(tbase + (size_t)k * KS, rc);
+                if (act) {
+                    if constexpr (R::TL > 0) rec_store_range<0, R::TL, RS, QM>(tbase + (size_t)k * KS, rc);
+                    if constexpr (R::TL + 4 < R::P1S1) rec_store_range<R::TL + 4, R::P1S1, RS, QM>(tbase + (size_t)k * KS, rc);
+                }
             } else {
-                if (act) rec_store_prefix<R::NP1, RS, QM>(tbase + (size_t)k * KS, rc);
+                if (act) rec_store_range<0, R::P1S1, RS, QM>(tbase + (size_t)k * KS, rc);
             }
             STAMPF(7);
         });
@@ -791,7 +805,7 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
             if (pass > 0) {
                 // corrector rhs through the stored factorisation (backward)
                 float pvc = 0.0f;
-                sweepd(std::integral_constant<int, LIGHT_D>{}, std::integral_constant<int, R::NB>{}, N, 0, -1, ld, [&](int k, float (&rc)[RS]) {
+                sweepd(std::integral_constant<int, LIGHT_DC>{}, std::integral_constant<int, 0>{}, std::integral_constant<int, R::NB>{}, N, 0, -1, ld, [&](int k, float (&rc)[RS]) {
                     const bool vu = is_u && k < N;
                     float ghat;
                     {  // branch-free: 0 on the kFar-sentinel slots (see P0)
@@ -831,7 +845,7 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
             auto fwd = [&](auto cc) {
             constexpr bool corr = decltype(cc)::value == 1;
             float dxs = 0.0f;
-            sweepd(std::integral_constant<int, LIGHT_D>{}, std::integral_constant<int, R::NF>{}, 0, N, 1, ld, [&](int k, float (&rc)[RS]) {
+            sweepd(std::integral_constant<int, LIGHT_D>{}, std::integral_constant<int, 0>{}, std::integral_constant<int, R::NF>{}, 0, N, 1, ld, [&](int k, float (&rc)[RS]) {
                 const bool vu = is_u && k < N;
                 const bool vx = is_x && k >= 1;
                 const bool valid = vu || vx;

@@ -58,7 +58,7 @@ def test_placement_invariance(built, model, B):
     ref = run_fleet(model, 20, B, 5, "off")
     spread = np.concatenate([o[2] for o in ref[0]])
     assert spread.max() > spread.min()  # the sort actually permutes
-    for sched in ("sorted", "interleaved", "auto"):
+    for sched in ("sorted", "interleaved", "spread", "auto"):
         assert_same(ref, run_fleet(model, 20, B, 5, sched))
 
 

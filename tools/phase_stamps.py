@@ -5,13 +5,14 @@ import os, sys, ctypes, numpy as np, torch
 root = os.environ.get("GRAFT_REPO_ROOT", "/root/repo")
 os.environ["NMPC_AMD_LIB"] = os.environ.get("STAMPS_LIB") or os.path.join(root, "nmpc_nav_control_amd/lib/diag/libnmpc_amd.so")
 sys.path.insert(0, root)
-import bench
+from nmpc_nav_control_amd.fleet import Fleet
+from nmpc_nav_control_amd.scenario import DEFAULT_SEED
 from nmpc_nav_control_amd._lib import lib
 dev = torch.device("cuda", 0)
 model = sys.argv[1] if len(sys.argv) > 1 else "diff"
 B = int(sys.argv[2]) if len(sys.argv) > 2 else 4096
 N = int(sys.argv[3]) if len(sys.argv) > 3 else 40
-f = bench.Fleet(model, B, N, bench.DEFAULT_SEED + 1, dev)
+f = Fleet(model, B, N, DEFAULT_SEED + 1, dev)
 for _ in range(30):
     f.tick()
 torch.cuda.synchronize()
@@ -53,7 +54,7 @@ assert L.nmpc_debug_stamps_p1(buf2) == 0
 s2 = np.frombuffer(buf2, dtype=np.uint64).reshape(256, 8).astype(np.int64)[:nw]
 ok = (s2[:, 7] > s2[:, 0]) & (s2[:, 0] > 0)
 d2 = np.diff(s2[ok], axis=1)
-names = ["update+resid", "adjoint+terminal..Gd", "lba", "mrow", "cholesky", "rhs+LR+carry", "store"]
+names = ["update+resid", "adjoint+terminal..Gd", "pg", "mrow", "cholesky", "rhs+LR+carry", "store"]
 print("P1 stage sub-phases (cycles, median over waves):", {n: int(np.median(d2[:, i])) for i, n in enumerate(names)}, "total", int(np.median(s2[ok, 7] - s2[ok, 0])))
 
 buf3 = (ctypes.c_ulonglong * (256 * 64))()
