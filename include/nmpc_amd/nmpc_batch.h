@@ -17,6 +17,8 @@
 #ifndef NMPC_AMD_NMPC_BATCH_H
 #define NMPC_AMD_NMPC_BATCH_H
 
+#include "nmpc_amd/nmpc_path.h"
+
 #ifdef __cplusplus
 extern "C" {
 #endif
@@ -99,6 +101,18 @@ int nmpc_batch_solve(nmpc_batch* b, int B, const float* x0, const float* yref, i
 int nmpc_batch_run(nmpc_batch* b, int B, const float* pose, const float* vel, const float* steer,
                    const float* traj, const int* traj_len, const unsigned char* reset, float* cmd, float* u0,
                    int* status, int* qp_iter, float* qp_res, void* stream);
+
+/* A path-following tick in one launch: PathDiscretizer::getNextNPoses (nmpc_path.h, PathDiscretizer.cpp:14-63)
+ * of every robot followed by nmpc_batch_run on those N+1 poses -- processFollowPath's discretize + run
+ * (NMPCNavControlROS.cpp:666-668 -> :713) without the trip of the poses through a second launch. The march
+ * runs in the solve kernel (fp64, the reference's operation order: the same poses as nmpc_path_discretize
+ * with num_poses = N+1, bit for bit). Arguments as nmpc_path_discretize and nmpc_batch_run; traj_out
+ * [N+1][3][B] receives the poses (NULL: not written). Every robot's reference has N+1 poses (padded with the
+ * path end). nseg [B] >= 1. */
+int nmpc_batch_run_path(nmpc_batch* b, int B, const float* pose, const float* vel, const float* steer,
+                        const nmpc_path_segment* segs, int seg_stride, const int* nseg, const double* nearest_u,
+                        double sample_period, int is_holonomic, const unsigned char* reset, float* traj_out,
+                        float* cmd, float* u0, int* status, int* qp_iter, float* qp_res, void* stream);
 
 /* Kernel variant: NMPC_KERNEL_TEAM (16-lane team per robot, DPP row exchange) is the only one; any other value
  * returns NMPC_ERR_UNSUPPORTED. (The round-1 one-lane-per-robot kernel was removed: its fp32 factor is not

@@ -134,6 +134,26 @@ class BatchSolver:
             _ptr(qp_iter, I32, (B,), "qp_iter"), _ptr(qp_res, F32, (3, B), "qp_res"), _stream(stream)),
             "nmpc_batch_run")
 
+    def run_path(self, pose, vel, segs, nseg, nearest_u, sample_period, is_holonomic=False, steer=None, reset=None,
+                 traj_out=None, cmd=None, u0=None, status=None, qp_iter=None, qp_res=None, stream=None):
+        """processFollowPath's getNextNPoses + run for B robots in one launch (nmpc_batch_run_path): segs
+        float64 [B][S][16] (the nmpc_path_segment layout, nmpc_nav_control_amd.path.pack_paths), nseg int32
+        [B], nearest_u float64 [B]; traj_out [N+1][3][B] receives the poses."""
+        B = pose.shape[1]
+        if not 0 <= B <= self.capacity:
+            raise ValueError(f"batch {B} exceeds the capacity {self.capacity}")
+        if segs.dim() != 3 or segs.shape[0] != B or segs.shape[2] != 16:
+            raise ValueError(f"segs: expected shape ({B}, S, 16), got {tuple(segs.shape)}")
+        check(lib().nmpc_batch_run_path(
+            self._h, B, _ptr(pose, F32, (3, B), "pose"), _ptr(vel, F32, (3, B), "vel"),
+            _ptr(steer, F32, (B,), "steer"), _ptr(segs, torch.float64, None, "segs"), segs.shape[1],
+            _ptr(nseg, I32, (B,), "nseg"), _ptr(nearest_u, torch.float64, (B,), "nearest_u"), float(sample_period),
+            1 if is_holonomic else 0, _ptr(reset, U8, (B,), "reset"),
+            _ptr(traj_out, F32, (self.N + 1, 3, B), "traj_out"), _ptr(cmd, F32, (3, B), "cmd"),
+            _ptr(u0, F32, (self.nu, B), "u0"), _ptr(status, I32, (B,), "status"),
+            _ptr(qp_iter, I32, (B,), "qp_iter"), _ptr(qp_res, F32, (3, B), "qp_res"), _stream(stream)),
+            "nmpc_batch_run_path")
+
     def fleet_sim_step(self, path, s, pose, vel, steer, u0, status, traj, traj_len, advance=True, stream=None):
         B = pose.shape[1]
         if not 0 <= B <= self.capacity:

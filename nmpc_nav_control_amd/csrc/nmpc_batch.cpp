@@ -389,6 +389,47 @@ int nmpc_batch_run(nmpc_batch* b, int B, const float* pose, const float* vel, co
     return hip_err(launch(b, a, kModeRun, (hipStream_t)stream), "run launch");
 }
 
+int nmpc_batch_run_path(nmpc_batch* b, int B, const float* pose, const float* vel, const float* steer,
+                        const nmpc_path_segment* segs, int seg_stride, const int* nseg, const double* nearest_u,
+                        double sample_period, int is_holonomic, const unsigned char* reset, float* traj_out,
+                        float* cmd, float* u0, int* status, int* qp_iter, float* qp_res, void* stream)
+{
+    if (!b) return set_err(NMPC_ERR_ARG, "batch is NULL");
+    if (B < 0 || B > b->capacity) return set_err(NMPC_ERR_ARG, "B out of range [0, capacity]");
+    if (B == 0) return NMPC_OK;
+    if (!pose || !vel || !segs || !nseg || !nearest_u)
+        return set_err(NMPC_ERR_ARG, "pose, vel, segs, nseg and nearest_u are required");
+    if (seg_stride < 1) return set_err(NMPC_ERR_ARG, "seg_stride < 1");
+    if (!(sample_period >= 0.0)) return set_err(NMPC_ERR_ARG, "sample_period must be >= 0");
+    if (16 * (sizeof(double) + 3 * sizeof(float)) * (size_t)(b->prm.N + 1) > 65536)
+        return set_err(NMPC_ERR_UNSUPPORTED, "horizon too long for the in-kernel path march");
+    KArgs a;
+    std::memset(&a, 0, sizeof(a));
+    a.B = B;
+    a.stride = b->capacity;
+    a.xbar = b->xbar;
+    a.ubar = b->ubar;
+    a.carried = b->carried;
+    a.scratch = b->scratch;
+    a.pose = pose;
+    a.vel = vel;
+    a.steer = steer;
+    a.segs = segs;
+    a.seg_stride = seg_stride;
+    a.nseg = nseg;
+    a.nearest_u = nearest_u;
+    a.period = sample_period;
+    a.holo = is_holonomic ? 1 : 0;
+    a.traj_out = traj_out;
+    a.reset = reset;
+    a.cmd = cmd;
+    a.u0 = u0;
+    a.status = status;
+    a.qp_iter = qp_iter;
+    a.qp_res = qp_res;
+    return hip_err(launch(b, a, kModeRun, (hipStream_t)stream), "run_path launch");
+}
+
 int nmpc_batch_set_kernel(nmpc_batch* b, int kernel)
 {
     if (!b) return set_err(NMPC_ERR_ARG, "batch is NULL");

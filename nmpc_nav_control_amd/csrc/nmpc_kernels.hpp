@@ -34,6 +34,13 @@ struct KArgs {
     const float* traj;   // [N+1][3][B]
     const int* traj_len; // [B] or nullptr (= N+1)
     const unsigned char* reset;  // [B] or nullptr
+    // run mode from parametric paths (nmpc_batch_run_path): getNextNPoses in the kernel instead of traj
+    const nmpc_path_segment* segs;  // [B][seg_stride] or nullptr
+    int seg_stride, holo;
+    const int* nseg;                // [B]
+    const double* nearest_u;        // [B]
+    double period;
+    float* traj_out;                // [N+1][3][B] or nullptr: the poses the march produced
     // outputs (each may be nullptr)
     float* u0;     // [NU][B]
     float* x1;     // [NX][B]

@@ -25,6 +25,7 @@
 #include "nmpc_kernels.hpp"
 #include "team_asm_gen.hpp"
 #include "team_dpp.hpp"
+#include "path_march.hpp"
 
 namespace nmpc {
 
@@ -350,6 +351,38 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
         __threadfence_block();
     }
 
+    // ---- path-following tick (nmpc_batch_run_path): getNextNPoses in-kernel ------------------------------
+    // Lane 0 of the team marches the robot's path (PathDiscretizer.cpp:14-63, path_march.hpp, fp64 without
+    // contraction: bit-identical poses to k_path_discretize) and records the path parameter of each pose in the
+    // team's LDS slice; the rest is padded with the path end (:58-63). The team's 16 lanes then evaluate the
+    // poses 16 at a time (atan2 and all), so no lane waits in a divergent emit. A team's lanes share the wave
+    // and LDS accesses of a wave retire in order, so P0 reads the poses from LDS directly afterwards.
+    extern __shared__ double s_path[];  // path mode: [16 teams][N+1] parameters, then [16][N+1][3] float poses
+    const bool path = (mode == kModeRun) && a.segs;
+    const int tslot = threadIdx.x >> 4;
+    float* const my_traj = reinterpret_cast<float*>(s_path + 16 * (N + 1)) + (size_t)tslot * (N + 1) * 3;
+    if (path) {
+        double* const my_u = s_path + (size_t)tslot * (N + 1);
+        const nmpc_path_segment* S = a.segs + (size_t)inst * a.seg_stride;
+        const int n = a.nseg[inst];
+        if (r == 0) {
+            const int cnt = path_march(S, n, a.nearest_u[inst], a.period, N + 1, [&](int j, double su) { my_u[j] = su; });
+            for (int j = cnt; j <= N; j++) my_u[j] = (double)n;
+        }
+        for (int j = r; j <= N; j += 16) {
+            double px, py, pt;
+            path_pose(S, n, my_u[j], a.holo, &px, &py, &pt);
+            my_traj[j * 3 + 0] = (float)px;
+            my_traj[j * 3 + 1] = (float)py;
+            my_traj[j * 3 + 2] = (float)pt;
+            if (a.traj_out) {
+                a.traj_out[((size_t)j * 3 + 0) * Bn + inst] = (float)px;
+                a.traj_out[((size_t)j * 3 + 1) * Bn + inst] = (float)py;
+                a.traj_out[((size_t)j * 3 + 2) * Bn + inst] = (float)pt;
+            }
+        }
+    }
+
     // ---- x0 (every lane keeps the full vector) ----------------------------------------------------------
     float x0[NX];
     float pose_th = 0.0f;
@@ -378,7 +411,7 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
     if (is_x) we_lane = (mode != kModeRun && a.We) ? a.We[(size_t)xi * Bn + inst] : P.We[xi];
 
     // ---- P0: linearisation (lane v: nominal step + column v), gradient, bounds, feasible initial iterate --
-    const int len = (mode == kModeRun) ? (a.traj_len ? a.traj_len[inst] : N + 1) : 0;
+    const int len = (mode == kModeRun) ? ((a.traj_len && !path) ? a.traj_len[inst] : N + 1) : 0;
     float ref_x = 0.0f, ref_y = 0.0f, ref_t = pose_th, prv_x = 0.0f, prv_y = 0.0f, prv_t = 0.0f;
     // Iterate rows are read two stages ahead (every lane of a team reads the same addresses: one request per
     // wave), the reference row likewise.
@@ -392,7 +425,7 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
         if (mode == kModeRun) {
             const int kt = kk < len ? kk : (len > 0 ? len - 1 : 0);
 #pragma unroll
-            for (int j = 0; j < 3; j++) tr[j] = a.traj[((size_t)kt * 3 + j) * Bn + inst];
+            for (int j = 0; j < 3; j++) tr[j] = path ? my_traj[kt * 3 + j] : a.traj[((size_t)kt * 3 + j) * Bn + inst];
         } else {
             tr[0] = tr[1] = tr[2] = 0.0f;
         }
@@ -989,10 +1022,14 @@ hipError_t launch_sqp_rti_team(const KParams& P, const KArgs& a, int mode, hipSt
     const int block = 256;  // 16 teams
     const long long threads = (long long)a.B * 16;
     const int grid = (int)((threads + block - 1) / block);
+    // path mode: each team's N+1 path parameters and reference poses in LDS (16 teams x (N+1) x (8 + 12) B,
+    // 26 KB at N = 80)
+    const size_t lds = (mode == kModeRun && a.segs) ? (sizeof(double) + 3 * sizeof(float)) * 16 * (size_t)(P.N + 1) : 0;
+    if (lds > 65536) return hipErrorInvalidValue;
     if (a.dense)
-        hipLaunchKernelGGL((k_sqp_rti_team<M, true>), dim3(grid), dim3(block), 0, stream, P, a, mode);
+        hipLaunchKernelGGL((k_sqp_rti_team<M, true>), dim3(grid), dim3(block), lds, stream, P, a, mode);
     else
-        hipLaunchKernelGGL((k_sqp_rti_team<M, false>), dim3(grid), dim3(block), 0, stream, P, a, mode);
+        hipLaunchKernelGGL((k_sqp_rti_team<M, false>), dim3(grid), dim3(block), lds, stream, P, a, mode);
     return hipGetLastError();
 }
 

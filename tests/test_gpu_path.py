@@ -125,3 +125,39 @@ def test_follow_path_tick_on_device_matches_oracle(built):
         assert st == 0
         err = max(err, np.abs(u0[i] - ub[0]).max())
     assert err <= 1e-3, err
+
+
+@pytest.mark.parametrize("holo", [False, True])
+def test_run_path_one_launch_equals_two_launches(built, holo):
+    """nmpc_batch_run_path (getNextNPoses in the solve kernel: a path-following tick in one launch,
+    NMPCNavControlROS.cpp:666-668 -> :713) against nmpc_path_discretize followed by nmpc_batch_run: the poses
+    are bit-identical (both fp64 marches without contraction, path_march.hpp) and so is every output of the
+    solve; over three ticks of warm-started solves."""
+    N, B = 40, 1000
+    rng = np.random.default_rng(5)
+    segs, nseg, nu = random_paths(B, seed=5, max_segs=4, reverse_frac=0.2)
+    nu[:] = rng.uniform(0, 0.3, B)
+    exp_traj, _ = path_discretize(segs, nseg, nu, 1 / 40, N + 1, holo)
+    pose = exp_traj[:, 0, :].copy()
+    pose[:, :2] += rng.uniform(-0.1, 0.1, (B, 2))
+    pose[:, 2] += rng.uniform(-0.2, 0.2, B)
+    vel = np.zeros((B, 3))
+    vel[:, 0] = rng.uniform(0.0, 0.5, B)
+    d = lambda a, dt=torch.float32: torch.from_numpy(np.ascontiguousarray(a)).to(DEV, dt)  # noqa: E731
+    P, V = d(pose.T), d(vel.T)
+    S, NS, NU = d(segs, torch.float64), d(nseg, torch.int32), d(nu, torch.float64)
+    two, one = BatchSolver("diff", N, B, device=DEV), BatchSolver("diff", N, B, device=DEV)
+    out = {k: [torch.zeros(r, B, device=DEV) for _ in range(2)] for k, r in (("u0", 2), ("cmd", 3))}
+    st = [torch.zeros(B, dtype=torch.int32, device=DEV) for _ in range(2)]
+    it = [torch.zeros(B, dtype=torch.int32, device=DEV) for _ in range(2)]
+    traj_out = torch.zeros(N + 1, 3, B, device=DEV)
+    for tick in range(3):
+        traj = discretize(S, NS, NU, 1 / 40, N + 1, holo)
+        two.run(P, V, traj, cmd=out["cmd"][0], u0=out["u0"][0], status=st[0], qp_iter=it[0])
+        one.run_path(P, V, S, NS, NU, 1 / 40, holo, traj_out=traj_out, cmd=out["cmd"][1], u0=out["u0"][1],
+                     status=st[1], qp_iter=it[1])
+        torch.cuda.synchronize()
+        assert torch.equal(traj_out, traj), tick
+        for k in ("u0", "cmd"):
+            assert torch.equal(out[k][0], out[k][1]), (tick, k)
+        assert torch.equal(st[0], st[1]) and torch.equal(it[0], it[1]) and (st[0] == 0).all(), tick

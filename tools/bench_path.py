@@ -3,7 +3,10 @@
 (lines and cubic Beziers, 1-4 segments per robot), N+1 = 41 poses per robot at dt = 1/40 s, inputs resident in
 HBM. Prints one JSON line: robots/s, ms per launch (HIP events on the launch stream), bytes moved per launch.
 
-usage: python tools/bench_path.py [--B 4096] [--num-poses 41] [--iters 50]
+With --tick: a whole path-following tick of diff robots (N = num_poses - 1), the two-launch form
+(nmpc_path_discretize + nmpc_batch_run) against the one-launch nmpc_batch_run_path, ms per tick each.
+
+usage: python tools/bench_path.py [--B 4096] [--num-poses 41] [--iters 50] [--tick]
 """
 import argparse
 import json
@@ -47,7 +50,10 @@ def main(argv=None):
     ap.add_argument("--B", type=int, default=4096)
     ap.add_argument("--num-poses", type=int, default=41)
     ap.add_argument("--iters", type=int, default=50)
+    ap.add_argument("--tick", action="store_true")
     a = ap.parse_args(argv)
+    if a.tick:
+        return tick(a)
     dev = torch.device("cuda:0")
     segs, nseg, nu = seeded_paths(a.B)
     S, NS, U = (torch.from_numpy(x).to(dev) for x in (segs, nseg, nu))
@@ -69,6 +75,45 @@ def main(argv=None):
                           num_poses=a.num_poses, ms_per_launch=round(ms, 4), bytes_per_launch=nbytes,
                           achieved_GBs=round(nbytes / (ms * 1e-3) / 1e9, 2),
                           bound="latency (sequential fp64 march per robot)")), flush=True)
+
+
+def tick(a):
+    """Path-following tick: discretize + run (two launches) vs run_path (one launch), same robots and state.
+    Each variant runs its own solver handle through `iters` warm-started ticks on fixed measurements."""
+    from nmpc_nav_control_amd.batch import BatchSolver
+    from nmpc_nav_control_amd.path import discretize as disc
+    dev = torch.device("cuda:0")
+    N, B = a.num_poses - 1, a.B
+    segs, nseg, nu = seeded_paths(B)
+    S, NS, U = (torch.from_numpy(x).to(dev) for x in (segs, nseg, nu))
+    traj = torch.empty((N + 1, 3, B), dtype=torch.float32, device=dev)
+    disc(S, NS, U, 1 / 40, N + 1, traj=traj)
+    pose = traj[0].clone()
+    vel = torch.zeros(3, B, device=dev)
+    res = {}
+    for name in ("two_launch", "one_launch"):
+        s = BatchSolver("diff", N, B, device=dev)
+        u0 = torch.zeros(2, B, device=dev)
+        st = torch.zeros(B, dtype=torch.int32, device=dev)
+
+        def step():
+            if name == "two_launch":
+                disc(S, NS, U, 1 / 40, N + 1, traj=traj)
+                s.run(pose, vel, traj, u0=u0, status=st)
+            else:
+                s.run_path(pose, vel, S, NS, U, 1 / 40, traj_out=None, u0=u0, status=st)
+        for _ in range(5):
+            step()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(a.iters):
+            step()
+        e1.record()
+        torch.cuda.synchronize()
+        res[name] = round(e0.elapsed_time(e1) / a.iters, 4)
+        res[name + "_failed"] = int((st != 0).sum())
+    print(json.dumps(dict(metric="path-following tick ms (diff N=%d, B=%d)" % (N, B), **res)), flush=True)
 
 
 if __name__ == "__main__":
