@@ -31,11 +31,15 @@ from nmpc_nav_control_amd.sharding import TimedRegion, world_info  # noqa: E402
 
 # BASELINE.json configs (index -> seed offset 20250824 + idx)
 CONFIGS = {
-    "metric": dict(idx=1, models=[("diff", 4096)], N=40, desc="diff2amr N=40 batch=4096 per GPU"),
+    # groups: stream groups per model (FleetNode), decoupled closed loops on their own HIP streams; chosen per
+    # config from same-box A/B runs (profiles/r02/ab/groups.txt): metric 2.96 -> 3.00 M it/s with 2 groups
+    # (3 or more lose), tric 1.91 -> 2.28 M with 2, omni4 and diff1024 lose or tie with more than one
+    "metric": dict(idx=1, models=[("diff", 4096)], N=40, groups=2, desc="diff2amr N=40 batch=4096 per GPU"),
     "diff1024": dict(idx=1, models=[("diff", 1024)], N=40, desc="diff2amr N=40 batch=1024"),
     "omni4": dict(idx=2, models=[("omni4", 4096)], N=40, desc="omni4amr (11x4) N=40 batch=4096"),
-    "tric": dict(idx=3, models=[("tric", 8192)], N=60, desc="tric3amr N=60 batch=8192, alpha bounds active"),
-    # whole fleet: 65536 robots over 8 GPUs -> 8192 per GPU, a third of each model
+    "tric": dict(idx=3, models=[("tric", 8192)], N=60, groups=2, desc="tric3amr N=60 batch=8192, alpha bounds active"),
+    # whole fleet: 65536 robots over 8 GPUs -> 8192 per GPU, a third of each model; the three models' streams run
+    # decoupled at N=1 (2.94 -> 3.71 M it/s against a fleet-wide tick boundary) and joined under --gather
     "mixed": dict(idx=4, models=[("diff", 2731), ("omni4", 2731), ("tric", 2730)], N=40,
                   desc="mixed fleet diff+omni4+tric, 8192 per GPU (65536 on 8 GPUs)"),
 }
@@ -81,13 +85,16 @@ def valu_peaks():
     return FP32_PEAK_TFLOPS, fp64
 
 
-def roofline(fleets, node, kernel_ms, steps):
+def roofline(fleets, node, kernel_ms, steps, step_s=None):
     """Roofline record of the solve kernel(s) of one step: algorithmic flops, split into the fp32
     part and the fp64 Riccati factorisation, each priced at its own VALU peak; frac = the share of the VALU
     time budget of the timed launches that the algorithmic flops would need at peak. The PMC-side figures
     (L2<->fabric traffic, VALU issue share of the wave cycles) come from the rocprofv3 --pmc passes of the
     same config (tools/pmc.sh -> tools/pmc_summary.py -> profiles/<round>/pmc/pmc_<config>.json)."""
-    t_k = float(np.mean(kernel_ms)) * 1e-3
+    t_launch = float(np.mean(kernel_ms)) * 1e-3
+    # decoupled stream groups: the launches of a step overlap each other, so the rate is the step's flops over
+    # the step's share of the timed region (conservative: it includes the plant steps and any idle gaps)
+    t_k = step_s if node.decoupled else t_launch
     f32 = f64 = 0.0
     cbytes = 0
     for j, f in enumerate(fleets):
@@ -101,9 +108,14 @@ def roofline(fleets, node, kernel_ms, steps):
     a32, a64 = f32 / t_k / 1e12, f64 / t_k / 1e12
     frac = a32 / p32 + a64 / p64
     achieved = a32 + a64
-    cfg = "+".join(f"{f.model}_N{f.N}_B{f.B}" for f in fleets)
+    per_model = {}
+    for f in fleets:
+        per_model[(f.model, f.N)] = per_model.get((f.model, f.N), 0) + f.B
+    cfg = "+".join(f"{m}_N{n}_B{b}" for (m, n), b in per_model.items()) + (f"_g{node.groups}" if node.groups > 1 else "")
     pmc, src = _profile_json(f"pmc/pmc_{cfg}.json")
     traffic = pmc.get("l2_fabric_bytes_per_launch") if pmc else None
+    if traffic is not None and node.groups > 1:
+        traffic *= node.groups  # the PMC record averages one dispatch per kernel name; a step runs `groups` of each
     return {"bound": "valu", "achieved": round(achieved, 4), "peak": round(achieved / frac, 2), "unit": "TFLOP/s",
             "frac": round(frac, 6), "traffic": traffic,
             "fp32": {"flop_per_launch": f32, "achieved_tflops": round(a32, 4), "peak_tflops": p32,
@@ -115,10 +127,14 @@ def roofline(fleets, node, kernel_ms, steps):
                                                "active_frac", "source_commit")} if pmc else None),
             "traffic_source": src, "kernel": f"k_sqp_rti_{fleets[0].solver.kernel}" +
             (f" x{len(fleets)} concurrent streams" if len(fleets) > 1 else ""),
-            "kernel_ms_mean": round(t_k * 1e3, 4), "timing": "HIP events on the launch stream(s), timed region",
+            "kernel_ms_mean": round(t_launch * 1e3, 4),
+            "timing": ("HIP events per launch on its stream; achieved = the step's flops / (timed region / steps), "
+                       "the launches of %d decoupled streams overlapping" % len(fleets)) if node.decoupled else
+                      "HIP events on the launch stream(s), timed region",
             "compulsory_bytes_per_launch": cbytes, "achieved_compulsory_GBs": round(cbytes / t_k / 1e9, 2),
             "note": "VALU-bound, latency-limited: <=15x15 per-robot blocks, no GEMM-shaped work (no MFMA); "
-                    "traffic = 2*FETCH_SIZE + WRITE_SIZE (L2<->fabric incl. Infinity-Cache hits) per launch"}
+                    "traffic = 2*FETCH_SIZE + WRITE_SIZE (L2<->fabric incl. Infinity-Cache hits) per step (the sum "
+                    "over the step's launches: one per model and stream group)"}
 
 
 def bytes_per_instance(model, N):
@@ -178,6 +194,10 @@ def main():
     ap.add_argument("--cpu-ticks", type=int, default=8)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--gather", action="store_true", help="all-gather u0+status to rank 0 every tick (RCCL)")
+    ap.add_argument("--groups", type=int, default=None,
+                    help="stream groups per model (default: the config's); each is a Fleet on its own HIP stream")
+    ap.add_argument("--joined", action="store_true",
+                    help="fleet-wide tick boundary across streams (default: decoupled streams unless --gather)")
     args = ap.parse_args()
 
     rank, world, local_rank = world_info()
@@ -190,7 +210,9 @@ def main():
     gather = args.gather or (args.config == "mixed" and world > 1)
     # weak scaling: the global fleet holds B x world robots of each model; this rank owns the contiguous
     # shard [rank*B, (rank+1)*B) of it (sharding.shard_range), no collective on the solve path
-    node = FleetNode(cfg["models"], cfg["N"], DEFAULT_SEED + cfg["idx"], dev, rank=rank, world=world, gather=gather)
+    groups = cfg.get("groups", 1) if args.groups is None else args.groups
+    node = FleetNode(cfg["models"], cfg["N"], DEFAULT_SEED + cfg["idx"], dev, rank=rank, world=world, gather=gather,
+                     groups=groups, decoupled=False if args.joined else None)
     fleets = node.fleets
     torch.cuda.synchronize()
 
@@ -200,19 +222,27 @@ def main():
     node.reset_stats()
     torch.cuda.synchronize()
 
-    # per-kernel timing of the solve launches with HIP events on the launch streams: a single model's solve
-    # runs on the current stream; a mixed node's three solves run concurrently on their own streams, timed
-    # from one start event on the main stream to each stream's end-of-solve event (the region = the latest)
+    # per-launch timing of the solve kernels with HIP events on their launch streams. One stream: the solve's
+    # duration. Joined streams: from one start event on the main stream to each stream's end-of-solve event
+    # (the region = the latest). Decoupled streams: each launch from its own stream's start event.
     main_stream = torch.cuda.current_stream()
-    ev = [(torch.cuda.Event(enable_timing=True), [torch.cuda.Event(enable_timing=True) for _ in fleets])
-          for _ in range(args.steps)]
+    T = lambda: torch.cuda.Event(enable_timing=True)  # noqa: E731
+    ev = [([T() for _ in fleets], [T() for _ in fleets]) for _ in range(args.steps)]
 
     with TimedRegion(dev) as region:
         for k in range(args.steps):
-            ev[k][0].record(main_stream)
+            if node.decoupled:
+                for j, f in enumerate(fleets):
+                    ev[k][0][j].record(f.stream)
+                    f.solve()
+                    ev[k][1][j].record(f.stream)
+                    f.advance()
+                    node.accumulate_one(j)
+                continue
+            ev[k][0][0].record(main_stream)
             if node.multi:
                 for f in fleets:
-                    f.stream.wait_event(ev[k][0])
+                    f.stream.wait_event(ev[k][0][0])
             for j, f in enumerate(fleets):
                 f.solve()
                 ev[k][1][j].record(f.stream if f.stream is not None else main_stream)
@@ -226,7 +256,11 @@ def main():
                 node.gather_commands()
     elapsed = region.elapsed
 
-    kernel_ms = [max(ev[k][0].elapsed_time(e) for e in ev[k][1]) for k in range(args.steps)]
+    if node.decoupled:  # mean launch duration, and the launches' share of the timed region per step
+        kernel_ms = [float(np.mean([ev[k][0][j].elapsed_time(ev[k][1][j]) for j in range(len(fleets))]))
+                     for k in range(args.steps)]
+    else:
+        kernel_ms = [max(ev[k][0][0].elapsed_time(e) for e in ev[k][1]) for k in range(args.steps)]
     B_rank = node.B
     k_mean = float(node.iters_sum.sum().item()) / (B_rank * args.steps)
     units = args.steps * B_rank * world
@@ -234,7 +268,7 @@ def main():
 
     result = None
     if rank == 0:
-        roof = roofline(fleets, node, kernel_ms, args.steps)
+        roof = roofline(fleets, node, kernel_ms, args.steps, step_s=elapsed / args.steps)
         cpu = None
         u0_err = None
         if not args.no_cpu_baseline and world == 1:

@@ -57,31 +57,41 @@ namespace {
 
 std::mutex g_mu;
 
-// Device engine per (model, N): one batch handle plus staging buffers.
+// Device engine per (model, N): one batch handle plus one input and one output staging block. A call with n
+// capsules packs its inputs densely ([row][n] per array) into the pinned input block, which goes to the device in
+// ONE copy; the kernel's outputs sit in one device block that comes back in ONE copy. Every copy is async on the
+// launch stream and the call synchronises once (a single robot's solve: 12 synchronous copies -> 2 + 2 on-device).
+struct Blocks {  // float offsets of the arrays inside the blocks for n capsules
+    size_t x0, We, yref, xb, ub, in_floats;     // input block
+    size_t oxb, oub, ores, ost, oit, out_words;  // output block (status / qp_iter are int32 words)
+    Blocks(int n, int N, int nx, int nu, int ny)
+    {
+        x0 = 0;
+        We = x0 + (size_t)nx * n;
+        yref = We + (size_t)nx * n;
+        xb = yref + (size_t)(N + 1) * ny * n;
+        ub = xb + (size_t)(N + 1) * nx * n;
+        in_floats = ub + (size_t)N * nu * n;
+        oxb = 0;
+        oub = oxb + (size_t)(N + 1) * nx * n;
+        ores = oub + (size_t)N * nu * n;
+        ost = ores + (size_t)3 * n;
+        oit = ost + (size_t)n;
+        out_words = oit + (size_t)n;
+    }
+};
 struct Engine {
     nmpc_batch* batch = nullptr;
     int cap = 0;
-    float *x0 = nullptr, *yref = nullptr, *We = nullptr, *xtraj = nullptr, *utraj = nullptr;
-    int *status = nullptr, *qp_iter = nullptr;
-    float* qp_res = nullptr;  // [3][cap]: stationarity, bound residual, mu at IPM exit
-    // pinned host staging of the same shapes ([row][n] dense): no per-call allocation, DMA-able copies
-    float *h_x0 = nullptr, *h_yref = nullptr, *h_We = nullptr, *h_xb = nullptr, *h_ub = nullptr;
-    int *h_status = nullptr, *h_qp_iter = nullptr;
-    float* h_qp_res = nullptr;
+    float *din = nullptr, *dout = nullptr;  // device blocks, sized for cap capsules
+    float *hin = nullptr, *hout = nullptr;  // pinned host blocks of the same size
     ~Engine() { release(); }
     void release()
     {
         nmpc_batch_destroy(batch);
         batch = nullptr;
-        (void)hipFree(x0); (void)hipFree(yref); (void)hipFree(We); (void)hipFree(xtraj); (void)hipFree(utraj);
-        (void)hipFree(status); (void)hipFree(qp_iter); (void)hipFree(qp_res); (void)hipHostFree(h_qp_res);
-        qp_res = h_qp_res = nullptr;
-        (void)hipHostFree(h_x0); (void)hipHostFree(h_yref); (void)hipHostFree(h_We); (void)hipHostFree(h_xb);
-        (void)hipHostFree(h_ub); (void)hipHostFree(h_status); (void)hipHostFree(h_qp_iter);
-        x0 = yref = We = xtraj = utraj = nullptr;
-        status = qp_iter = nullptr;
-        h_x0 = h_yref = h_We = h_xb = h_ub = nullptr;
-        h_status = h_qp_iter = nullptr;
+        (void)hipFree(din); (void)hipFree(dout); (void)hipHostFree(hin); (void)hipHostFree(hout);
+        din = dout = hin = hout = nullptr;
         cap = 0;
     }
 };
@@ -306,22 +316,12 @@ int ensure_engine(Engine& e, const nmpc_model_params& prm, int n, std::string& w
     const int N = prm.N;
     if (nmpc_batch_create(&prm, cap, &e.batch) != NMPC_OK) { why = nmpc_last_error(); return -1; }
     hipError_t r = hipSuccess;
-    if ((r = hipMalloc(&e.x0, sizeof(float) * nx * cap)) != hipSuccess ||
-        (r = hipMalloc(&e.yref, sizeof(float) * (N + 1) * ny * cap)) != hipSuccess ||
-        (r = hipMalloc(&e.We, sizeof(float) * nx * cap)) != hipSuccess ||
-        (r = hipMalloc(&e.xtraj, sizeof(float) * (N + 1) * nx * cap)) != hipSuccess ||
-        (r = hipMalloc(&e.utraj, sizeof(float) * N * nu * cap)) != hipSuccess ||
-        (r = hipMalloc(&e.status, sizeof(int) * cap)) != hipSuccess ||
-        (r = hipMalloc(&e.qp_iter, sizeof(int) * cap)) != hipSuccess ||
-        (r = hipMalloc(&e.qp_res, sizeof(float) * 3 * cap)) != hipSuccess ||
-        (r = hipHostMalloc(&e.h_qp_res, sizeof(float) * 3 * cap)) != hipSuccess ||
-        (r = hipHostMalloc(&e.h_x0, sizeof(float) * nx * cap)) != hipSuccess ||
-        (r = hipHostMalloc(&e.h_yref, sizeof(float) * (N + 1) * ny * cap)) != hipSuccess ||
-        (r = hipHostMalloc(&e.h_We, sizeof(float) * nx * cap)) != hipSuccess ||
-        (r = hipHostMalloc(&e.h_xb, sizeof(float) * (N + 1) * nx * cap)) != hipSuccess ||
-        (r = hipHostMalloc(&e.h_ub, sizeof(float) * N * nu * cap)) != hipSuccess ||
-        (r = hipHostMalloc(&e.h_status, sizeof(int) * cap)) != hipSuccess ||
-        (r = hipHostMalloc(&e.h_qp_iter, sizeof(int) * cap)) != hipSuccess) {
+    const Blocks bl(cap, N, nx, nu, ny);
+    static_assert(sizeof(int) == sizeof(float), "int32 words in the float output block");
+    if ((r = hipMalloc(&e.din, sizeof(float) * bl.in_floats)) != hipSuccess ||
+        (r = hipMalloc(&e.dout, sizeof(float) * bl.out_words)) != hipSuccess ||
+        (r = hipHostMalloc(&e.hin, sizeof(float) * bl.in_floats)) != hipSuccess ||
+        (r = hipHostMalloc(&e.hout, sizeof(float) * bl.out_words)) != hipSuccess) {
         why = hipGetErrorString(r);
         e.release();
         return -1;
@@ -347,9 +347,9 @@ void solve_group(std::vector<nmpc_capsule_impl*>& cs, std::vector<Packed>& ps, c
     if (ensure_engine(e, ps[idx[0]].prm, n, why)) return fail_all(why);
     const auto ta = std::chrono::steady_clock::now();
     const int S = e.cap;
-    float *hx0 = e.h_x0, *hyref = e.h_yref, *hWe = e.h_We, *hxb = e.h_xb, *hub = e.h_ub;
-    const size_t n_x0 = (size_t)nx * n, n_yref = (size_t)(N + 1) * ny * n, n_xb = (size_t)(N + 1) * nx * n,
-                 n_ub = (size_t)N * nu * n;
+    const Blocks bl(n, N, nx, nu, ny);
+    float *hx0 = e.hin + bl.x0, *hyref = e.hin + bl.yref, *hWe = e.hin + bl.We, *hxb = e.hin + bl.xb,
+          *hub = e.hin + bl.ub;
     {
         std::vector<const double*> x0s(n), yrefs(n), Wes(n), xbs(n), ubs(n);
         for (int q = 0; q < n; q++) {
@@ -369,31 +369,31 @@ void solve_group(std::vector<nmpc_capsule_impl*>& cs, std::vector<Packed>& ps, c
     const auto tb = std::chrono::steady_clock::now();
     float *dxb, *dub;
     nmpc_batch_state(e.batch, &dxb, &dub, nullptr, nullptr);
-    // the iterate goes to the dense [row][n] output buffers first (contiguous host->device copies), then into
-    // the [row][S] resident state by one device-side 2-D copy (a pitched copy from pageable host memory runs
-    // row by row); the solve overwrites the output buffers afterwards, in stream order
+    // one host->device copy of the input block; the iterate then moves from its dense [row][n] rows into the
+    // [row][S] resident state by device-side 2-D copies (stream order: the solve's outputs overwrite nothing
+    // these copies still read, since the output block is separate)
     hipError_t r = hipSuccess;
-    if ((r = hipMemcpy(e.x0, hx0, sizeof(float) * n_x0, hipMemcpyHostToDevice)) != hipSuccess ||
-        (r = hipMemcpy(e.yref, hyref, sizeof(float) * n_yref, hipMemcpyHostToDevice)) != hipSuccess ||
-        (r = hipMemcpy(e.We, hWe, sizeof(float) * n_x0, hipMemcpyHostToDevice)) != hipSuccess ||
-        (r = hipMemcpy(e.xtraj, hxb, sizeof(float) * n_xb, hipMemcpyHostToDevice)) != hipSuccess ||
-        (r = hipMemcpy(e.utraj, hub, sizeof(float) * n_ub, hipMemcpyHostToDevice)) != hipSuccess ||
-        (r = hipMemcpy2D(dxb, sizeof(float) * S, e.xtraj, sizeof(float) * n, sizeof(float) * n, (size_t)(N + 1) * nx,
-                         hipMemcpyDeviceToDevice)) != hipSuccess ||
-        (r = hipMemcpy2D(dub, sizeof(float) * S, e.utraj, sizeof(float) * n, sizeof(float) * n, (size_t)N * nu,
-                         hipMemcpyDeviceToDevice)) != hipSuccess)
+    const hipStream_t st = nullptr;
+    float* const dout = e.dout;
+    if ((r = hipMemcpyAsync(e.din, e.hin, sizeof(float) * bl.in_floats, hipMemcpyHostToDevice, st)) != hipSuccess ||
+        (r = hipMemcpy2DAsync(dxb, sizeof(float) * S, e.din + bl.xb, sizeof(float) * n, sizeof(float) * n,
+                              (size_t)(N + 1) * nx, hipMemcpyDeviceToDevice, st)) != hipSuccess ||
+        (r = hipMemcpy2DAsync(dub, sizeof(float) * S, e.din + bl.ub, sizeof(float) * n, sizeof(float) * n,
+                              (size_t)N * nu, hipMemcpyDeviceToDevice, st)) != hipSuccess)
         return fail_all(hipGetErrorString(r));
     const auto t1 = std::chrono::steady_clock::now();
-    if (nmpc_batch_solve(e.batch, n, e.x0, e.yref, ny, e.We, nullptr, nullptr, nullptr, e.xtraj, e.utraj, e.status,
-                         e.qp_iter, e.qp_res, nullptr) != NMPC_OK)
+    if (nmpc_batch_solve(e.batch, n, e.din + bl.x0, e.din + bl.yref, ny, e.din + bl.We, nullptr, nullptr, nullptr,
+                         dout + bl.oxb, dout + bl.oub, reinterpret_cast<int*>(dout + bl.ost),
+                         reinterpret_cast<int*>(dout + bl.oit), dout + bl.ores, st) != NMPC_OK)
         return fail_all(nmpc_last_error());
-    int *hst = e.h_status, *hit = e.h_qp_iter;
-    if ((r = hipMemcpy(hxb, e.xtraj, sizeof(float) * n_xb, hipMemcpyDeviceToHost)) != hipSuccess ||
-        (r = hipMemcpy(hub, e.utraj, sizeof(float) * n_ub, hipMemcpyDeviceToHost)) != hipSuccess ||
-        (r = hipMemcpy(hst, e.status, sizeof(int) * n, hipMemcpyDeviceToHost)) != hipSuccess ||
-        (r = hipMemcpy(hit, e.qp_iter, sizeof(int) * n, hipMemcpyDeviceToHost)) != hipSuccess ||
-        (r = hipMemcpy(e.h_qp_res, e.qp_res, sizeof(float) * n, hipMemcpyDeviceToHost)) != hipSuccess)
+    if ((r = hipMemcpyAsync(e.hout, dout, sizeof(float) * bl.out_words, hipMemcpyDeviceToHost, st)) != hipSuccess ||
+        (r = hipStreamSynchronize(st)) != hipSuccess)
         return fail_all(hipGetErrorString(r));
+    const float* const hres = e.hout + bl.ores;
+    const int* const hst = reinterpret_cast<const int*>(e.hout + bl.ost);
+    const int* const hit = reinterpret_cast<const int*>(e.hout + bl.oit);
+    hxb = e.hout + bl.oxb;
+    hub = e.hout + bl.oub;
     const auto t2 = std::chrono::steady_clock::now();
     const double tt = std::chrono::duration<double>(t2 - t0).count();
     const double tq = std::chrono::duration<double>(t2 - t1).count();
@@ -407,7 +407,7 @@ void solve_group(std::vector<nmpc_capsule_impl*>& cs, std::vector<Packed>& ps, c
         nmpc_capsule_impl* c = cs[idx[q]];
         c->status = hst[q];
         c->qp_iter = hit[q];
-        c->out.inf_norm_res = e.h_qp_res[q];  // row 0 of qp_res: max |QP stationarity residual| at IPM exit
+        c->out.inf_norm_res = hres[q];  // row 0 of qp_res: max |QP stationarity residual| at IPM exit
         c->sqp_iter = 1;
         c->out.sqp_iter = 1;
         c->time_tot = tt;

@@ -83,22 +83,42 @@ class FleetNode:
     """Every model's fleet of one rank (weak scaling: rank r owns robots [r*B, (r+1)*B) of each model's
     seeded global fleet, sharding.shard_range), ticked together.
 
-    models: [(model, B_per_rank), ...]; a node with several models runs their launches concurrently, one HIP
-    stream each, joined on the caller's stream (each launch alone leaves SIMDs idle: ~2730 robots = 683
-    waves on 1024 SIMDs), with interleaved team placement (nmpc_batch.h NMPC_SCHED_INTERLEAVED)."""
+    models: [(model, B_per_rank), ...]. Each model's robots may be split further into ``groups`` contiguous
+    stream groups (Fleet objects with their own HIP stream and handle; make_fleet(start=...) keeps every
+    robot's data a function of its global index, so the robots are the same for any grouping).
 
-    def __init__(self, models, N, seed, dev, rank=0, world=1, gather=False, solver_factory=None):
+    Launches on several streams (several models, or groups > 1) run concurrently. ``decoupled`` picks how the
+    streams advance:
+      * joined (False): every tick starts after the previous tick of every stream ended (one fleet-wide tick
+        boundary per step; required by the per-tick command all-gather);
+      * decoupled (True): each stream runs its own closed loop (solve -> plant/reference step -> statistics)
+        with no cross-stream wait; the step boundary is only a count. A solve launch ends with its slowest
+        wave (its hardest robot: up to 19 IPM iterations against a mean of 7), and while it drains, the SIMDs
+        its finished waves freed run the next launches of the other streams.
+    With one stream (a single model, groups = 1) both are the same sequential loop."""
+
+    def __init__(self, models, N, seed, dev, rank=0, world=1, gather=False, solver_factory=None, groups=1,
+                 decoupled=None, schedule=None):
         self.dev = torch.device(dev)
         self.rank, self.world = rank, world
-        self.multi = len(models) > 1
         cuda = self.dev.type == "cuda"
+        self.groups = max(1, int(groups))
+        self.multi = (len(models) > 1 or self.groups > 1) and cuda
+        self.decoupled = (self.multi and not gather) if decoupled is None else (bool(decoupled) and self.multi)
+        if self.decoupled and gather:
+            raise ValueError("the per-tick command gather needs joined ticks")
         self.fleets = []
         for j, (m, B) in enumerate(models):
             lo, hi = shard_range(B * world, rank, world)
-            stream = torch.cuda.Stream(self.dev) if (self.multi and cuda) else None
-            self.fleets.append(Fleet(m, hi - lo, N, seed + 100 * j, self.dev, start=lo, stream=stream,
-                                     solver_factory=solver_factory,
-                                     schedule="interleaved" if stream is not None else None))
+            for g in range(self.groups):
+                glo, ghi = shard_range(hi - lo, g, self.groups)
+                if ghi <= glo:
+                    continue
+                stream = torch.cuda.Stream(self.dev) if self.multi else None
+                sched = schedule if schedule is not None else ("interleaved" if len(models) > 1 and stream is not None
+                                                               else None)
+                self.fleets.append(Fleet(m, ghi - glo, N, seed + 100 * j, self.dev, start=lo + glo, stream=stream,
+                                         solver_factory=solver_factory, schedule=sched))
         self.B = sum(f.B for f in self.fleets)
         self.offs = [int(v) for v in np.cumsum([0] + [f.B for f in self.fleets])]
         self.gather = CommandGather(5, [self.B] * world, self.dev) if gather else None
@@ -109,8 +129,12 @@ class FleetNode:
         self.fail_cnt = torch.zeros(self.B, dtype=torch.int64, device=self.dev)
 
     def tick_all(self):
-        """One control tick of every robot of this rank."""
-        if not self.multi or self.dev.type != "cuda":
+        """One control tick of every robot of this rank (joined: with the fleet-wide tick boundary)."""
+        if not self.multi:
+            for f in self.fleets:
+                f.tick()
+            return
+        if self.decoupled:
             for f in self.fleets:
                 f.tick()
             return
@@ -124,14 +148,31 @@ class FleetNode:
             done.record(f.stream)
             main.wait_event(done)
 
-    def accumulate(self):
-        for j, f in enumerate(self.fleets):
-            sl = slice(self.offs[j], self.offs[j + 1])
+    def accumulate_one(self, j):
+        """Statistics of fleet j's last tick, on fleet j's stream (decoupled streams) or the current one."""
+        f = self.fleets[j]
+        sl = slice(self.offs[j], self.offs[j + 1])
+        ctx = torch.cuda.stream(f.stream) if (self.decoupled and f.stream is not None) else _nullctx()
+        with ctx:
             self.iters_sum[sl] += f.qp_iter
             torch.maximum(self.iters_max[sl], f.qp_iter, out=self.iters_max[sl])
             self.fail_cnt[sl] += f.status != 0
 
+    def accumulate(self):
+        for j in range(len(self.fleets)):
+            self.accumulate_one(j)
+
+    def join(self):
+        """Make the current stream wait for every fleet stream (end of a decoupled run)."""
+        if self.multi:
+            main = torch.cuda.current_stream(self.dev)
+            for f in self.fleets:
+                done = torch.cuda.Event()
+                done.record(f.stream)
+                main.wait_event(done)
+
     def reset_stats(self):
+        self.join()
         for t_ in (self.iters_sum, self.iters_max, self.fail_cnt):
             t_.zero_()
 
@@ -149,3 +190,11 @@ class FleetNode:
         self.accumulate()
         if self.gather is not None:
             self.gather_commands()
+
+
+class _nullctx:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        return False

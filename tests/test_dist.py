@@ -124,3 +124,24 @@ def test_gloo_world2_fleet_node_equals_single(tmp_path):
     assert (got["g"][:, 4] == 0).all()  # every solve succeeded
     assert np.abs(got["g"][:, :4]).max() > 0  # the commands are not trivially zero
     assert float(got["elapsed"]) > 0 and (got["fails"] == 0).all() and (got["iters"] > 0).all()
+
+
+def test_stream_groups_hold_the_same_robots():
+    """FleetNode groups (bench.py's metric / tric configs run 2): each model's rank-local robots split into
+    contiguous groups that are separate Fleets; with the oracle behind the solver interface the grouped node's
+    commands equal the ungrouped node's bit for bit (on the CPU the groups tick in turn, without streams)."""
+    from cpu_fleet_solver import OracleFleetSolver
+    from nmpc_nav_control_amd.fleet import FleetNode
+    models = [("diff", 5), ("tric", 4)]
+    mk = lambda g: FleetNode(models, MIX_N, MIX_SEED, torch.device("cpu"), groups=g,  # noqa: E731
+                             solver_factory=OracleFleetSolver)
+    one, three = mk(1), mk(3)
+    assert [f.B for f in three.fleets] == [2, 2, 1, 2, 1, 1] and not three.decoupled
+    for _ in range(MIX_TICKS):
+        one.step()
+        three.step()
+    for name in ("u0", "cmd", "status"):
+        a = torch.cat([getattr(f, name) for f in one.fleets], dim=-1)
+        b = torch.cat([getattr(f, name) for f in three.fleets], dim=-1)
+        assert torch.equal(a, b), name
+    assert torch.equal(one.iters_sum, three.iters_sum)

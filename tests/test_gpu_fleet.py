@@ -112,6 +112,28 @@ def test_mixed_fleet_concurrent_streams_full_replay(built):
             assert eu <= TOL_U and ex <= TOL_X, (f.model, eu, ex)
 
 
+@pytest.mark.parametrize("model,N,B,idx", [("diff", 40, 4096, 1), ("tric", 60, 8192, 3)])
+def test_stream_groups_decoupled_bit_identical(built, model, N, B, idx):
+    """bench.py's metric and tric configs split each fleet into 2 stream groups whose closed loops run decoupled
+    on their own HIP streams (FleetNode groups=2). The groups hold the same robots (make_fleet(start=...)), so
+    after 15 ticks every robot's u0, command, status and IPM statistics equal the single-stream run bit for
+    bit, and the decoupled node really did run on two streams without a fleet-wide tick boundary."""
+    one = FleetNode([(model, B)], N, SEED + idx, DEV)
+    two = FleetNode([(model, B)], N, SEED + idx, DEV, groups=2)
+    assert not one.multi and two.multi and two.decoupled and len(two.fleets) == 2
+    assert [f.B for f in two.fleets] == [B // 2, B // 2]
+    for _ in range(15):
+        one.step()
+        two.step()
+    torch.cuda.synchronize()
+    f1 = one.fleets[0]
+    for name in ("u0", "cmd", "status", "qp_iter"):
+        cat = torch.cat([getattr(f, name) for f in two.fleets], dim=-1)
+        assert torch.equal(getattr(f1, name), cat), name
+    assert torch.equal(one.iters_sum, two.iters_sum) and torch.equal(one.fail_cnt, two.fail_cnt)
+    assert int(two.fail_cnt.sum()) == 0
+
+
 def _restore(f, st):
     xv, uv, cv = f.solver.state()
     xv.copy_from(st["X"])

@@ -9,6 +9,7 @@ cd $GRAFT_REPO_ROOT
 mkdir -p $OUT
 ok() { local rc=$1; if [ $rc -ne 0 ]; then echo "STOP rc=$rc"; exit $rc; fi; }
 timeout -k 10 60 build/ubench_valu > $OUT/${TAG}_ubench.json 2> $OUT/${TAG}_ubench.err; rc=$?; echo "ubench rc=$rc"; ok $rc
+timeout -k 10 120 build/capsule_latency 300 > $OUT/${TAG}_capsule_c.json 2> $OUT/${TAG}_capsule_c.err; rc=$?; echo "capsule rc=$rc"; ok $rc
 for c in $CONFIGS; do
   timeout -k 10 300 python bench.py --config $c > $OUT/${TAG}_bench_$c.json 2> $OUT/${TAG}_bench_$c.err; rc=$?; echo "bench $c rc=$rc"; ok $rc
 done
