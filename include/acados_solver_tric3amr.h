@@ -5,10 +5,10 @@
  * libacados_ocp_solver_tric3amr.so at CMakeLists.txt:112-114).
  * Implemented by libnmpc_amd.so on the MI355X batched SQP-RTI kernels.
  *
- * The horizon is a codegen-time constant in acados. Here TRIC3AMR_N defaults to the shipped codegen
- * yaml (tf_ini 2.0 s at 40 Hz -> N = 80, scripts/diff/common.py:6); compile with -DTRIC3AMR_N=<n> and
- * create the solver with tric3amr_acados_create_with_discretization(capsule, TRIC3AMR_N, NULL), or set
- * NMPC_AMD_TRIC3AMR_N=<n> in the environment so that tric3amr_acados_create() uses the same N.
+ * The horizon is a codegen-time constant in acados, and here: tools/generate_solver_libs.py bakes TRIC3AMR_N
+ * from the codegen yaml (the in-tree default follows the shipped yaml). For another horizon regenerate the
+ * library from a yaml with that tf_ini / freq, or call tric3amr_acados_create_with_discretization(capsule, n,
+ * steps) with n uniform time steps (as in acados, a NULL steps vector with n != TRIC3AMR_N fails).
  */
 #ifndef ACADOS_SOLVER_TRIC3AMR_H_
 #define ACADOS_SOLVER_TRIC3AMR_H_

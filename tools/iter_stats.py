@@ -18,7 +18,8 @@ import torch
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-from bench import CONFIGS, Fleet  # noqa: E402
+from bench import CONFIGS  # noqa: E402
+from nmpc_nav_control_amd.fleet import Fleet  # noqa: E402
 from nmpc_nav_control_amd.scenario import DEFAULT_SEED, make_fleet  # noqa: E402
 
 
