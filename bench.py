@@ -182,6 +182,27 @@ def cpu_baseline(fleets, sample, ticks, nthreads):
     return total_solves / total_time, err, fails, total_solves, solves_1 / time_1
 
 
+class LaunchTimer:
+    """HIP events around each solve launch of a timed step, on the launch's own stream (FleetNode.step's timer)."""
+
+    def __init__(self, n_fleets, steps):
+        T = lambda: torch.cuda.Event(enable_timing=True)  # noqa: E731
+        self.ev = [([T() for _ in range(n_fleets)], [T() for _ in range(n_fleets)]) for _ in range(steps)]
+        self.k = 0
+
+    def start(self, j, stream):
+        self.ev[self.k][0][max(j, 0)].record(stream)
+
+    def end(self, j, stream):
+        self.ev[self.k][1][j].record(stream)
+
+    def kernel_ms(self, decoupled):
+        """Per step: the mean launch duration (decoupled streams), or the latest end from the common start."""
+        if decoupled:
+            return [float(np.mean([a.elapsed_time(b) for a, b in zip(s, e)])) for s, e in self.ev]
+        return [max(s[0].elapsed_time(b) for b in e) for s, e in self.ev]
+
+
 def main():
     ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
     ap.add_argument("--gpus", type=int, default=1)
@@ -222,45 +243,18 @@ def main():
     node.reset_stats()
     torch.cuda.synchronize()
 
-    # per-launch timing of the solve kernels with HIP events on their launch streams. One stream: the solve's
-    # duration. Joined streams: from one start event on the main stream to each stream's end-of-solve event
-    # (the region = the latest). Decoupled streams: each launch from its own stream's start event.
-    main_stream = torch.cuda.current_stream()
-    T = lambda: torch.cuda.Event(enable_timing=True)  # noqa: E731
-    ev = [([T() for _ in fleets], [T() for _ in fleets]) for _ in range(args.steps)]
-
+    # per-launch timing of the solve kernels with HIP events on their launch streams (FleetNode.step calls the
+    # timer around every solve launch). One stream: the solve's duration. Joined streams: from one start event
+    # on the main stream to each stream's end-of-solve event (the region = the latest). Decoupled streams: each
+    # launch from its own stream's start event.
+    timer = LaunchTimer(len(fleets), args.steps)
     with TimedRegion(dev) as region:
         for k in range(args.steps):
-            if node.decoupled:
-                for j, f in enumerate(fleets):
-                    ev[k][0][j].record(f.stream)
-                    f.solve()
-                    ev[k][1][j].record(f.stream)
-                    f.advance()
-                    node.accumulate_one(j)
-                continue
-            ev[k][0][0].record(main_stream)
-            if node.multi:
-                for f in fleets:
-                    f.stream.wait_event(ev[k][0][0])
-            for j, f in enumerate(fleets):
-                f.solve()
-                ev[k][1][j].record(f.stream if f.stream is not None else main_stream)
-                f.advance()
-                if f.stream is not None:
-                    done = torch.cuda.Event()
-                    done.record(f.stream)
-                    main_stream.wait_event(done)
-            node.accumulate()
-            if gather:
-                node.gather_commands()
+            timer.k = k
+            node.step(timer)
     elapsed = region.elapsed
 
-    if node.decoupled:  # mean launch duration, and the launches' share of the timed region per step
-        kernel_ms = [float(np.mean([ev[k][0][j].elapsed_time(ev[k][1][j]) for j in range(len(fleets))]))
-                     for k in range(args.steps)]
-    else:
-        kernel_ms = [max(ev[k][0][0].elapsed_time(e) for e in ev[k][1]) for k in range(args.steps)]
+    kernel_ms = timer.kernel_ms(node.decoupled)
     B_rank = node.B
     k_mean = float(node.iters_sum.sum().item()) / (B_rank * args.steps)
     units = args.steps * B_rank * world

@@ -184,9 +184,41 @@ class FleetNode:
                                                     f.status.float()[None]]) for f in self.fleets])
         return self.gathered
 
-    def step(self):
-        """tick_all + statistics + (optional) command gather: one timed step of bench.py."""
-        self.tick_all()
+    def step(self, timer=None):
+        """One step of bench.py's timed region: every robot ticks once (solve -> plant / reference step), the
+        statistics accumulate on the device, and (optional) the commands are all-gathered.
+
+        timer: None, or an object with ``start(j, stream)`` / ``end(j, stream)`` called around fleet j's solve
+        launch on the stream it runs on (bench.py records HIP events there). Joined streams start every fleet
+        from one point of the current stream, so ``start`` is called once, with j = -1."""
+        if self.decoupled:
+            for j, f in enumerate(self.fleets):
+                if timer is not None:
+                    timer.start(j, f.stream)
+                f.solve()
+                if timer is not None:
+                    timer.end(j, f.stream)
+                f.advance()
+                self.accumulate_one(j)
+            return
+        cuda = self.dev.type == "cuda"
+        main = torch.cuda.current_stream(self.dev) if cuda else None
+        if timer is not None:
+            timer.start(-1, main)
+        if self.multi:
+            start = torch.cuda.Event()
+            start.record(main)
+            for f in self.fleets:
+                f.stream.wait_event(start)
+        for j, f in enumerate(self.fleets):
+            f.solve()
+            if timer is not None:
+                timer.end(j, f.stream if f.stream is not None else main)
+            f.advance()
+            if self.multi:
+                done = torch.cuda.Event()
+                done.record(f.stream)
+                main.wait_event(done)
         self.accumulate()
         if self.gather is not None:
             self.gather_commands()
