@@ -116,15 +116,30 @@ def roofline(fleets, node, kernel_ms, steps, step_s=None):
     traffic = pmc.get("l2_fabric_bytes_per_launch") if pmc else None
     if traffic is not None and node.groups > 1:
         traffic *= node.groups  # the PMC record averages one dispatch per kernel name; a step runs `groups` of each
+    # per launch (the contract's figure, checkable against the rocprofv3 kernel-trace average): the flops of one
+    # launch over the mean launch duration; with one launch per step this equals `achieved`
+    n_launch = len(fleets)
+    per_launch = None
+    if n_launch > 1 and len({(f.model, f.N) for f in fleets}) == 1:
+        per_launch = {"flop": (f32 + f64) / n_launch, "ms": round(t_launch * 1e3, 4),
+                      "achieved_tflops": round((f32 + f64) / n_launch / t_launch / 1e12, 4),
+                      "note": "one of the step's %d concurrent launches (%d robots)" % (n_launch, fleets[0].B)}
     return {"bound": "valu", "achieved": round(achieved, 4), "peak": round(achieved / frac, 2), "unit": "TFLOP/s",
-            "frac": round(frac, 6), "traffic": traffic,
-            "fp32": {"flop_per_launch": f32, "achieved_tflops": round(a32, 4), "peak_tflops": p32,
+            "frac": round(frac, 6), "traffic": traffic, "per_launch": per_launch,
+            "fp32": {"flop_per_step": f32, "achieved_tflops": round(a32, 4), "peak_tflops": p32,
                      "frac": round(a32 / p32, 6)},
-            "fp64": {"flop_per_launch": f64, "achieved_tflops": round(a64, 4), "peak_tflops": p64,
+            "fp64": {"flop_per_step": f64, "achieved_tflops": round(a64, 4), "peak_tflops": p64,
                      "frac": round(a64 / p64, 6), "peak_source": "tools/ubench_valu.hip (profiles/%s/ubench_valu.json)"
                      % PROFILE_ROUND},
-            "issue": ({k: pmc.get(k) for k in ("valu_insts_per_wave", "valu_issue_frac", "wait_frac",
+            "issue": ({k: pmc.get(k) for k in ("valu_insts_per_wave", "valu_issue_frac", "valu_issue_est_frac",
+                                               "valu_active_frac", "valu_fma_f64_per_wave", "wait_frac",
                                                "active_frac", "source_commit")} if pmc else None),
+            "executed_flops": ({"fp64_per_step": _scaled(pmc.get("executed_flops_fp64_per_launch"), node.groups),
+                                "fp32_per_step": _scaled(pmc.get("executed_flops_fp32_per_launch"), node.groups),
+                                "note": "64 x SQ_INSTS_VALU_FLOPS_FP64/FP32 from the PMC record: every lane of "
+                                        "every issued instruction, idle team lanes and the lockstep waves' extra "
+                                        "iterations included"}
+                               if pmc and pmc.get("executed_flops_fp64_per_launch") else None),
             "traffic_source": src, "kernel": f"k_sqp_rti_{fleets[0].solver.kernel}" +
             (f" x{len(fleets)} concurrent streams" if len(fleets) > 1 else ""),
             "kernel_ms_mean": round(t_launch * 1e3, 4),
@@ -135,6 +150,10 @@ def roofline(fleets, node, kernel_ms, steps, step_s=None):
             "note": "VALU-bound, latency-limited: <=15x15 per-robot blocks, no GEMM-shaped work (no MFMA); "
                     "traffic = 2*FETCH_SIZE + WRITE_SIZE (L2<->fabric incl. Infinity-Cache hits) per step (the sum "
                     "over the step's launches: one per model and stream group)"}
+
+
+def _scaled(v, g):
+    return None if v is None else v * g
 
 
 def bytes_per_instance(model, N):

@@ -42,6 +42,24 @@ def load(prefix):
     return {k: {c: sum(v) / len(v) for c, v in d.items()} for k, d in acc.items()}
 
 
+C_F64 = 5.19  # cycles per v_fma_f64 wave instruction at one wave per SIMD (tools/ubench_valu.hip)
+C_VALU = 4.0  # one quad-cycle: the wave64 issue cost of any other VALU instruction (a lower bound)
+
+
+def per_wave(tot, c):
+    return tot[c] / tot["SQ_WAVES"] if tot.get(c) is not None and tot.get("SQ_WAVES") else None
+
+
+def issue_est(tot):
+    """Estimated VALU issue cycles over the waves' lifetime (pass 4 counters)."""
+    need = ("SQ_INSTS_VALU_FMA_F64", "SQ_WAVE_CYCLES")
+    if not all(tot.get(c) for c in need) or not tot.get("SQ_INSTS_VALU"):
+        return None
+    f64 = tot["SQ_INSTS_VALU_FMA_F64"]
+    cycles = f64 * C_F64 + (tot["SQ_INSTS_VALU"] - f64) * C_VALU
+    return cycles / (4.0 * tot["SQ_WAVE_CYCLES"])
+
+
 def main():
     prefix, key = sys.argv[1], sys.argv[2]
     rnd = sys.argv[sys.argv.index("--round") + 1] if "--round" in sys.argv else "r02"
@@ -59,6 +77,7 @@ def main():
             tot[c] += v
     fetch, write = tot.get("FETCH_SIZE", 0.0), tot.get("WRITE_SIZE", 0.0)
     cyc = tot.get("SQ_WAVE_CYCLES", 0.0)
+    cyc4 = cyc
     hit, miss = tot.get("TCC_HIT_sum", 0.0), tot.get("TCC_MISS_sum", 0.0)
     try:
         commit = subprocess.run(["git", "-C", ROOT, "rev-parse", "--short", "HEAD"], capture_output=True,
@@ -73,6 +92,22 @@ def main():
            "wait_frac": tot["SQ_WAIT_ANY"] / cyc if cyc else None,
            "active_frac": tot["SQ_ACTIVE_INST_ANY"] / cyc if cyc else None,
            "salu_insts_per_wave": tot["SQ_INSTS_SALU"] / tot["SQ_WAVES"] if tot.get("SQ_WAVES") else None,
+           # pass 4: the VALU mix. fp64 FMAs issue at 5.19 cycles per wave instruction, any other VALU at >= 4
+           # (one quad-cycle; profiles/<round>/ubench_valu.json, one wave per SIMD), so issue_cycles_est / (4 x
+           # SQ_WAVE_CYCLES) is the share of the waves' lifetime the SIMD needs just to issue their VALU work.
+           # The FLOPS counters count flops per wave instruction (2 per FMA; measured: FLOPS_FP64 ~= 2 x FMA_F64
+           # x waves), so x 64 lanes gives the executed flops with idle team lanes and the lockstep max-of-4-teams
+           # iterations included (exec masks ignored): executed_flops_per_launch against bench.py's algorithmic
+           # flops.
+           "valu_fma_f64_per_wave": per_wave(tot, "SQ_INSTS_VALU_FMA_F64"),
+           "valu_fma_f32_per_wave": per_wave(tot, "SQ_INSTS_VALU_FMA_F32"),
+           "valu_trans_f32_per_wave": per_wave(tot, "SQ_INSTS_VALU_TRANS_F32"),
+           "valu_issue_est_frac": issue_est(tot),
+           "valu_active_frac": (tot["SQ_ACTIVE_INST_VALU"] / cyc4 if tot.get("SQ_ACTIVE_INST_VALU") and cyc4 else None),
+           "executed_flops_fp64_per_launch": (64 * tot["SQ_INSTS_VALU_FLOPS_FP64"]
+                                              if tot.get("SQ_INSTS_VALU_FLOPS_FP64") else None),
+           "executed_flops_fp32_per_launch": (64 * tot["SQ_INSTS_VALU_FLOPS_FP32"]
+                                              if tot.get("SQ_INSTS_VALU_FLOPS_FP32") else None),
            "source": os.path.basename(prefix.rstrip("/")), "source_commit": commit,
            "note": "per launch (mixed: summed over the per-model launches of one step); "
                    "traffic = 2*FETCH_SIZE + WRITE_SIZE (L2<->fabric incl. Infinity-Cache hits)"}
