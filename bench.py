@@ -32,9 +32,10 @@ from nmpc_nav_control_amd.sharding import TimedRegion, world_info  # noqa: E402
 # BASELINE.json configs (index -> seed offset 20250824 + idx)
 CONFIGS = {
     # groups: stream groups per model (FleetNode), decoupled closed loops on their own HIP streams; chosen per
-    # config from same-box A/B runs (profiles/r02/ab/groups.txt): metric 2.96 -> 3.00 M it/s with 2 groups
-    # (3 or more lose), tric 1.91 -> 2.28 M with 2, omni4 and diff1024 lose or tie with more than one
-    "metric": dict(idx=1, models=[("diff", 4096)], N=40, groups=2, desc="diff2amr N=40 batch=4096 per GPU"),
+    # config from same-box A/B runs with the single-direction IPM (profiles/r02/ab/ipm_single.txt): tric
+    # 2.11 -> 2.37 M it/s with 2 groups; metric (3.52 -> 3.35 M) and diff1024 lose with 2; omni4 and mixed (one
+    # stream per model already) lose with more (profiles/r02/ab/groups.txt)
+    "metric": dict(idx=1, models=[("diff", 4096)], N=40, desc="diff2amr N=40 batch=4096 per GPU"),
     "diff1024": dict(idx=1, models=[("diff", 1024)], N=40, desc="diff2amr N=40 batch=1024"),
     "omni4": dict(idx=2, models=[("omni4", 4096)], N=40, desc="omni4amr (11x4) N=40 batch=4096"),
     "tric": dict(idx=3, models=[("tric", 8192)], N=60, groups=2, desc="tric3amr N=60 batch=8192, alpha bounds active"),

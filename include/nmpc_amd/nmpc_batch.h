@@ -50,7 +50,14 @@ typedef struct nmpc_model_params {
     int qp_iter_max;   /* 50 */
     double qp_tol_stat, qp_tol_ineq, qp_tol_comp; /* fp32 stopping rule, see DESIGN.md */
     double qp_mu0, qp_thr0, qp_tau;              /* IPM initial point and fraction-to-boundary */
+    /* IPM direction rule: NMPC_IPM_SINGLE (default) one Newton direction per iteration with the centring
+     * sigma = clamp((1 - alpha_prev)^2, qp_sigma_lo, qp_sigma_hi); NMPC_IPM_MEHROTRA predictor-corrector (the
+     * fp64 oracle's rule). Both solve the same QP to the same stopping rule (DESIGN.md "Algorithm"). */
+    int qp_ipm;
+    double qp_sigma_lo, qp_sigma_hi; /* 0.01, 0.5 */
 } nmpc_model_params;
+
+enum { NMPC_IPM_MEHROTRA = 0, NMPC_IPM_SINGLE = 1 };
 
 typedef struct nmpc_batch nmpc_batch;
 

@@ -77,6 +77,13 @@ KParams to_kparams(const nmpc_model_params& p, int nx, int nu, int nbx, int nbu)
     k.mu0 = (float)p.qp_mu0;
     k.thr0 = (float)p.qp_thr0;
     k.tau = (float)p.qp_tau;
+    k.ipm = p.qp_ipm;
+    k.sd_lo = (float)p.qp_sigma_lo;
+    k.sd_hi = (float)p.qp_sigma_hi;
+    if (const char* v = std::getenv("NMPC_AMD_IPM")) {  // single | mehrotra: same-box A/B override
+        if (!std::strcmp(v, "single")) k.ipm = NMPC_IPM_SINGLE;
+        else if (!std::strcmp(v, "mehrotra")) k.ipm = NMPC_IPM_MEHROTRA;
+    }
     return k;
 }
 
@@ -143,6 +150,11 @@ int check_params(const nmpc_model_params* prm)
     if (prm->N < 1 || prm->N > 4096) return set_err(NMPC_ERR_ARG, "horizon N out of range [1, 4096]");
     if (!(prm->dt > 0.0) || !(prm->dt_ctrl > 0.0)) return set_err(NMPC_ERR_ARG, "dt must be positive");
     if (prm->qp_iter_max < 1) return set_err(NMPC_ERR_ARG, "qp_iter_max must be >= 1");
+    if (prm->qp_ipm != NMPC_IPM_MEHROTRA && prm->qp_ipm != NMPC_IPM_SINGLE)
+        return set_err(NMPC_ERR_ARG, "qp_ipm must be NMPC_IPM_MEHROTRA or NMPC_IPM_SINGLE");
+    if (prm->qp_ipm == NMPC_IPM_SINGLE &&
+        !(prm->qp_sigma_lo > 0.0 && prm->qp_sigma_lo <= prm->qp_sigma_hi && prm->qp_sigma_hi <= 1.0))
+        return set_err(NMPC_ERR_ARG, "qp_sigma_lo / qp_sigma_hi need 0 < lo <= hi <= 1");
     for (int i = 0; i < nbx; i++)
         if (!(prm->lbx[i] < prm->ubx[i])) return set_err(NMPC_ERR_ARG, "state bounds need lbx < ubx");
     for (int i = 0; i < nbu; i++)
@@ -214,6 +226,13 @@ int nmpc_model_params_default(int model, int N, nmpc_model_params* prm)
     // the cold-start tail grows by at most 2 iterations (DESIGN.md "Algorithm and precision")
     prm->qp_thr0 = 0.25;
     prm->qp_tau = 0.995;
+    // one direction per IPM iteration (P1 + one forward sweep) instead of Mehrotra's two (P1 + F0 + C1 + F1):
+    // more, cheaper iterations; the slowest robot, which sets the kernel time, gets there sooner. Same-box A/B,
+    // M it/s: diff N=40 B=4096 2.89 -> 3.24 (2 stream groups; 3.52 with one), B=1024 0.89 -> 1.00, tric 2.12 ->
+    // 2.28, mixed 3.51 -> 3.64, omni4 2.45 -> 2.44 (profiles/r02/ab/ipm_single.txt)
+    prm->qp_ipm = NMPC_IPM_SINGLE;
+    prm->qp_sigma_lo = 0.01;
+    prm->qp_sigma_hi = 0.5;
     return NMPC_OK;
 }
 

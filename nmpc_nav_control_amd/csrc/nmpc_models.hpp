@@ -24,6 +24,10 @@ struct KParams {
     int terminal_hack, sin_bug;
     int iter_max;
     float tol_stat, tol_ineq, tol_comp, mu0, thr0, tau;
+    // IPM direction rule: 0 Mehrotra predictor-corrector, 1 one direction per iteration with centring
+    // sigma = clamp((1 - alpha_prev)^2, sd_lo, sd_hi) (DESIGN.md "Algorithm and precision")
+    int ipm;
+    float sd_lo, sd_hi;
 };
 
 enum ModelId { kDiff = 0, kOmni4 = 1, kTric = 2 };

@@ -303,7 +303,10 @@ __device__ __forceinline__ float step_bound_r(float amax, float v, float dv)
 // MS: store the slack / multiplier quad only where a bound lives (launches with more waves than SIMDs, where the
 // record traffic shows: tric N=60 B=8192 4.47 -> 4.39 ms; with one wave per SIMD the exec-mask switches cost
 // more than the bytes save: diff N=40 B=4096 1.555 -> 1.566 ms)
-template <class M, bool MS>
+// SD: one direction per IPM iteration (P1 builds the rhs with the centring target sigma mu, one forward sweep
+// computes the direction, the step and the complementarity polynomial that predicts the next mu) instead of
+// Mehrotra's predictor-corrector (P1 + F0 + C1 + F1 sweeps)
+template <class M, bool MS, bool SD>
 __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int mode)
 {
     using R = TeamRec<M>;
@@ -635,6 +638,9 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
     bool done = false;
     float exit_res[3] = {0.0f, 0.0f, 0.0f};
     float alpha = 0.0f, sigma_mu = 0.0f, eta = 0.0f, mu_prev = 3.0e38f;
+    // SD: centring target of the next direction, built into P1's rhs. The first direction: sigma = sd_hi (no
+    // previous step) and mu = mu0 exactly (every bounded pair starts at t * lambda = mu0, P0)
+    float tg_rhs = P.sd_hi * P.mu0;
     for (int it = 0;; it++) {
         // P1 (backward): apply the previous step, residuals, adjoint, fp64 classic Riccati factorisation,
         // predictor rhs
@@ -668,8 +674,12 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
                 const float dz = rc[R::DZ];
                 const float rl = z - lb - tl, rr = ubd - z - tu;
                 const float itl = frcp(tl), itu = frcp(tu);
-                const BoundDir da = bound_dir(rc[R::DZA], rl, rr, tl, tu, ll, lu, itl, itu, 0.0f, 0.0f);
-                const float tgl = sigma_mu - eta * da.dll * da.dtl, tgu = sigma_mu - eta * da.dlu * da.dtu;
+                float tgl = sigma_mu, tgu = sigma_mu;  // SD: the previous direction's target
+                if constexpr (!SD) {
+                    const BoundDir da = bound_dir(rc[R::DZA], rl, rr, tl, tu, ll, lu, itl, itu, 0.0f, 0.0f);
+                    tgl = sigma_mu - eta * da.dll * da.dtl;
+                    tgu = sigma_mu - eta * da.dlu * da.dtu;
+                }
                 const BoundDir d = bound_dir(dz, rl, rr, tl, tu, ll, lu, itl, itu, tgl, tgu);
                 const float ab = bnd ? a_upd : 0.0f, av = valid ? a_upd : 0.0f;
                 tl += ab * d.dtl;
@@ -690,7 +700,9 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
             max_c = fmaxf(max_c, fmaxf(ll * tl, lu * tu));
             const float lamdiff = ll - lu;
             const float sig = ll * itl + lu * itu;
-            const float gh = ll * rl * itl + ll - lu * rr * itu - lu;
+            // predictor rhs (zero complementarity target); SD: the centring target tg_rhs (0 on kFar slots)
+            const float gh = SD ? ll * rl * itl + ll - lu * rr * itu - lu - tg_rhs * itl + tg_rhs * itu
+                                : ll * rl * itl + ll - lu * rr * itu - lu;
             STAMPF(1);
             float Gc[NX];
             column(rc, Gc);
@@ -819,11 +831,15 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
 
         // pass 0: affine direction (forward; stores DZA, sums s1/s2 of the mu_aff polynomial);
         // pass 1: Mehrotra corrector (backward rhs through the stored factor, then forward; stores DZ);
-        // pass 2: pure-centring safeguard for teams whose pass-1 step stayed below 0.1
+        // pass 2: pure-centring safeguard for teams whose pass-1 step stayed below 0.1.
+        // SD: pass 1 only, without the backward sweep: P1 already built the rhs with the target tg_rhs
         float sigma = 0.0f, alpha_aff = 0.0f;
-        for (int pass = 0; pass < 3; pass++) {
+        for (int pass = SD ? 1 : 0; pass < (SD ? 2 : 3); pass++) {
             bool run = !done;
-            if (pass == 1) {
+            if (SD) {
+                sigma_mu = tg_rhs;
+                eta = 0.0f;
+            } else if (pass == 1) {
                 sigma_mu = sigma * mu;
                 eta = alpha_aff;
             } else if (pass == 2) {
@@ -835,7 +851,7 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
                 eta = run ? 0.0f : eta;
             }
             const bool ld = lv && run;
-            if (pass > 0) {
+            if (!SD && pass > 0) {
                 // corrector rhs through the stored factorisation (backward)
                 float pvc = 0.0f;
                 sweepd(std::integral_constant<int, LIGHT_DC>{}, std::integral_constant<int, 0>{}, std::integral_constant<int, R::NB>{}, N, 0, -1, ld, [&](int k, float (&rc)[RS]) {
@@ -874,9 +890,11 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
             if (pass == 1) STAMPC1();
             // forward: du from the stored factor, dz, bounded-variable directions, next-stage dx
             float amax = 1e30f, s1 = 0.0f, s2 = 0.0f;
-            // CORR 0: affine pass, 1: corrector / safeguard pass (compile-time bodies)
+            // body kind 0: affine pass, 1: corrector / safeguard pass, 2: SD direction (target sigma_mu without the
+            // affine correction; sums the complementarity polynomial of the step) -- compile-time bodies
             auto fwd = [&](auto cc) {
-            constexpr bool corr = decltype(cc)::value == 1;
+            constexpr int kind = decltype(cc)::value;
+            constexpr bool corr = kind != 0;
             float dxs = 0.0f;
             sweepd(std::integral_constant<int, LIGHT_D>{}, std::integral_constant<int, 0>{}, std::integral_constant<int, R::NF>{}, 0, N, 1, ld, [&](int k, float (&rc)[RS]) {
                 const bool vu = is_u && k < N;
@@ -914,19 +932,26 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
                     const float rl = z - rc[R::LB] - tl, rr = rc[R::UB] - z - tu;
                     const float itl = frcp(tl), itu = frcp(tu);
                     float tgl = 0.0f, tgu = 0.0f;
-                    if (corr) {
+                    if (kind == 1) {
                         const BoundDir da = bound_dir(rc[R::DZA], rl, rr, tl, tu, ll, lu, itl, itu, 0.0f, 0.0f);
                         tgl = sigma_mu - eta * da.dll * da.dtl;
                         tgu = sigma_mu - eta * da.dlu * da.dtu;
+                    } else if (kind == 2) {
+                        tgl = sigma_mu;
+                        tgu = sigma_mu;
                     }
                     const BoundDir d = bound_dir(dz, rl, rr, tl, tu, ll, lu, itl, itu, tgl, tgu);
                     amax = step_bound_r(amax, tl, d.dtl);
                     amax = step_bound_r(amax, tu, d.dtu);
                     amax = step_bound_r(amax, ll, d.dll);
                     amax = step_bound_r(amax, lu, d.dlu);
-                    if (!corr) {  // dll = dlu = 0 on sentinel slots at zero targets
+                    if (kind == 0) {  // dll = dlu = 0 on sentinel slots at zero targets
                         s1 += ll * d.dtl + tl * d.dll + lu * d.dtu + tu * d.dlu;
                         s2 += d.dll * d.dtl + d.dlu * d.dtu;
+                    } else if (kind == 2) {  // a nonzero target moves the sentinels' multipliers: bounded slots only
+                        const bool bnd = valid && has_b;
+                        s1 += bnd ? ll * d.dtl + tl * d.dll + lu * d.dtu + tu * d.dlu : 0.0f;
+                        s2 += bnd ? d.dll * d.dtl + d.dlu * d.dtu : 0.0f;
                     }
                 }
                 if (ld && valid) tbase[(size_t)k * KS + (!corr ? rec_off<RS, QM>(R::DZA) : rec_off<RS, QM>(R::DZ))] = dz;
@@ -934,10 +959,21 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
             });
             };
             // one compiled body per pass kind: same-box A/B diff metric 1.553 -> 1.526 ms, tric 4.382 -> 4.363 ms
-            if (pass == 0) fwd(std::integral_constant<int, 0>{});
+            if constexpr (SD) fwd(std::integral_constant<int, 2>{});
+            else if (pass == 0) fwd(std::integral_constant<int, 0>{});
             else fwd(std::integral_constant<int, 1>{});
             amax = row_min16(lv ? amax : 1e30f);
-            if (pass == 0) {
+            if (SD) {
+                // the step, then the next direction's target: mu after the step is exactly the complementarity
+                // polynomial (sum_c + a s1 + a^2 s2) / 2m; sigma = clamp((1 - a)^2, sd_lo, sd_hi)
+                s1 = row_sum16(lv ? s1 : 0.0f);
+                s2 = row_sum16(lv ? s2 : 0.0f);
+                if (run) alpha = fminf(1.0f, P.tau * amax);
+                const float mu_next = fmaxf((sum_c + alpha * s1 + alpha * alpha * s2) * inv_m2, 0.0f);
+                const float om = 1.0f - alpha;
+                tg_rhs = fminf(fmaxf(om * om, P.sd_lo), P.sd_hi) * mu_next;
+                if (it < kStampItsC) STAMP(4 + 4 * it);
+            } else if (pass == 0) {
                 s1 = row_sum16(lv ? s1 : 0.0f);
                 s2 = row_sum16(lv ? s2 : 0.0f);
                 alpha_aff = fminf(1.0f, amax);
@@ -1026,10 +1062,16 @@ hipError_t launch_sqp_rti_team(const KParams& P, const KArgs& a, int mode, hipSt
     // 26 KB at N = 80)
     const size_t lds = (mode == kModeRun && a.segs) ? (sizeof(double) + 3 * sizeof(float)) * 16 * (size_t)(P.N + 1) : 0;
     if (lds > 65536) return hipErrorInvalidValue;
-    if (a.dense)
-        hipLaunchKernelGGL((k_sqp_rti_team<M, true>), dim3(grid), dim3(block), lds, stream, P, a, mode);
-    else
-        hipLaunchKernelGGL((k_sqp_rti_team<M, false>), dim3(grid), dim3(block), lds, stream, P, a, mode);
+    if (P.ipm == 1) {
+        if (a.dense)
+            hipLaunchKernelGGL((k_sqp_rti_team<M, true, true>), dim3(grid), dim3(block), lds, stream, P, a, mode);
+        else
+            hipLaunchKernelGGL((k_sqp_rti_team<M, false, true>), dim3(grid), dim3(block), lds, stream, P, a, mode);
+    } else if (a.dense) {
+        hipLaunchKernelGGL((k_sqp_rti_team<M, true, false>), dim3(grid), dim3(block), lds, stream, P, a, mode);
+    } else {
+        hipLaunchKernelGGL((k_sqp_rti_team<M, false, false>), dim3(grid), dim3(block), lds, stream, P, a, mode);
+    }
     return hipGetLastError();
 }
 

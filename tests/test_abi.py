@@ -147,3 +147,24 @@ def test_codegen_horizon():
     """scripts/diff/common.py: N = ceil(tf_ini * freq); shipped config tf_ini 2.0, freq 40 -> N 80."""
     assert horizon_from_codegen({"tf_ini": 2.0, "freq": 40}) == (80, 1 / 40)
     assert horizon_from_codegen({"tf_ini": 1.0, "freq": 40})[0] == 40
+
+
+def test_params_struct_layout_and_ipm_options(built):
+    """The ctypes mirror of nmpc_model_params covers exactly what the library writes (a guard region past the
+    mirror stays untouched), the IPM rule defaults to one direction per iteration, and a bad rule or sigma
+    clamp is an argument error at nmpc_batch_create."""
+    import ctypes
+    L = _lib.lib()
+    n = ctypes.sizeof(_lib.ModelParams)
+    buf = (ctypes.c_ubyte * (n + 64))(*([0xAB] * (n + 64)))
+    prm = _lib.ModelParams.from_buffer(buf)
+    assert L.nmpc_model_params_default(0, 40, ctypes.byref(prm)) == 0
+    assert bytes(buf[n:]) == b"\xab" * 64
+    assert prm.qp_ipm == 1 and (prm.qp_sigma_lo, prm.qp_sigma_hi) == (0.01, 0.5)
+    h = ctypes.c_void_p()
+    for field, val in (("qp_ipm", 2), ("qp_sigma_lo", 0.0), ("qp_sigma_hi", 1.5)):
+        bad = _lib.ModelParams()
+        assert L.nmpc_model_params_default(0, 20, ctypes.byref(bad)) == 0
+        setattr(bad, field, val)
+        assert L.nmpc_batch_create(ctypes.byref(bad), 8, ctypes.byref(h)) != 0, field
+        assert b"qp_" in L.nmpc_last_error()

@@ -12,6 +12,7 @@ import torch
 
 from helpers import oracle_closed_loop
 
+from nmpc_nav_control_amd._lib import default_params
 from nmpc_nav_control_amd.batch import BatchSolver
 from nmpc_nav_control_amd.scenario import make_fleet
 from oracle.oracle import Oracle
@@ -40,16 +41,24 @@ def upload_iterate(solver, xbars, ubars):
     uv.copy_from(U)
 
 
-KERNELS = ["team"]
+# IPM direction rules (nmpc_model_params.qp_ipm): the default one direction per iteration, and Mehrotra's
+# predictor-corrector (the oracle's rule); both must reach the oracle's QP solution within the tolerance
+IPMS = {"single": 1, "mehrotra": 0}
 
 
-@pytest.mark.parametrize("kernel", KERNELS)
+def make_solver(model, N, cap, ipm):
+    prm = default_params(model, N)
+    prm.qp_ipm = IPMS[ipm]
+    return BatchSolver(model, N, cap, params=prm)
+
+
+@pytest.mark.parametrize("ipm", sorted(IPMS))
 @pytest.mark.parametrize("model", MODELS)
 # (80: the shipped codegen horizon; 1 and 2: the shortest horizons; B not a multiple of the 4 teams per wave)
 @pytest.mark.parametrize("N,B,ticks", [(20, 48, 8), (40, 5, 4), (80, 13, 3), (1, 7, 4), (2, 3, 4)])
-def test_solve_matches_oracle(built, kernel, model, N, B, ticks):
+def test_solve_matches_oracle(built, ipm, model, N, B, ticks):
     o, rec = oracle_closed_loop(model, N, B, ticks)
-    solver = BatchSolver(model, N, 64, kernel=kernel)
+    solver = make_solver(model, N, 64, ipm)
     nx, nu, ny = o.nx, o.nu, o.ny
     x0 = np.stack([r[0] for r in rec]).T
     yref = np.stack([r[1] for r in rec]).transpose(1, 2, 0)
@@ -78,10 +87,10 @@ def test_solve_matches_oracle(built, kernel, model, N, B, ticks):
     assert qp_iter.cpu().numpy().max() < 50
 
 
-@pytest.mark.parametrize("kernel", KERNELS)
+@pytest.mark.parametrize("ipm", sorted(IPMS))
 @pytest.mark.parametrize("model", MODELS)
 @pytest.mark.parametrize("resets", [False, True])
-def test_run_closed_loop_matches_oracle(built, kernel, model, resets):
+def test_run_closed_loop_matches_oracle(built, ipm, model, resets):
     """Batched run() + closed-loop plant on the GPU; the oracle replays the same per-tick inputs with its own
     fp64 warm-start chain (prepare -> sqp_rti -> post, NMPCNavControl*::run: no shift, x1 -> x0 carry of the
     vel-refs, NMPCNavControlDiff.cpp:168-172). With resets, every fifth robot is reset
@@ -89,7 +98,7 @@ def test_run_closed_loop_matches_oracle(built, kernel, model, resets):
     N, B, T = 20, 70, 12
     reset_mask = torch.from_numpy((np.arange(B) % 5 == 0).astype(np.uint8)).to(DEV)
     fl = make_fleet(model, B, seed=11)
-    solver = BatchSolver(model, N, B, kernel=kernel)
+    solver = make_solver(model, N, B, ipm)
     o = Oracle(model, N)
     _, _, cr = solver.state()
     cr.copy_from(t(fl["carried"]))
