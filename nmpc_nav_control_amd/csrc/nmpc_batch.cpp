@@ -80,10 +80,13 @@ KParams to_kparams(const nmpc_model_params& p, int nx, int nu, int nbx, int nbu)
     k.ipm = p.qp_ipm;
     k.sd_lo = (float)p.qp_sigma_lo;
     k.sd_hi = (float)p.qp_sigma_hi;
-    if (const char* v = std::getenv("NMPC_AMD_IPM")) {  // single | mehrotra: same-box A/B override
+    // same-box A/B overrides (tools/ab_env.py): the IPM rule and its sigma clamp
+    if (const char* v = std::getenv("NMPC_AMD_IPM")) {  // single | mehrotra
         if (!std::strcmp(v, "single")) k.ipm = NMPC_IPM_SINGLE;
         else if (!std::strcmp(v, "mehrotra")) k.ipm = NMPC_IPM_MEHROTRA;
     }
+    if (const char* v = std::getenv("NMPC_AMD_SIGMA_LO")) k.sd_lo = std::strtof(v, nullptr);
+    if (const char* v = std::getenv("NMPC_AMD_SIGMA_HI")) k.sd_hi = std::strtof(v, nullptr);
     return k;
 }
 
