@@ -564,6 +564,11 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
 #pragma unroll
         for (int j = 0; j < 3; j++) { tr[j] = tr1[j]; tr1[j] = tr2[j]; }
     }
+    // e_r: places the diagonal D of M = D + G'PG with one multiply per entry instead of two selects (same-box
+    // A/B: diff N=40 B=4096 +0.8 %, B=1024 +1.2 %, tric +0.6 %; profiles/r02/ab/onehot.txt)
+    double onehot[NV];
+#pragma unroll
+    for (int j = 0; j < NV; j++) onehot[j] = (r == j) ? 1.0 : 0.0;
     double gcol64[NX];
 #pragma unroll
     for (int i = 0; i < NX; i++) gcol64[i] = (double)gcol[i];
@@ -750,7 +755,7 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
                 const double dg = valid ? (double)h_stage + (double)sig : 1.0;
                 double Lr[NV];
 #pragma unroll
-                for (int j = 0; j < NV; j++) Lr[j] = (r == j) ? dg : 0.0;
+                for (int j = 0; j < NV; j++) Lr[j] = onehot[j] * dg;
                 double pivot;
                 mrow_pg_block<NX, NU>(Lr, pivot, pg, Gd);  // pivot = M[0][0]
                 STAMPF(4);
