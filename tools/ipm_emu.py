@@ -3,7 +3,9 @@
 
 Same algorithm as k_sqp_rti_team / oracle/nmpc_oracle.c oc_qp_ipm (dynamics-feasible Mehrotra IPM over the
 delta-form OCP-QP, Riccati recursion, fp32-style stopping rule of the device) vectorised over robots in fp64,
-plus the active-set polish variants studied in DESIGN.md. Input: the QPs of a dumped closed-loop tick
+plus the variants studied in DESIGN.md: `single=` is the device's default one-direction rule
+(qp_ipm = NMPC_IPM_SINGLE: solve(single=lambda mu, a, it: np.clip((1 - a) ** 2, 0.01, 0.5))), `polish=` the
+active-set polish. Input: the QPs of a dumped closed-loop tick
 (tools/iter_stats.py --dump) built by the oracle's oc_build_qp.
 usage: python tools/ipm_emu.py gpurun_out/iter_dump.npz [--tick 0] [--n 4096]
 """
