@@ -55,6 +55,12 @@ typedef struct nmpc_model_params {
      * fp64 oracle's rule). Both solve the same QP to the same stopping rule (DESIGN.md "Algorithm"). */
     int qp_ipm;
     double qp_sigma_lo, qp_sigma_hi; /* 0.01, 0.5 */
+    /* IPM warm start (default 1): a robot whose previous solve on this handle succeeded starts its bound
+     * multipliers at max(lambda_previous, qp_warm_kappa / t) instead of qp_mu0 / t (the QP solution is the same;
+     * the IPM path is shorter). 0 gives acados' cold start every tick. Reset robots and nmpc_batch_init_iterate
+     * start cold. The capsule ABI always starts cold (its capsules do not own a slot). */
+    int qp_warm_start;
+    double qp_warm_kappa; /* 0.05 */
 } nmpc_model_params;
 
 enum { NMPC_IPM_MEHROTRA = 0, NMPC_IPM_SINGLE = 1 };
@@ -148,6 +154,12 @@ int nmpc_batch_set_schedule(nmpc_batch* b, int mode);
 /* Device pointers of the resident state: xbar [(N+1)*NX][stride], ubar [N*NU][stride],
  * carried [NBX][stride]; stride = capacity. */
 int nmpc_batch_state(nmpc_batch* b, float** xbar, float** ubar, float** carried, int* stride);
+
+/* Device pointers of the IPM warm-start state (qp_warm_start): warm [capacity] per-robot flags (1: the robot's
+ * last solve succeeded) and the scratch records [scratch_bytes] that hold each robot's multipliers. With
+ * nmpc_batch_state this is everything a solve reads from the handle, e.g. to checkpoint a fleet or to replay a
+ * tick bit for bit. */
+int nmpc_batch_warm_state(nmpc_batch* b, unsigned char** warm, float** scratch, size_t* scratch_bytes);
 
 /* Bench / test harness: closed-loop plant step and path-reference regeneration for B robots
  * (see DESIGN.md "Synthetic closed loop"). All device pointers, [field][B]:

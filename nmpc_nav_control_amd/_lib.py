@@ -29,6 +29,7 @@ class ModelParams(ctypes.Structure):
         ("qp_tol_stat", ctypes.c_double), ("qp_tol_ineq", ctypes.c_double), ("qp_tol_comp", ctypes.c_double),
         ("qp_mu0", ctypes.c_double), ("qp_thr0", ctypes.c_double), ("qp_tau", ctypes.c_double),
         ("qp_ipm", ctypes.c_int), ("qp_sigma_lo", ctypes.c_double), ("qp_sigma_hi", ctypes.c_double),
+        ("qp_warm_start", ctypes.c_int), ("qp_warm_kappa", ctypes.c_double),
     ]
 
 
@@ -57,7 +58,7 @@ class SolverCapsule(ctypes.Structure):
 BATCH_SYMBOLS = [
     "nmpc_model_dims", "nmpc_model_params_default", "nmpc_model_params_set_limits", "nmpc_batch_create",
     "nmpc_batch_destroy", "nmpc_batch_set_params", "nmpc_batch_get_params", "nmpc_batch_init_iterate",
-    "nmpc_batch_solve", "nmpc_batch_run", "nmpc_batch_run_path", "nmpc_batch_state", "nmpc_batch_set_kernel", "nmpc_batch_set_schedule",
+    "nmpc_batch_solve", "nmpc_batch_run", "nmpc_batch_run_path", "nmpc_batch_state", "nmpc_batch_warm_state", "nmpc_batch_set_kernel", "nmpc_batch_set_schedule",
     "nmpc_fleet_sim_step",
     "nmpc_last_error", "nmpc_version", "nmpc_path_discretize", "nmpc_codegen_default", "nmpc_capsule_new",
     "nmpc_capsule_delete", "nmpc_capsule_create", "nmpc_capsule_reset", "nmpc_capsule_update_params",
@@ -105,6 +106,7 @@ def lib():
     L.nmpc_batch_set_kernel.argtypes = [vp, i]
     L.nmpc_batch_set_schedule.argtypes = [vp, i]
     L.nmpc_batch_state.argtypes = [vp, ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.POINTER(vp), c_int_p]
+    L.nmpc_batch_warm_state.argtypes = [vp, ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.POINTER(ctypes.c_size_t)]
     L.nmpc_fleet_sim_step.argtypes = [vp, i, vp, vp, vp, vp, vp, vp, vp, vp, vp, i, vp]
     L.nmpc_path_discretize.argtypes = [i, vp, i, vp, vp, ctypes.c_double, i, i, vp, vp, vp]
     L.nmpc_codegen_default.argtypes = [i, ctypes.POINTER(CodegenDesc)]

@@ -103,6 +103,23 @@ class BatchSolver:
                 _DeviceView(ub.value, (self.N * self.nu, S), self.device),
                 _DeviceView(cr.value, (self.nbx, S), self.device))
 
+    def warm_state(self):
+        """Views of the IPM warm-start state (nmpc_batch_warm_state): per-robot flags [cap] (uint8) and the
+        scratch records (bytes); with state() everything a solve reads from the handle."""
+        w, sc, nb = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_size_t()
+        check(lib().nmpc_batch_warm_state(self._h, ctypes.byref(w), ctypes.byref(sc), ctypes.byref(nb)),
+              "nmpc_batch_warm_state")
+        return (_DeviceView(w.value, (1, self.capacity), self.device, torch.uint8),
+                _DeviceView(sc.value, (1, nb.value // 4), self.device))
+
+    def save_state(self):
+        """Device copies of everything a solve reads from the handle (iterate, carried refs, warm start)."""
+        return [v.to_tensor() for v in self.state() + self.warm_state()]
+
+    def restore_state(self, saved):
+        for v, t in zip(self.state() + self.warm_state(), saved):
+            v.copy_from(t)
+
     def empty(self, *shape, dtype=torch.float32):
         return torch.empty(*shape, dtype=dtype, device=self.device)
 
@@ -168,20 +185,21 @@ class BatchSolver:
 class _DeviceView:
     """Copy helpers for device memory owned by the library (no torch tensor aliases it)."""
 
-    def __init__(self, addr, shape, device):
-        self.addr, self.shape, self.device = addr, shape, device
+    def __init__(self, addr, shape, device, dtype=torch.float32):
+        self.addr, self.shape, self.device, self.dtype = addr, shape, device, dtype
+        self.itemsize = torch.empty(0, dtype=dtype).element_size()
 
     def to_tensor(self):
         rows, S = self.shape
-        out = torch.empty(rows, S, dtype=torch.float32, device=self.device)
-        _memcpy(out.data_ptr(), self.addr, rows * S * 4)
+        out = torch.empty(rows, S, dtype=self.dtype, device=self.device)
+        _memcpy(out.data_ptr(), self.addr, rows * S * self.itemsize)
         return out
 
     def copy_from(self, t):
         rows, S = self.shape
-        t = t.to(device=self.device, dtype=torch.float32).contiguous()
+        t = t.to(device=self.device, dtype=self.dtype).contiguous()
         assert t.numel() == rows * S
-        _memcpy(self.addr, t.data_ptr(), rows * S * 4)
+        _memcpy(self.addr, t.data_ptr(), rows * S * self.itemsize)
 
 
 def _memcpy(dst, src, nbytes):

@@ -122,6 +122,7 @@ void codegen_defaults(nmpc_capsule_impl* c, const nmpc_codegen_desc& d)
 {
     nmpc_model_params_default(c->model, c->N, &c->prm);
     c->prm.terminal_hack = 0;  // the wrappers apply it themselves through cost_model_set(N, "W")
+    c->prm.qp_warm_start = 0;  // capsules share an engine's slots call by call: no per-robot multiplier history
     c->prm.dt = d.tf / d.N;    // uniform time steps tf / N_codegen (ocp.solver_options.tf, N_horizon)
     std::memcpy(c->prm.p, d.p, sizeof(d.p));
     std::memcpy(c->prm.lbx, d.lbx, sizeof(d.lbx));

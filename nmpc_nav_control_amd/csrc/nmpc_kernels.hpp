@@ -53,6 +53,8 @@ struct KArgs {
     // team placement (schedule.hip): team slot -> instance, or nullptr (slot i = instance i)
     const int* order;
     int* iter_key;  // [stride] resident: executed IPM iterations of the last solve, or nullptr
+    unsigned char* warm;  // [stride] resident: 1 if the robot's last solve succeeded (its records hold its
+                          // multipliers), or nullptr (cold start, nothing written)
     int dense;      // the launch has more waves than the device has SIMDs (selects the team kernel variant)
 };
 

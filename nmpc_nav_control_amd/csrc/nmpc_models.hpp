@@ -28,6 +28,9 @@ struct KParams {
     // sigma = clamp((1 - alpha_prev)^2, sd_lo, sd_hi) (DESIGN.md "Algorithm and precision")
     int ipm;
     float sd_lo, sd_hi;
+    // warm start of the bound multipliers from the robot's previous solve (KArgs::warm flags)
+    int warm;
+    float warm_kappa;
 };
 
 enum ModelId { kDiff = 0, kOmni4 = 1, kTric = 2 };

@@ -348,7 +348,11 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
     // this lane's record of stage k: tbase + k * 16 * RS
     // idle slots (r >= NV) alias slot 0's record: their (unpredicated) loads then read valid data and touch no
     // extra cache lines; they never store
-    float* const tbase = a.scratch + (size_t)team * (N + 1) * 16 * RS + (lv ? r : 0) * rec_lane<RS, QM>();
+    // the robot's records (indexed by the robot, not the team slot, so that they carry its multipliers to its next
+    // solve whatever the placement)
+    float* const tbase = a.scratch + (size_t)inst * (N + 1) * 16 * RS + (lv ? r : 0) * rec_lane<RS, QM>();
+    // IPM warm start: the bound multipliers of the robot's previous successful solve are still in its records
+    const bool warm = P.warm && a.warm && a.warm[inst] && !(a.reset && a.reset[inst]);
     constexpr int KS = 16 * RS;
 
 #define XB(k, j) a.xbar[((size_t)(k) * NX + (j)) * S + inst]
@@ -466,7 +470,16 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
         });
     }
     float dx = is_x ? x0_lane - XB(0, xi) : 0.0f;  // this lane's state delta at the current stage
+    float sum_c0 = 0.0f;  // complementarity of the initial point (its mean sets the first SD target)
+    // warm start: the previous multipliers (LL, LU) of the stage, prefetched one stage ahead
+    auto load_l = [&](int k) -> float2 {
+        return warm ? *reinterpret_cast<const float2*>(tbase + (size_t)(k <= N ? k : N) * KS + rec_off<RS, QM>(R::LL))
+                    : make_float2(0.0f, 0.0f);
+    };
+    float2 lprev = load_l(0);
     for (int k = 0; k <= N; k++) {
+        const float2 lp = lprev;
+        lprev = load_l(k + 1);
         float xb2[NX], ub2[NU], tr2[3];
         load_row(k + 2, xb2, ub2, tr2);  // two stages ahead (clamped)
         // stage reference of this lane: run mode unwraps + pads the pose refs (NMPCNavControlDiff.cpp:104-118),
@@ -535,8 +548,12 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
             rec[R::UB] = ubd;
             rec[R::TL] = tl;
             rec[R::TU] = tu;
-            rec[R::LL] = P.mu0 / tl;
-            rec[R::LU] = P.mu0 / tu;
+            // cold: t lambda = mu0; warm: the previous multipliers, floored at kappa / t
+            const float ll0 = warm ? fmaxf(lp.x, P.warm_kappa / tl) : P.mu0 / tl;
+            const float lu0 = warm ? fmaxf(lp.y, P.warm_kappa / tu) : P.mu0 / tu;
+            rec[R::LL] = ll0;
+            rec[R::LU] = lu0;
+            sum_c0 += ll0 * tl + lu0 * tu;
         }
 #pragma unroll
         for (int i = 0; i < NGV; i++) rec[R::GV + i] = (k < N && lv) ? g[i] : 0.0f;
@@ -576,6 +593,7 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
     STAMP(1);
     const int m = N * NU + N * M::NBX;
     const float inv_m2 = 0.5f / (float)m;
+    sum_c0 = row_sum16(lv ? sum_c0 : 0.0f);
 
     // dx_{k+1} (lane NU+i) = sum_v G_k[i][v] dz_v: NGV row sums over the stored columns + the constant rows
     auto dyn = [&](const float (&rc)[RS], float dzv) -> float {
@@ -654,8 +672,8 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
     float exit_res[3] = {0.0f, 0.0f, 0.0f};
     float alpha = 0.0f, sigma_mu = 0.0f, eta = 0.0f, mu_prev = 3.0e38f;
     // SD: centring target of the next direction, built into P1's rhs. The first direction: sigma = sd_hi (no
-    // previous step) and mu = mu0 exactly (every bounded pair starts at t * lambda = mu0, P0)
-    float tg_rhs = P.sd_hi * P.mu0;
+    // previous step) and the initial point's mu (P0; mu0 for a cold start, where every pair has t lambda = mu0)
+    float tg_rhs = P.sd_hi * sum_c0 * inv_m2;
     for (int it = 0;; it++) {
         // P1 (backward): apply the previous step, residuals, adjoint, fp64 classic Riccati factorisation,
         // predictor rhs
@@ -1036,6 +1054,7 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
         if (a.status) a.status[inst] = status;
         if (a.qp_iter) a.qp_iter[inst] = it_done;
         if (a.iter_key) a.iter_key[inst] = it_done;
+        if (a.warm) a.warm[inst] = (P.warm && status == 0) ? 1 : 0;
         if (a.qp_res) {
 #pragma unroll
             for (int j = 0; j < 3; j++) a.qp_res[(size_t)j * Bn + inst] = exit_res[j];

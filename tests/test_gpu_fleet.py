@@ -135,17 +135,14 @@ def test_stream_groups_decoupled_bit_identical(built, model, N, B, idx):
 
 
 def _restore(f, st):
-    xv, uv, cv = f.solver.state()
-    xv.copy_from(st["X"])
-    uv.copy_from(st["U"])
-    cv.copy_from(st["C"])
+    f.solver.restore_state(st["handle"])  # iterate, carried refs and the IPM warm-start state
     for k in ("pose", "vel", "traj", "tlen"):
         getattr(f, k).copy_(st[k])
 
 
 def _save(f):
-    xv, uv, cv = f.solver.state()
-    return dict(X=xv.to_tensor(), U=uv.to_tensor(), C=cv.to_tensor(), pose=f.pose.clone(), vel=f.vel.clone(),
+    X, U, C = (v.to_tensor() for v in f.solver.state())
+    return dict(handle=f.solver.save_state(), X=X, U=U, C=C, pose=f.pose.clone(), vel=f.vel.clone(),
                 traj=f.traj.clone(), tlen=f.tlen.clone())
 
 
