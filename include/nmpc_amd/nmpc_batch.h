@@ -60,7 +60,7 @@ typedef struct nmpc_model_params {
      * the IPM path is shorter). 0 gives acados' cold start every tick. Reset robots and nmpc_batch_init_iterate
      * start cold. The capsule ABI always starts cold (its capsules do not own a slot). */
     int qp_warm_start;
-    double qp_warm_kappa; /* 0.05 */
+    double qp_warm_kappa; /* diff 0.2, omni4 / tric 0.01 */
 } nmpc_model_params;
 
 enum { NMPC_IPM_MEHROTRA = 0, NMPC_IPM_SINGLE = 1 };

@@ -247,9 +247,11 @@ int nmpc_model_params_default(int model, int N, nmpc_model_params* prm)
     prm->qp_sigma_lo = 0.01;
     prm->qp_sigma_hi = 0.5;
     // warm-started bound multipliers, floored at kappa / t: steady-state closed loop, emulator on 4096 robots of
-    // real bench ticks: mean 10.9 -> 9.3 single-direction iterations, tail 22 -> 19 (DESIGN.md "Algorithm")
+    // real bench ticks: mean 10.9 -> 9.3 single-direction iterations, tail 22 -> 19 (DESIGN.md "Algorithm").
+    // kappa per model from same-box A/B runs (profiles/r02/ab/warm.txt): diff 0.2 (as fast as 0.05, shorter
+    // worst case: 29 against 39 iterations), omni4 and tric 0.01 (+7 % / +4 % against 0.05)
     prm->qp_warm_start = 1;
-    prm->qp_warm_kappa = 0.05;
+    prm->qp_warm_kappa = (model == NMPC_MODEL_DIFF2AMR) ? 0.2 : 0.01;
     return NMPC_OK;
 }
 

@@ -161,8 +161,10 @@ def test_params_struct_layout_and_ipm_options(built):
     assert L.nmpc_model_params_default(0, 40, ctypes.byref(prm)) == 0
     assert bytes(buf[n:]) == b"\xab" * 64
     assert prm.qp_ipm == 1 and (prm.qp_sigma_lo, prm.qp_sigma_hi) == (0.01, 0.5)
+    assert prm.qp_warm_start == 1 and prm.qp_warm_kappa == 0.2
     h = ctypes.c_void_p()
-    for field, val in (("qp_ipm", 2), ("qp_sigma_lo", 0.0), ("qp_sigma_hi", 1.5)):
+    for field, val in (("qp_ipm", 2), ("qp_sigma_lo", 0.0), ("qp_sigma_hi", 1.5), ("qp_warm_start", 3),
+                       ("qp_warm_kappa", 0.0)):
         bad = _lib.ModelParams()
         assert L.nmpc_model_params_default(0, 20, ctypes.byref(bad)) == 0
         setattr(bad, field, val)
