@@ -101,6 +101,14 @@ int nmpc_batch_solve(nmpc_batch* b, int B, const float* x0, const float* yref, i
                      const unsigned char* reset, float* u0, float* x1, float* xtraj, float* utraj, int* status,
                      int* qp_iter, float* qp_res, void* stream);
 
+/* nmpc_batch_solve with the iterate held by the caller instead of the handle: xbar [(N+1)*NX][ld] and
+ * ubar [N*NU][ld] (device) are read as the linearisation point and overwritten with the new iterate (a failed solve
+ * keeps its own). Used by the capsule ABI, whose iterate travels with each call; the warm-start records are still
+ * the handle's (slot i = instance i). */
+int nmpc_batch_solve_iterate(nmpc_batch* b, int B, const float* x0, const float* yref, int ny_in, const float* We,
+                             const unsigned char* reset, float* xbar, float* ubar, int ld, int* status, int* qp_iter,
+                             float* qp_res, void* stream);
+
 /* Batched NMPCNavControl*::run(): pre-solve + SQP-RTI + post-solve for B robots.
  *   pose  [3][B] {x, y, theta}; vel [3][B] {v, vn, w}; steer [B] (tric; NULL = 0)
  *   traj  [N+1][3][B] reference poses; traj_len [B] poses valid per robot (NULL = N+1; padded with the

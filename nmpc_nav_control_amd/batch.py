@@ -138,6 +138,25 @@ class BatchSolver:
             _ptr(qp_iter, I32, (B,), "qp_iter"), _ptr(qp_res, F32, (3, B), "qp_res"), _stream(stream)),
             "nmpc_batch_solve")
 
+    def solve_iterate(self, x0, yref, xbar, ubar, We=None, reset=None, status=None, qp_iter=None, qp_res=None,
+                      stream=None):
+        """nmpc_batch_solve with a caller-held iterate: xbar [(N+1)*NX][ld], ubar [N*NU][ld] are read and overwritten
+        with the new iterate in place (nmpc_batch_solve_iterate)."""
+        B = x0.shape[1]
+        if not 0 <= B <= self.capacity:
+            raise ValueError(f"batch {B} exceeds the capacity {self.capacity}")
+        ld = xbar.shape[1]
+        if ubar.shape[1] != ld:
+            raise ValueError("xbar and ubar need the same leading dimension")
+        ny_in = yref.shape[1]
+        N, nx, nu = self.N, self.nx, self.nu
+        check(lib().nmpc_batch_solve_iterate(
+            self._h, B, _ptr(x0, F32, (nx, B), "x0"), _ptr(yref, F32, (N + 1, ny_in, B), "yref"), ny_in,
+            _ptr(We, F32, (nx, B), "We"), _ptr(reset, U8, (B,), "reset"), _ptr(xbar, F32, ((N + 1) * nx, ld), "xbar"),
+            _ptr(ubar, F32, (N * nu, ld), "ubar"), ld, _ptr(status, I32, (B,), "status"),
+            _ptr(qp_iter, I32, (B,), "qp_iter"), _ptr(qp_res, F32, (3, B), "qp_res"), _stream(stream)),
+            "nmpc_batch_solve_iterate")
+
     def run(self, pose, vel, traj, steer=None, traj_len=None, reset=None, cmd=None, u0=None, status=None,
             qp_iter=None, qp_res=None, stream=None):
         B = pose.shape[1]

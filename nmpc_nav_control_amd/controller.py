@@ -162,6 +162,12 @@ class NMPCNavControl:
         self._L.ocp_nlp_out_set(self._cfg, self._dims, self._out, stage, field.encode(),
                                 a.ctypes.data_as(ctypes.c_void_p))
 
+    def qp_iter(self):
+        """IPM iterations of the last solve (ocp_nlp_get "qp_iter")."""
+        n = ctypes.c_int()
+        self._L.ocp_nlp_get(self._solver, b"qp_iter", ctypes.byref(n))
+        return n.value
+
     def iterate(self):
         xs = np.stack([self._out_get(k, "x", self.nx) for k in range(self.N + 1)])
         us = np.stack([self._out_get(k, "u", self.nu) for k in range(self.N)])

@@ -12,10 +12,12 @@
 // copies the new iterate back. Device engines are shared per (model, N) and grow on demand.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <cstdint>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -46,6 +48,10 @@ struct nmpc_capsule_impl {
     std::vector<double> uniform_We;
     double time_tot = 0.0, time_lin = 0.0, time_qp = 0.0;
     int status = 5, qp_iter = 0, sqp_iter = 0;  // ACADOS_READY before the first solve
+    // IPM warm start: the capsule's bound multipliers stay in the engine slot of its last solve; they are used
+    // while the capsule still owns that slot, its last solve succeeded and no reset/create came in between
+    std::uint64_t uid = 0;
+    bool warm_ok = false;
     ocp_nlp_config config;
     ocp_nlp_dims dims;
     ocp_nlp_in in;
@@ -56,14 +62,16 @@ struct nmpc_capsule_impl {
 namespace {
 
 std::mutex g_mu;
+std::atomic<std::uint64_t> g_next_uid{1};
 
-// Device engine per (model, N): one batch handle plus one input and one output staging block. A call with n
-// capsules packs its inputs densely ([row][n] per array) into the pinned input block, which goes to the device in
-// ONE copy; the kernel's outputs sit in one device block that comes back in ONE copy. Every copy is async on the
-// launch stream and the call synchronises once (a single robot's solve: 12 synchronous copies -> 2 + 2 on-device).
-struct Blocks {  // float offsets of the arrays inside the blocks for n capsules
-    size_t x0, We, yref, xb, ub, in_floats;     // input block
-    size_t oxb, oub, ores, ost, oit, out_words;  // output block (status / qp_iter are int32 words)
+// Device engine per (model, N): one batch handle plus one I/O block, on the device and pinned on the host. A call
+// with n capsules packs its inputs densely ([row][n] per array) into the host block, which goes to the device in ONE
+// copy; the kernel reads the iterate from the block and overwrites it with the new one in place
+// (nmpc_batch_solve_iterate), next to its status / qp_iter / residual outputs, so that ONE copy brings everything
+// back. Every copy is async on the launch stream and the call synchronises once.
+struct Blocks {  // float offsets of the arrays inside the I/O block for n capsules
+    size_t x0, We, yref, xb, ub, in_floats;  // host -> device: [0, in_floats)
+    size_t ores, ost, oit, io_words;         // device -> host: [xb, io_words) (status / qp_iter are int32 words)
     Blocks(int n, int N, int nx, int nu, int ny)
     {
         x0 = 0;
@@ -72,26 +80,33 @@ struct Blocks {  // float offsets of the arrays inside the blocks for n capsules
         xb = yref + (size_t)(N + 1) * ny * n;
         ub = xb + (size_t)(N + 1) * nx * n;
         in_floats = ub + (size_t)N * nu * n;
-        oxb = 0;
-        oub = oxb + (size_t)(N + 1) * nx * n;
-        ores = oub + (size_t)N * nu * n;
+        ores = in_floats;
         ost = ores + (size_t)3 * n;
         oit = ost + (size_t)n;
-        out_words = oit + (size_t)n;
+        io_words = oit + (size_t)n;
     }
 };
+// Slot q of an engine keeps the scratch records (and so the bound multipliers) of the capsule that last solved
+// in it. owner[q] names that capsule; dev_warm[q] mirrors the handle's device warm flag of slot q (1 after a
+// successful solve, which is what the kernel leaves; 2 = unknown), so the flags only travel to the device when a
+// slot changes hands or a capsule was reset.
 struct Engine {
     nmpc_batch* batch = nullptr;
     int cap = 0;
-    float *din = nullptr, *dout = nullptr;  // device blocks, sized for cap capsules
-    float *hin = nullptr, *hout = nullptr;  // pinned host blocks of the same size
+    float *dio = nullptr, *hio = nullptr;  // the device I/O block, sized for cap capsules, and its pinned twin
+    unsigned char *dwarm = nullptr, *hwarm = nullptr;  // the handle's warm flags; pinned staging for them
+    std::vector<std::uint64_t> owner;
+    std::vector<unsigned char> dev_warm;
     ~Engine() { release(); }
     void release()
     {
         nmpc_batch_destroy(batch);
         batch = nullptr;
-        (void)hipFree(din); (void)hipFree(dout); (void)hipHostFree(hin); (void)hipHostFree(hout);
-        din = dout = hin = hout = nullptr;
+        (void)hipFree(dio); (void)hipHostFree(hio); (void)hipHostFree(hwarm);
+        dio = hio = nullptr;
+        dwarm = hwarm = nullptr;
+        owner.clear();
+        dev_warm.clear();
         cap = 0;
     }
 };
@@ -122,7 +137,9 @@ void codegen_defaults(nmpc_capsule_impl* c, const nmpc_codegen_desc& d)
 {
     nmpc_model_params_default(c->model, c->N, &c->prm);
     c->prm.terminal_hack = 0;  // the wrappers apply it themselves through cost_model_set(N, "W")
-    c->prm.qp_warm_start = 0;  // capsules share an engine's slots call by call: no per-robot multiplier history
+    // a capsule is one robot whose latency is its own IPM count, so its warm start floors the multipliers for the
+    // mean count (kappa 0.01; the batch default for diff, 0.2, is tuned for the slowest robot of a fleet)
+    c->prm.qp_warm_kappa = 0.01;
     c->prm.dt = d.tf / d.N;    // uniform time steps tf / N_codegen (ocp.solver_options.tf, N_horizon)
     std::memcpy(c->prm.p, d.p, sizeof(d.p));
     std::memcpy(c->prm.lbx, d.lbx, sizeof(d.lbx));
@@ -172,6 +189,7 @@ nmpc_capsule_impl* new_impl(int model)
     c->out.total_cost = 0.0;
     c->out.sqp_iter = 0;
     c->solver.impl = c;
+    c->uid = g_next_uid++;
     return c;
 }
 
@@ -191,6 +209,7 @@ int impl_create(nmpc_capsule_impl* c, int N, const nmpc_codegen_desc& d)
     c->created = true;
     c->uniform_dirty = true;
     c->status = 5;
+    c->warm_ok = false;
     return 0;
 }
 
@@ -319,14 +338,16 @@ int ensure_engine(Engine& e, const nmpc_model_params& prm, int n, std::string& w
     hipError_t r = hipSuccess;
     const Blocks bl(cap, N, nx, nu, ny);
     static_assert(sizeof(int) == sizeof(float), "int32 words in the float output block");
-    if ((r = hipMalloc(&e.din, sizeof(float) * bl.in_floats)) != hipSuccess ||
-        (r = hipMalloc(&e.dout, sizeof(float) * bl.out_words)) != hipSuccess ||
-        (r = hipHostMalloc(&e.hin, sizeof(float) * bl.in_floats)) != hipSuccess ||
-        (r = hipHostMalloc(&e.hout, sizeof(float) * bl.out_words)) != hipSuccess) {
+    if ((r = hipMalloc(&e.dio, sizeof(float) * bl.io_words)) != hipSuccess ||
+        (r = hipHostMalloc(&e.hio, sizeof(float) * bl.io_words)) != hipSuccess ||
+        (r = hipHostMalloc(&e.hwarm, (size_t)cap)) != hipSuccess) {
         why = hipGetErrorString(r);
         e.release();
         return -1;
     }
+    nmpc_batch_warm_state(e.batch, &e.dwarm, nullptr, nullptr);
+    e.owner.assign(cap, 0);
+    e.dev_warm.assign(cap, 0);  // nmpc_batch_create zeroes the flags
     e.cap = cap;
     return 0;
 }
@@ -343,14 +364,20 @@ void solve_group(std::vector<nmpc_capsule_impl*>& cs, std::vector<Packed>& ps, c
     std::string why;
     auto fail_all = [&](const std::string& msg) {
         log_err("solve", msg);
-        for (int i : idx) cs[i]->status = 4;
+        for (int i : idx) {
+            cs[i]->status = 4;
+            cs[i]->warm_ok = false;
+        }
+        for (int q = 0; q < (int)e.owner.size() && q < n; q++) {
+            e.owner[q] = 0;
+            e.dev_warm[q] = 2;
+        }
     };
     if (ensure_engine(e, ps[idx[0]].prm, n, why)) return fail_all(why);
     const auto ta = std::chrono::steady_clock::now();
-    const int S = e.cap;
     const Blocks bl(n, N, nx, nu, ny);
-    float *hx0 = e.hin + bl.x0, *hyref = e.hin + bl.yref, *hWe = e.hin + bl.We, *hxb = e.hin + bl.xb,
-          *hub = e.hin + bl.ub;
+    float *hx0 = e.hio + bl.x0, *hyref = e.hio + bl.yref, *hWe = e.hio + bl.We, *hxb = e.hio + bl.xb,
+          *hub = e.hio + bl.ub;
     {
         std::vector<const double*> x0s(n), yrefs(n), Wes(n), xbs(n), ubs(n);
         for (int q = 0; q < n; q++) {
@@ -368,33 +395,31 @@ void solve_group(std::vector<nmpc_capsule_impl*>& cs, std::vector<Packed>& ps, c
         to_soa(hub, n, (size_t)N * nu, ubs);
     }
     const auto tb = std::chrono::steady_clock::now();
-    float *dxb, *dub;
-    nmpc_batch_state(e.batch, &dxb, &dub, nullptr, nullptr);
-    // one host->device copy of the input block; the iterate then moves from its dense [row][n] rows into the
-    // [row][S] resident state by device-side 2-D copies (stream order: the solve's outputs overwrite nothing
-    // these copies still read, since the output block is separate)
     hipError_t r = hipSuccess;
     const hipStream_t st = nullptr;
-    float* const dout = e.dout;
-    if ((r = hipMemcpyAsync(e.din, e.hin, sizeof(float) * bl.in_floats, hipMemcpyHostToDevice, st)) != hipSuccess ||
-        (r = hipMemcpy2DAsync(dxb, sizeof(float) * S, e.din + bl.xb, sizeof(float) * n, sizeof(float) * n,
-                              (size_t)(N + 1) * nx, hipMemcpyDeviceToDevice, st)) != hipSuccess ||
-        (r = hipMemcpy2DAsync(dub, sizeof(float) * S, e.din + bl.ub, sizeof(float) * n, sizeof(float) * n,
-                              (size_t)N * nu, hipMemcpyDeviceToDevice, st)) != hipSuccess)
+    float* const dio = e.dio;
+    bool flags_differ = false;
+    for (int q = 0; q < n; q++) {
+        const nmpc_capsule_impl* c = cs[idx[q]];
+        e.hwarm[q] = (e.owner[q] == c->uid && c->warm_ok) ? 1 : 0;
+        flags_differ |= e.hwarm[q] != e.dev_warm[q];
+    }
+    if (flags_differ && (r = hipMemcpyAsync(e.dwarm, e.hwarm, (size_t)n, hipMemcpyHostToDevice, st)) != hipSuccess)
+        return fail_all(hipGetErrorString(r));
+    if ((r = hipMemcpyAsync(dio, e.hio, sizeof(float) * bl.in_floats, hipMemcpyHostToDevice, st)) != hipSuccess)
         return fail_all(hipGetErrorString(r));
     const auto t1 = std::chrono::steady_clock::now();
-    if (nmpc_batch_solve(e.batch, n, e.din + bl.x0, e.din + bl.yref, ny, e.din + bl.We, nullptr, nullptr, nullptr,
-                         dout + bl.oxb, dout + bl.oub, reinterpret_cast<int*>(dout + bl.ost),
-                         reinterpret_cast<int*>(dout + bl.oit), dout + bl.ores, st) != NMPC_OK)
+    if (nmpc_batch_solve_iterate(e.batch, n, dio + bl.x0, dio + bl.yref, ny, dio + bl.We, nullptr, dio + bl.xb,
+                                 dio + bl.ub, n, reinterpret_cast<int*>(dio + bl.ost),
+                                 reinterpret_cast<int*>(dio + bl.oit), dio + bl.ores, st) != NMPC_OK)
         return fail_all(nmpc_last_error());
-    if ((r = hipMemcpyAsync(e.hout, dout, sizeof(float) * bl.out_words, hipMemcpyDeviceToHost, st)) != hipSuccess ||
+    if ((r = hipMemcpyAsync(e.hio + bl.xb, dio + bl.xb, sizeof(float) * (bl.io_words - bl.xb), hipMemcpyDeviceToHost,
+                            st)) != hipSuccess ||
         (r = hipStreamSynchronize(st)) != hipSuccess)
         return fail_all(hipGetErrorString(r));
-    const float* const hres = e.hout + bl.ores;
-    const int* const hst = reinterpret_cast<const int*>(e.hout + bl.ost);
-    const int* const hit = reinterpret_cast<const int*>(e.hout + bl.oit);
-    hxb = e.hout + bl.oxb;
-    hub = e.hout + bl.oub;
+    const float* const hres = e.hio + bl.ores;
+    const int* const hst = reinterpret_cast<const int*>(e.hio + bl.ost);
+    const int* const hit = reinterpret_cast<const int*>(e.hio + bl.oit);
     const auto t2 = std::chrono::steady_clock::now();
     const double tt = std::chrono::duration<double>(t2 - t0).count();
     const double tq = std::chrono::duration<double>(t2 - t1).count();
@@ -414,6 +439,9 @@ void solve_group(std::vector<nmpc_capsule_impl*>& cs, std::vector<Packed>& ps, c
         c->time_tot = tt;
         c->time_qp = tq;
         c->time_lin = 0.0;
+        c->warm_ok = hst[q] == 0;
+        e.owner[q] = c->uid;
+        e.dev_warm[q] = hst[q] == 0 ? 1 : 0;  // the kernel's epilogue: warm = qp_warm_start && status == 0
         xbs[q] = hst[q] == 0 ? c->xbar.data() : nullptr;
         ubs[q] = hst[q] == 0 ? c->ubar.data() : nullptr;
     }
@@ -687,11 +715,12 @@ int nmpc_capsule_create(nmpc_solver_capsule* capsule, const nmpc_codegen_desc* d
 
 int nmpc_capsule_reset(nmpc_solver_capsule* capsule, int reset_qp_solver_mem)
 {
-    (void)reset_qp_solver_mem;  // the IPM cold-starts every QP: no QP memory to reset
+    (void)reset_qp_solver_mem;  // the only QP memory is the warm-start multipliers, dropped either way
     if (!capsule || !capsule->impl || !capsule->impl->created) return 1;
     nmpc_capsule_impl* c = capsule->impl;
     std::fill(c->xbar.begin(), c->xbar.end(), 0.0);
     std::fill(c->ubar.begin(), c->ubar.end(), 0.0);
+    c->warm_ok = false;  // the next solve starts the IPM cold, like a fresh capsule
     return 0;
 }
 

@@ -399,6 +399,35 @@ int nmpc_batch_solve(nmpc_batch* b, int B, const float* x0, const float* yref, i
     return hip_err(launch(b, a, kModeSolve, (hipStream_t)stream), "solve launch");
 }
 
+int nmpc_batch_solve_iterate(nmpc_batch* b, int B, const float* x0, const float* yref, int ny_in, const float* We,
+                             const unsigned char* reset, float* xbar, float* ubar, int ld, int* status, int* qp_iter,
+                             float* qp_res, void* stream)
+{
+    if (!b) return set_err(NMPC_ERR_ARG, "batch is NULL");
+    if (B < 0 || B > b->capacity) return set_err(NMPC_ERR_ARG, "B out of range [0, capacity]");
+    if (B == 0) return NMPC_OK;
+    if (!x0 || !yref || !xbar || !ubar) return set_err(NMPC_ERR_ARG, "x0, yref, xbar and ubar are required");
+    if (ld < B) return set_err(NMPC_ERR_ARG, "ld < B");
+    if (ny_in < 1 || ny_in > b->ny) return set_err(NMPC_ERR_ARG, "ny_in out of range [1, NY]");
+    KArgs a;
+    std::memset(&a, 0, sizeof(a));
+    a.B = B;
+    a.stride = ld;
+    a.xbar = xbar;
+    a.ubar = ubar;
+    a.carried = b->carried;  // run mode only
+    a.scratch = b->scratch;
+    a.x0 = x0;
+    a.yref = yref;
+    a.ny_in = ny_in;
+    a.We = We;
+    a.reset = reset;
+    a.status = status;
+    a.qp_iter = qp_iter;
+    a.qp_res = qp_res;
+    return hip_err(launch(b, a, kModeSolve, (hipStream_t)stream), "solve launch");
+}
+
 int nmpc_batch_run(nmpc_batch* b, int B, const float* pose, const float* vel, const float* steer,
                    const float* traj, const int* traj_len, const unsigned char* reset, float* cmd, float* u0,
                    int* status, int* qp_iter, float* qp_res, void* stream)

@@ -110,6 +110,53 @@ def test_batch_solve_equals_individual(built):
         np.testing.assert_allclose(xa, xb_, atol=1e-6)
 
 
+def _set_tick(c, x0, yref):
+    c._cset(0, "lbx", x0)
+    c._cset(0, "ubx", x0)
+    for k in range(N + 1):
+        c._wset(k, "yref", yref[k, : (c.nx if k == N else c.ny)])
+
+
+def test_capsule_warm_start_and_reset(built):
+    """A capsule solved tick after tick starts its IPM from its own previous multipliers (qp_warm_start): a fresh
+    capsule given the same inputs and iterate starts cold, in the same launch, and reaches the same QP solution.
+    After reset the next solve is cold again: bit-identical to a fresh capsule's solve from a zero iterate."""
+    a = make("diff")[0]
+    o = Oracle("diff", N)
+    x0 = np.array([0.05, -0.02, 2.9, 0.1, 0.05, 0.0, 0.0])
+    yref = np.zeros((N + 1, a.ny))
+    it_warm = it_cold = 0
+    for tick in range(10):
+        for k, p in enumerate(path(tick, N + 1)):
+            yref[k, :3] = [p.x, p.y, np.unwrap([x0[2], p.theta])[1]]
+        cold = make("diff")[0]
+        xs, us = a.iterate()
+        for k in range(N + 1):
+            cold.out_set(k, "x", xs[k])
+        for k in range(N):
+            cold.out_set(k, "u", us[k])
+        for c in (a, cold):
+            _set_tick(c, x0, yref)
+        assert (batch_solve([a, cold]) == 0).all()
+        ua, uc = a.iterate()[1], cold.iterate()[1]
+        np.testing.assert_allclose(ua[0], uc[0], atol=2e-4)
+        if tick > 0:
+            it_warm += a.qp_iter()
+            it_cold += cold.qp_iter()
+        x0 = o.rk4(x0, ua[0], 1 / 40)[0]
+    assert it_warm < it_cold, (it_warm, it_cold)
+    assert a.reset_mpc()
+    fresh = make("diff")[0]
+    fresh.reset_mpc()
+    for c in (a, fresh):
+        _set_tick(c, x0, yref)
+        c._solve()
+        assert c.status == 0
+    assert a.qp_iter() == fresh.qp_iter()
+    np.testing.assert_array_equal(a.iterate()[1], fresh.iterate()[1])
+    np.testing.assert_array_equal(a.iterate()[0], fresh.iterate()[0])
+
+
 def test_unsupported_ocp_data_rejected_and_recovered(built):
     """The shim rejects OCP data the batched kernel does not implement (status 4 -> the wrapper's exception) and
     re-validates after every setter: the cached stage-uniform data must not hide a later change either way."""

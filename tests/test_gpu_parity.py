@@ -87,6 +87,44 @@ def test_solve_matches_oracle(built, ipm, model, N, B, ticks):
     assert qp_iter.cpu().numpy().max() < 50
 
 
+def test_solve_iterate_equals_resident_solve(built):
+    """nmpc_batch_solve_iterate (the capsule ABI's entry: the iterate in caller memory with its own leading
+    dimension, updated in place) equals nmpc_batch_solve on the handle's resident iterate bit for bit, on a cold
+    tick and on the warm-started tick after it."""
+    N, B = 40, 13
+    o, rec = oracle_closed_loop("diff", N, B, 2)
+    nx, nu = o.nx, o.nu
+    a, b = make_solver("diff", N, 64, "single"), make_solver("diff", N, 64, "single")
+    upload_iterate(a, [r[3] for r in rec], [r[4] for r in rec])
+    ld = B + 3
+    xb = torch.zeros((N + 1) * nx, ld, device=DEV)
+    ub = torch.zeros(N * nu, ld, device=DEV)
+    xb[:, :B] = t(np.stack([r[3] for r in rec]).reshape(B, -1).T)
+    ub[:, :B] = t(np.stack([r[4] for r in rec]).reshape(B, -1).T)
+    x0 = t(np.stack([r[0] for r in rec]).T)
+    yref = t(np.stack([r[1] for r in rec]).transpose(1, 2, 0))
+    We = t(np.stack([r[2] for r in rec]).T)
+    for tick in range(2):
+        outs = []
+        for s in (a, b):
+            st = torch.full((B,), -7, dtype=torch.int32, device=DEV)
+            it = torch.zeros(B, dtype=torch.int32, device=DEV)
+            res = torch.zeros(3, B, device=DEV)
+            if s is a:
+                s.solve(x0, yref, We=We, status=st, qp_iter=it, qp_res=res)
+            else:
+                s.solve_iterate(x0, yref, xb, ub, We=We, status=st, qp_iter=it, qp_res=res)
+            outs.append((st, it, res))
+        torch.cuda.synchronize()
+        assert (outs[0][0] == 0).all()
+        for u, v in zip(*outs):
+            assert torch.equal(u, v)
+        xv, uv, _ = a.state()
+        assert torch.equal(xv.to_tensor()[:, :B], xb[:, :B])
+        assert torch.equal(uv.to_tensor()[:, :B], ub[:, :B])
+        assert not xb[:, B:].any() and not ub[:, B:].any()  # the padding columns are untouched
+
+
 @pytest.mark.parametrize("ipm", sorted(IPMS))
 @pytest.mark.parametrize("model", MODELS)
 @pytest.mark.parametrize("resets", [False, True])
