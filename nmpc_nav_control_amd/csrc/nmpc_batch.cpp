@@ -25,6 +25,7 @@ struct nmpc_batch {
     float* scratch = nullptr;
     int sched = NMPC_SCHED_AUTO;
     int n_simd = 1024;           // SIMDs of the device (4 per CU)
+    int split_max = 256;         // launches of at most this many robots run one wave per robot (KArgs::split)
     int* iter_key = nullptr;     // [capacity] last executed IPM iterations per robot (written by the team kernel)
     int* order = nullptr;        // [capacity] team slot -> robot
     unsigned char* warm = nullptr;  // [capacity] the robot's last solve succeeded: its scratch records hold its
@@ -118,6 +119,9 @@ hipError_t schedule(nmpc_batch* b, KArgs& a, hipStream_t s)
     a.iter_key = b->iter_key;
     a.warm = b->warm;
     a.dense = ((a.B + 3) / 4 > b->n_simd) ? 1 : 0;  // 4 teams per wave
+    // small batches leave most of the chip idle: one wave per robot, whose spare rows integrate P0's stages
+    a.split = (!a.dense && a.B <= b->split_max) ? 1 : 0;
+    if (a.split) return hipSuccess;  // one robot per wave: nothing to place
     int layout = b->sched;
     if (layout == NMPC_SCHED_AUTO) layout = a.dense ? NMPC_SCHED_SORTED : NMPC_SCHED_OFF;
     if (layout == NMPC_SCHED_OFF) return hipSuccess;
@@ -292,6 +296,7 @@ int nmpc_batch_create(const nmpc_model_params* prm, int capacity, nmpc_batch** o
         for (int i = 0; i < 5; i++)
             if (std::strcmp(sv, names[i]) == 0) b->sched = i;
     }
+    if (const char* v = std::getenv("NMPC_AMD_SPLIT_MAX")) b->split_max = std::atoi(v);  // A/B: 0 = never split
     const int N = prm->N;
     const size_t S = (size_t)capacity;
     hipError_t e;

@@ -39,6 +39,8 @@ __device__ unsigned long long g_stamps[256][2 + 4 * kStampIts];
     } while (0)
 // fine-grained stamps inside one P1 stage body (iteration 2, stage 20)
 __device__ unsigned long long g_stamps_p1[256][8];
+// end of the split launches' stage-parallel P0 part (row 0 of the first robot of each group of 4)
+__device__ unsigned long long g_stamps_pa[256];
 // end of the corrector backward sweep (C1) of iteration it, first team of the first 256 waves
 __device__ unsigned long long g_stamps_c1[256][kStampIts];
 #define STAMPC1()                                                                                                \
@@ -323,7 +325,10 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
     constexpr int NX = M::NX, NU = M::NU, NV = R::NV, NGV = R::NGV, RS = R::RS;
     constexpr bool QM = rec_quad_major<NV>();
     const int gt = blockIdx.x * blockDim.x + threadIdx.x;
-    const int team = gt >> 4;
+    // split launches (a.split: small batches on an otherwise idle chip): one 256-lane block per robot. Row 0 of
+    // the block is the robot's team; rows 1-15 share the stage-parallel part of P0 with it and leave.
+    const int team = a.split ? (int)blockIdx.x : (gt >> 4);
+    const int row = a.split ? (int)(threadIdx.x >> 4) : 0;
     const int r = gt & 15;
     if (team >= a.B) return;  // whole DPP rows leave together
     const int N = P.N;
@@ -337,7 +342,10 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
     const int cx = is_x ? xcomp<M>(xi) : -1;
     const bool has_b = is_u || cx >= 0;  // bounded slot: every input (idxbu = all), states on idxbx
     const float sc = P.dt;
-    const float h_stage = is_u ? sc * P.W[NX + r] : (is_x ? sc * P.W[xi] : 0.0f);
+    // this lane's stage weight, read once: indexed by the lane, the W entries are vector loads from the kernel
+    // arguments, and inside P0's loop each one waited on vmcnt(0), i.e. on the previous stage's record stores
+    const float w_lane = is_u ? P.W[NX + r] : (is_x ? P.W[xi] : 0.0f);
+    const float h_stage = sc * w_lane;
     float lo_b = 0.0f, hi_b = 0.0f;
 #pragma unroll
     for (int q = 0; q < NU; q++)
@@ -374,11 +382,16 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
     // team's LDS slice; the rest is padded with the path end (:58-63). The team's 16 lanes then evaluate the
     // poses 16 at a time (atan2 and all), so no lane waits in a divergent emit. A team's lanes share the wave
     // and LDS accesses of a wave retire in order, so P0 reads the poses from LDS directly afterwards.
-    extern __shared__ double s_path[];  // path mode: [16 teams][N+1] parameters, then [16][N+1][3] float poses
+    // LDS: path mode and split run launches: [teams][N+1] path parameters, then [teams][N+1][3] float poses
+    // (split: one team); split launches then the serial P0 pass's stage inputs
+    extern __shared__ double s_path[];
     const bool path = (mode == kModeRun) && a.segs;
-    const int tslot = threadIdx.x >> 4;
-    float* const my_traj = reinterpret_cast<float*>(s_path + 16 * (N + 1)) + (size_t)tslot * (N + 1) * 3;
-    if (path) {
+    const bool traj_lds = path || (a.split && mode == kModeRun);
+    const int nslot = a.split ? 1 : 16;
+    const int tslot = a.split ? 0 : (int)(threadIdx.x >> 4);
+    float* const my_traj = reinterpret_cast<float*>(s_path + nslot * (N + 1)) + (size_t)tslot * (N + 1) * 3;
+    float* const s_stg = reinterpret_cast<float*>(s_path) + (traj_lds ? (size_t)nslot * (N + 1) * 5 : 0);
+    if (path && row == 0) {
         double* const my_u = s_path + (size_t)tslot * (N + 1);
         const nmpc_path_segment* S = a.segs + (size_t)inst * a.seg_stride;
         const int n = a.nseg[inst];
@@ -428,6 +441,77 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
     if (is_x) we_lane = (mode != kModeRun && a.We) ? a.We[(size_t)xi * Bn + inst] : P.We[xi];
 
     // ---- P0: linearisation (lane v: nominal step + column v), gradient, bounds, feasible initial iterate --
+    // Split launches: the RK4 integrations and every global load of P0 do not depend on each other; only the
+    // initial-iterate simulation (and the reference unwrap) is a recursion over the stages. The wave's four
+    // rows take stages row, row + 4, ... and leave each lane's stage inputs in LDS ([k][field][lane], SF
+    // fields: zbar, yref entry, warm multipliers, defect b_k = xn_i - xbar_{k+1,i}, the NGV varying Jacobian
+    // rows) and run-mode reference poses in row 0's pose slice; row 0 then runs the serial pass from LDS only.
+    constexpr int SF = 5 + NGV;
+    if (a.split) {
+        const int len_a = (mode == kModeRun) ? ((a.traj_len && !path) ? a.traj_len[inst] : N + 1) : 0;
+        // a stage's global inputs, loaded one stage (of this row) ahead while the current one integrates
+        struct In {
+            float x[NX], u[NU], y, xnext, tq;
+            float2 l;
+        };
+        auto ld = [&](int k, In& v) {
+            const int kk = k <= N ? k : N;
+#pragma unroll
+            for (int j = 0; j < NX; j++) v.x[j] = XB(kk, j);
+            const int ku = kk < N ? kk : N - 1;
+#pragma unroll
+            for (int j = 0; j < NU; j++) v.u[j] = UBAR(ku, j);
+            v.xnext = XB(kk < N ? kk + 1 : N, xi);
+            v.y = 0.0f;
+            v.tq = 0.0f;
+            if (mode != kModeRun) {
+                const int j = is_u ? NX + r : xi;
+                v.y = (lv && j < a.ny_in) ? a.yref[((size_t)kk * a.ny_in + j) * Bn + inst] : 0.0f;
+            } else if (!path && r < 3) {
+                const int kt = kk < len_a ? kk : (len_a > 0 ? len_a - 1 : 0);
+                v.tq = a.traj[((size_t)kt * 3 + r) * Bn + inst];
+            }
+            v.l = warm ? *reinterpret_cast<const float2*>(tbase + (size_t)kk * KS + rec_off<RS, QM>(R::LL))
+                       : make_float2(0.0f, 0.0f);
+        };
+        In cur, nxt;
+        ld(row, cur);
+        for (int k = row; k <= N; k += 16) {
+            ld(k + 16, nxt);
+            if (mode == kModeRun && !path && r < 3) my_traj[k * 3 + r] = cur.tq;
+            float xn[NX], g[NX];
+#pragma unroll
+            for (int i = 0; i < NX; i++) { xn[i] = 0.0f; g[i] = 0.0f; }
+            float bk = 0.0f;
+            if (k < N) {
+                rk4_column<M>(cur.x, cur.u, P, lv ? r : NU, xn, g);
+#pragma unroll
+                for (int i = 0; i < NX; i++)
+                    if (is_x && xi == i) bk = xn[i] - cur.xnext;
+            }
+            float zb = 0.0f;
+#pragma unroll
+            for (int j = 0; j < NU; j++)
+                if (r == j) zb = cur.u[j];
+#pragma unroll
+            for (int j = 0; j < NX; j++)
+                if (is_x && xi == j) zb = cur.x[j];
+            float* const st = s_stg + (size_t)k * SF * 16 + r;
+            st[0] = zb;
+            st[16] = cur.y;
+            st[32] = cur.l.x;
+            st[48] = cur.l.y;
+            st[64] = bk;
+#pragma unroll
+            for (int i = 0; i < NGV; i++) st[(5 + i) * 16] = g[i];
+            cur = nxt;
+        }
+        __syncthreads();  // every row's stage inputs are in LDS
+        if (row != 0) return;
+#ifdef NMPC_STAMPS
+        if (r == 0 && (team & 3) == 0 && (team >> 2) < 256) g_stamps_pa[team >> 2] = __builtin_amdgcn_s_memtime();
+#endif
+    }
     const int len = (mode == kModeRun) ? ((a.traj_len && !path) ? a.traj_len[inst] : N + 1) : 0;
     float ref_x = 0.0f, ref_y = 0.0f, ref_t = pose_th, prv_x = 0.0f, prv_y = 0.0f, prv_t = 0.0f;
     // Iterate rows are read two stages ahead (every lane of a team reads the same addresses: one request per
@@ -476,20 +560,20 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
         return warm ? *reinterpret_cast<const float2*>(tbase + (size_t)(k <= N ? k : N) * KS + rec_off<RS, QM>(R::LL))
                     : make_float2(0.0f, 0.0f);
     };
-    float2 lprev = load_l(0);
-    for (int k = 0; k <= N; k++) {
-        const float2 lp = lprev;
-        lprev = load_l(k + 1);
-        float xb2[NX], ub2[NU], tr2[3];
-        load_row(k + 2, xb2, ub2, tr2);  // two stages ahead (clamped)
+    // One stage of the serial pass: reference (run mode: unwrap + pad), cost gradient, bounds / slacks /
+    // multipliers, the stage record, and the dynamics-feasible initial state of the next stage. Inputs: this
+    // lane's iterate entry zbar, its yref entry (solve mode) or the stage's pose ref (run mode), its warm
+    // multipliers, the NGV varying Jacobian rows of its column and its defect b_k.
+    auto p0_body = [&](int k, float zbar, float yr_in, const float (&trk)[3], float2 lp, const float (&g)[NX],
+                       float bk) __attribute__((always_inline)) {
         // stage reference of this lane: run mode unwraps + pads the pose refs (NMPCNavControlDiff.cpp:104-118),
         // entries >= 3 of yref are left at zero
-        float yr = 0.0f;
+        float yr = yr_in;
         if (mode == kModeRun) {
             if (k < len) {
-                ref_x = tr[0];
-                ref_y = tr[1];
-                float th = tr[2];
+                ref_x = trk[0];
+                ref_y = trk[1];
+                float th = trk[2];
                 const float d = th - ref_t;
                 if (d > kPi) th -= 2.0f * kPi;
                 else if (d < -kPi) th += 2.0f * kPi;
@@ -497,35 +581,21 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
             }
             if (k == N - 1) { prv_x = ref_x; prv_y = ref_y; prv_t = ref_t; }
             yr = (is_x && xi == 0) ? ref_x : ((is_x && xi == 1) ? ref_y : ((is_x && xi == 2) ? ref_t : 0.0f));
-        } else {
-            const int j = is_u ? NX + r : xi;
-            yr = (lv && j < a.ny_in) ? a.yref[((size_t)k * a.ny_in + j) * Bn + inst] : 0.0f;
         }
         float rec[RS];
 #pragma unroll
         for (int f = 0; f < RS; f++) rec[f] = 0.0f;
-        float xn[NX], g[NX];
-#pragma unroll
-        for (int i = 0; i < NX; i++) { xn[i] = 0.0f; g[i] = 0.0f; }
-        if (k < N) rk4_column<M>(xb, ub, P, lv ? r : NU, xn, g);
         const bool vu = is_u && k < N, vx = is_x && k >= 1;
         const bool valid = vu || vx;
-        float zbar = 0.0f;
-#pragma unroll
-        for (int j = 0; j < NU; j++)
-            if (r == j) zbar = ub[j];
-#pragma unroll
-        for (int j = 0; j < NX; j++)
-            if (is_x && xi == j) zbar = xb[j];
         // gradient of the Gauss-Newton cost (stage weights scaled by dt, terminal weight unscaled)
-        if (vu) rec[R::GR] = sc * P.W[NX + r] * (zbar - yr);
+        if (vu) rec[R::GR] = sc * w_lane * (zbar - yr);
         if (vx) {
-            float w = sc * P.W[xi];
+            float w = sc * w_lane;
             if (k == N) {
                 w = we_lane;
                 if (mode == kModeRun && P.terminal_hack && xi < 3) {  // NMPCNavControlDiff.cpp:127-139
                     const bool eq = (ref_x == prv_x) && (ref_y == prv_y) && (ref_t == prv_t);
-                    w = (eq ? 100.0f : 1.0f) * P.W[xi];
+                    w = (eq ? 100.0f : 1.0f) * w_lane;
                     we_lane = w;
                 }
             }
@@ -563,23 +633,66 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
         if (k < N) {
             const float dzd = is_x ? dx : 0.0f;
             float nxt = dot_v<NX, NU>(0.0f, dzd, grow);
-            float bk = 0.0f;
 #pragma unroll
             for (int i = 0; i < NGV; i++) {
                 const float sr = row_sum16(lv ? g[i] * dzd : 0.0f);
                 if (xi == i) nxt = sr;
             }
+            dx = is_x ? nxt + bk : 0.0f;
+        }
+    };
+    if (a.split) {
+        // split launches: every input from LDS. A loop of its own: merged with the global-load loop below, the
+        // LDS values waited on vmcnt(0), i.e. on the previous stage's record stores (about one memory latency
+        // per stage). Nothing is in flight past this point but the loop's own stores: the waits the compiler
+        // would otherwise place inside the loop for the loads above (len, x0) wait on those stores too.
+        __builtin_amdgcn_s_waitcnt(0);
+        for (int k = 0; k <= N; k++) {
+            const float* const st = s_stg + (size_t)k * SF * 16 + r;
+            float trk[3] = {0.0f, 0.0f, 0.0f}, g[NX];
+            if (mode == kModeRun) {
+#pragma unroll
+                for (int j = 0; j < 3; j++) trk[j] = my_traj[k * 3 + j];
+            }
+#pragma unroll
+            for (int i = 0; i < NX; i++) g[i] = (i < NGV && k < N) ? st[(5 + (i < NGV ? i : 0)) * 16] : 0.0f;
+            p0_body(k, st[0], st[16], trk, make_float2(st[32], st[48]), g, st[64]);
+        }
+    } else {
+        float2 lprev = load_l(0);
+        for (int k = 0; k <= N; k++) {
+            const float2 lp = lprev;
+            lprev = load_l(k + 1);
+            float xb2[NX], ub2[NU], tr2[3];
+            load_row(k + 2, xb2, ub2, tr2);  // two stages ahead (clamped)
+            float yr = 0.0f;
+            if (mode != kModeRun) {
+                const int j = is_u ? NX + r : xi;
+                yr = (lv && j < a.ny_in) ? a.yref[((size_t)k * a.ny_in + j) * Bn + inst] : 0.0f;
+            }
+            float xn[NX], g[NX];
+#pragma unroll
+            for (int i = 0; i < NX; i++) { xn[i] = 0.0f; g[i] = 0.0f; }
+            if (k < N) rk4_column<M>(xb, ub, P, lv ? r : NU, xn, g);
+            float zbar = 0.0f;
+#pragma unroll
+            for (int j = 0; j < NU; j++)
+                if (r == j) zbar = ub[j];
+#pragma unroll
+            for (int j = 0; j < NX; j++)
+                if (is_x && xi == j) zbar = xb[j];
+            float bk = 0.0f;
 #pragma unroll
             for (int i = 0; i < NX; i++)
                 if (xi == i) bk = xn[i] - xb1[i];
-            dx = is_x ? nxt + bk : 0.0f;
+            p0_body(k, zbar, yr, tr, lp, g, bk);
+#pragma unroll
+            for (int j = 0; j < NX; j++) { xb[j] = xb1[j]; xb1[j] = xb2[j]; }
+#pragma unroll
+            for (int j = 0; j < NU; j++) { ub[j] = ub1[j]; ub1[j] = ub2[j]; }
+#pragma unroll
+            for (int j = 0; j < 3; j++) { tr[j] = tr1[j]; tr1[j] = tr2[j]; }
         }
-#pragma unroll
-        for (int j = 0; j < NX; j++) { xb[j] = xb1[j]; xb1[j] = xb2[j]; }
-#pragma unroll
-        for (int j = 0; j < NU; j++) { ub[j] = ub1[j]; ub1[j] = ub2[j]; }
-#pragma unroll
-        for (int j = 0; j < 3; j++) { tr[j] = tr1[j]; tr1[j] = tr2[j]; }
     }
     // e_r: places the diagonal D of M = D + G'PG with one multiply per entry instead of two selects (same-box
     // A/B: diff N=40 B=4096 +0.8 %, B=1024 +1.2 %, tric +0.6 %; profiles/r02/ab/onehot.txt)
@@ -1089,22 +1202,29 @@ template <class M>
 hipError_t launch_sqp_rti_team(const KParams& P, const KArgs& a, int mode, hipStream_t stream)
 {
     if (a.B <= 0) return hipSuccess;
-    const int block = 256;  // 16 teams
-    const long long threads = (long long)a.B * 16;
+    // split launches: one robot per 256-lane block, P0's stage inputs in LDS (41 KB for diff at N = 80); a
+    // horizon whose inputs do not fit runs unsplit
+    const size_t stg = (size_t)(P.N + 1) * 16 * (5 + M::NGV) * sizeof(float);
+    const size_t split_lds = stg + (mode == kModeRun ? (sizeof(double) + 3 * sizeof(float)) * (size_t)(P.N + 1) : 0);
+    KArgs as = a;
+    if (as.split && split_lds > 65536) as.split = 0;
+    const int block = 256;  // 16 teams, or 1 robot (split)
+    const long long threads = (long long)a.B * (as.split ? 256 : 16);
     const int grid = (int)((threads + block - 1) / block);
     // path mode: each team's N+1 path parameters and reference poses in LDS (16 teams x (N+1) x (8 + 12) B,
     // 26 KB at N = 80)
-    const size_t lds = (mode == kModeRun && a.segs) ? (sizeof(double) + 3 * sizeof(float)) * 16 * (size_t)(P.N + 1) : 0;
+    const size_t lds = as.split ? split_lds
+                                : ((mode == kModeRun && a.segs) ? (sizeof(double) + 3 * sizeof(float)) * 16 * (size_t)(P.N + 1) : 0);
     if (lds > 65536) return hipErrorInvalidValue;
     if (P.ipm == 1) {
         if (a.dense)
-            hipLaunchKernelGGL((k_sqp_rti_team<M, true, true>), dim3(grid), dim3(block), lds, stream, P, a, mode);
+            hipLaunchKernelGGL((k_sqp_rti_team<M, true, true>), dim3(grid), dim3(block), lds, stream, P, as, mode);
         else
-            hipLaunchKernelGGL((k_sqp_rti_team<M, false, true>), dim3(grid), dim3(block), lds, stream, P, a, mode);
+            hipLaunchKernelGGL((k_sqp_rti_team<M, false, true>), dim3(grid), dim3(block), lds, stream, P, as, mode);
     } else if (a.dense) {
-        hipLaunchKernelGGL((k_sqp_rti_team<M, true, false>), dim3(grid), dim3(block), lds, stream, P, a, mode);
+        hipLaunchKernelGGL((k_sqp_rti_team<M, true, false>), dim3(grid), dim3(block), lds, stream, P, as, mode);
     } else {
-        hipLaunchKernelGGL((k_sqp_rti_team<M, false, false>), dim3(grid), dim3(block), lds, stream, P, a, mode);
+        hipLaunchKernelGGL((k_sqp_rti_team<M, false, false>), dim3(grid), dim3(block), lds, stream, P, as, mode);
     }
     return hipGetLastError();
 }
@@ -1120,6 +1240,10 @@ template size_t team_scratch_floats<Tric3>(int, int);
 extern "C" int nmpc_debug_stamps_c1(unsigned long long* host)
 {
     return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_stamps_c1), sizeof(g_stamps_c1), 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -2;
+}
+extern "C" int nmpc_debug_stamps_pa(unsigned long long* host)
+{
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_stamps_pa), sizeof(g_stamps_pa), 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -2;
 }
 extern "C" int nmpc_debug_stamps_p1(unsigned long long* host)
 {

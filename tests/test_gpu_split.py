@@ -1,0 +1,111 @@
+"""Split launches (KArgs::split, small batches: one wave per robot, P0's integrations spread over the wave's four
+rows, the serial initial-iterate pass reading its stage inputs from LDS) against the unsplit team launch of the
+same inputs (NMPC_AMD_SPLIT_MAX=0 at handle creation), in every kernel mode: solve (the capsule ABI's path,
+NMPCNavControlDiff.cpp:142), run with caller poses, and run_path (getNextNPoses in the launch). Both launches run
+the same fp32 IPM from the same linearisation, so they agree to fp32 rounding (the RK4 code is the same function
+inlined in two places); every launch is also checked against the fp64 oracle by the parity tests, which run at
+split batch sizes."""
+import numpy as np
+import pytest
+import torch
+
+from helpers import oracle_closed_loop
+
+from nmpc_nav_control_amd._lib import default_params
+from nmpc_nav_control_amd.batch import BatchSolver
+from nmpc_nav_control_amd.path import discretize
+from oracle.oracle import path_discretize
+from tests.path_cases import random_paths
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda:0")
+TOL = 1e-5
+
+
+def t(a, dtype=torch.float32):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(device=DEV, dtype=dtype)
+
+
+def pair(monkeypatch, model, N, cap):
+    """(split, unsplit) handles of the same model and horizon."""
+    a = BatchSolver(model, N, cap, params=default_params(model, N))
+    monkeypatch.setenv("NMPC_AMD_SPLIT_MAX", "0")
+    b = BatchSolver(model, N, cap, params=default_params(model, N))
+    monkeypatch.delenv("NMPC_AMD_SPLIT_MAX")
+    return a, b
+
+
+def close(u, v):
+    return float((u.float() - v.float()).abs().max()) if u.numel() else 0.0
+
+
+@pytest.mark.parametrize("model", ["diff", "omni4", "tric"])
+@pytest.mark.parametrize("N,B", [(80, 13), (40, 1), (2, 5)])
+def test_split_solve_equals_unsplit(built, monkeypatch, model, N, B):
+    o, rec = oracle_closed_loop(model, N, B, 2)
+    nx, nu = o.nx, o.nu
+    sp, un = pair(monkeypatch, model, N, 64)
+    x0 = t(np.stack([r[0] for r in rec]).T)
+    yref = t(np.stack([r[1] for r in rec]).transpose(1, 2, 0))
+    We = t(np.stack([r[2] for r in rec]).T)
+    for s in (sp, un):
+        xv, uv, _ = s.state()
+        X, U = xv.to_tensor(), uv.to_tensor()
+        X[:, :B] = t(np.stack([r[3] for r in rec]).reshape(B, -1).T)
+        U[:, :B] = t(np.stack([r[4] for r in rec]).reshape(B, -1).T)
+        xv.copy_from(X)
+        uv.copy_from(U)
+    for tick in range(3):  # a cold tick, then warm-started multipliers
+        outs = []
+        for s in (sp, un):
+            o_ = dict(u0=torch.zeros(nu, B, device=DEV), xtraj=torch.zeros((N + 1) * nx, B, device=DEV),
+                      status=torch.full((B,), -7, dtype=torch.int32, device=DEV),
+                      qp_iter=torch.zeros(B, dtype=torch.int32, device=DEV))
+            s.solve(x0, yref, We=We, u0=o_["u0"], xtraj=o_["xtraj"], status=o_["status"], qp_iter=o_["qp_iter"])
+            outs.append(o_)
+        torch.cuda.synchronize()
+        assert (outs[0]["status"] == 0).all() and torch.equal(outs[0]["status"], outs[1]["status"]), tick
+        assert close(outs[0]["u0"], outs[1]["u0"]) <= TOL, tick
+        assert close(outs[0]["xtraj"], outs[1]["xtraj"]) <= TOL, tick
+        assert (outs[0]["qp_iter"] - outs[1]["qp_iter"]).abs().max() <= 1, tick
+
+
+@pytest.mark.parametrize("holo", [False, True])
+def test_split_run_and_run_path_equal_unsplit(built, monkeypatch, holo):
+    """run (caller poses, traj_len shorter than the horizon for some robots) and run_path, split against
+    unsplit, over three warm-started ticks; run_path's poses come out of the launch bit-identical."""
+    N, B = 40, 24
+    rng = np.random.default_rng(9)
+    segs, nseg, nu = random_paths(B, seed=9, max_segs=4, reverse_frac=0.2)
+    nu[:] = rng.uniform(0, 0.3, B)
+    exp_traj, _ = path_discretize(segs, nseg, nu, 1 / 40, N + 1, holo)
+    pose = exp_traj[:, 0, :].copy()
+    pose[:, :2] += rng.uniform(-0.1, 0.1, (B, 2))
+    pose[:, 2] += rng.uniform(-0.2, 0.2, B)
+    vel = np.zeros((B, 3))
+    vel[:, 0] = rng.uniform(0.0, 0.5, B)
+    P, V = t(pose.T), t(vel.T)
+    S, NS, NU = t(segs, torch.float64), t(nseg, torch.int32), t(nu, torch.float64)
+    tlen = t(np.where(np.arange(B) % 3 == 0, N // 2, N + 1), torch.int32)
+    handles = {"run": pair(monkeypatch, "diff", N, B), "path": pair(monkeypatch, "diff", N, B)}
+    for tick in range(3):
+        traj = discretize(S, NS, NU, 1 / 40, N + 1, holo)
+        res = {}
+        for kind, hs in handles.items():
+            res[kind] = []
+            for h in hs:
+                o_ = dict(u0=torch.zeros(2, B, device=DEV), cmd=torch.zeros(3, B, device=DEV),
+                          status=torch.full((B,), -7, dtype=torch.int32, device=DEV),
+                          traj=torch.zeros(N + 1, 3, B, device=DEV))
+                if kind == "run":
+                    h.run(P, V, traj, traj_len=tlen, cmd=o_["cmd"], u0=o_["u0"], status=o_["status"])
+                else:
+                    h.run_path(P, V, S, NS, NU, 1 / 40, holo, traj_out=o_["traj"], cmd=o_["cmd"], u0=o_["u0"],
+                               status=o_["status"])
+                res[kind].append(o_)
+        torch.cuda.synchronize()
+        for kind, (a, b) in res.items():
+            assert (a["status"] == 0).all() and torch.equal(a["status"], b["status"]), (tick, kind)
+            assert close(a["u0"], b["u0"]) <= TOL, (tick, kind)
+            assert close(a["cmd"], b["cmd"]) <= TOL, (tick, kind)
+        assert torch.equal(res["path"][0]["traj"], traj) and torch.equal(res["path"][1]["traj"], traj), tick

@@ -23,8 +23,14 @@ L.nmpc_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
 ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 ev0.record(); f.solve(); ev1.record(); torch.cuda.synchronize()
 print("kernel ms", ev0.elapsed_time(ev1))
+if hasattr(L, "nmpc_debug_stamps_pa"):
+    pa = (ctypes.c_ulonglong * 256)()
+    L.nmpc_debug_stamps_pa.argtypes = [ctypes.c_void_p]
+    assert L.nmpc_debug_stamps_pa(pa) == 0
 assert L.nmpc_debug_stamps(buf, 256 * W) == 0
 st = np.frombuffer(buf, dtype=np.uint64).reshape(256, W).astype(np.int64)
+if hasattr(L, "nmpc_debug_stamps_pa") and pa[0] > st[0, 0]:  # split launches only
+    print("P0 stage-parallel part cycles", int(pa[0]) - st[0, 0], "serial pass", st[0, 1] - int(pa[0]))
 it = f.qp_iter.cpu().numpy()[::4][:256]
 itw = f.qp_iter.cpu().numpy().reshape(-1, 4).max(1)[:256]
 ph = {"P1": [], "F0": [], "C1F1": [], "SG": []}
