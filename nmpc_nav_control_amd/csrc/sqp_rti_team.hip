@@ -359,6 +359,8 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
     // the robot's records (indexed by the robot, not the team slot, so that they carry its multipliers to its next
     // solve whatever the placement)
     float* const tbase = a.scratch + (size_t)inst * (N + 1) * 16 * RS + (lv ? r : 0) * rec_lane<RS, QM>();
+    // every lane's own slot (idle lanes: one nobody reads), for P0's unconditional record stores
+    float* const tbase_own = a.scratch + (size_t)inst * (N + 1) * 16 * RS + r * rec_lane<RS, QM>();
     // IPM warm start: the bound multipliers of the robot's previous successful solve are still in its records
     const bool warm = P.warm && a.warm && a.warm[inst] && !(a.reset && a.reset[inst]);
     constexpr int KS = 16 * RS;
@@ -627,7 +629,13 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
         }
 #pragma unroll
         for (int i = 0; i < NGV; i++) rec[R::GV + i] = (k < N && lv) ? g[i] : 0.0f;
-        if (lv) rec_store<RS, QM>(tbase + (size_t)k * KS, rec);
+        // 15-slot teams (omni4): unconditional (the idle lane stores zeros / sentinels into its own unused
+        // slot). A store under a lane mask may or may not be issued, so the compiler's waits for the next loads
+        // drain the whole memory counter, these stores included. Same-box A/B: omni4 kernel 1.303 -> 1.256 ms;
+        // diff (7 idle lanes, +78 % P0 store bytes) 1.043 -> 1.065 ms, so 9-slot teams keep the masked store
+        // (profiles/r02/ab/uncond_stores.txt)
+        if constexpr (NV > 12) rec_store<RS, QM>(tbase_own + (size_t)k * KS, rec);
+        else if (lv) rec_store<RS, QM>(tbase + (size_t)k * KS, rec);
         // dynamics-feasible initial states: dx_{k+1} = A dx_k + b_k (inputs start at du = 0, dx_0 = x0 - xbar_0);
         // row i of [B A] dz: NGV row sums over the columns + the constant rows held in grow
         if (k < N) {
