@@ -178,7 +178,7 @@ def cpu_baseline(fleets, sample, ticks, nthreads):
             torch.cuda.synchronize()
             sn = f.snapshot()
             sl = lambda a, n: None if a is None else np.ascontiguousarray(a[:n])  # noqa: E731
-            args = [sl(sn[k], S) for k in ("pose", "vel", "steer", "traj", "tlen")]
+            args = [sl(sn[k], S) for k in ("pose", "vel", "steer", "traj", "tlen", "reset")]
             state = [sl(sn[k], S) for k in ("carried", "xbar", "ubar")]
             f.solve()
             # single-core rate on a slice of the same inputs (copies: batch_tick updates the iterate in place)
@@ -186,11 +186,11 @@ def cpu_baseline(fleets, sample, ticks, nthreads):
             a1 = [sl(a, S1) for a in args]
             s1 = [np.array(a[:S1]) for a in state]
             t0 = time.perf_counter()
-            o.batch_tick(*a1, None, *s1, nthreads=1)
+            o.batch_tick(*a1, *s1, nthreads=1)
             time_1 += time.perf_counter() - t0
             solves_1 += S1
             t0 = time.perf_counter()
-            nf, cmd_o, u0_o, st_o, _ = o.batch_tick(*args, None, *state, nthreads=nthreads)
+            nf, cmd_o, u0_o, st_o, _ = o.batch_tick(*args, *state, nthreads=nthreads)
             total_time += time.perf_counter() - t0
             total_solves += S
             torch.cuda.synchronize()
@@ -239,6 +239,8 @@ def main():
                     help="stream groups per model (default: the config's); each is a Fleet on its own HIP stream")
     ap.add_argument("--joined", action="store_true",
                     help="fleet-wide tick boundary across streams (default: decoupled streams unless --gather)")
+    ap.add_argument("--no-renew", action="store_true",
+                    help="every robot keeps its first goal / path (the round-2 workload, which parks and drifts)")
     args = ap.parse_args()
 
     rank, world, local_rank = world_info()
@@ -253,7 +255,7 @@ def main():
     # shard [rank*B, (rank+1)*B) of it (sharding.shard_range), no collective on the solve path
     groups = cfg.get("groups", 1) if args.groups is None else args.groups
     node = FleetNode(cfg["models"], cfg["N"], DEFAULT_SEED + cfg["idx"], dev, rank=rank, world=world, gather=gather,
-                     groups=groups, decoupled=False if args.joined else None)
+                     groups=groups, decoupled=False if args.joined else None, renew=not args.no_renew)
     fleets = node.fleets
     torch.cuda.synchronize()
 
@@ -275,6 +277,7 @@ def main():
     elapsed = region.elapsed
 
     kernel_ms = timer.kernel_ms(node.decoupled)
+    its = node.iter_stats()
     B_rank = node.B
     k_mean = float(node.iters_sum.sum().item()) / (B_rank * args.steps)
     units = args.steps * B_rank * world
@@ -300,12 +303,15 @@ def main():
             "value": round(value, 1), "unit": "SQP-RTI iterations/sec", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "fp32+fp64",
-            "data": "synthetic seeded closed-loop fleet (SURVEY 8d), random-arc paths + goal poses",
+            "data": ("synthetic seeded closed-loop fleet (SURVEY 8d), random-arc paths + goal poses" +
+                     ("" if args.no_renew else ", stationary: new goal / path + reset_mpc on arrival or after a "
+                                               "2-6 s ttl (NMPCNavControlROS.cpp:304-327)")),
             "config": {"workload": cfg["desc"], "config": args.config, "N": cfg["N"],
                        "batch_per_gpu": B_rank, "global_batch": B_rank * world,
                        "models": [m for m, _ in cfg["models"]], "parallelism": f"instance-sharded x{world}",
                        "closed_loop_warmup_ticks": args.closed_loop_warmup, "rccl_gather": gather},
             "u0_max_abs_err": u0_err, "qp_iter_mean": round(k_mean, 3), "qp_iter_max": int(node.iters_max.max().item()),
+            "qp_iter": {k: (round(v, 3) if isinstance(v, float) else v) for k, v in its.items()},
             "failed_solves": int(node.fail_cnt.sum().item()), "roofline": roof, "cpu_baseline": cpu,
         }
         print(json.dumps(result), flush=True)

@@ -177,6 +177,34 @@ int nmpc_batch_warm_state(nmpc_batch* b, unsigned char** warm, float** scratch, 
 int nmpc_fleet_sim_step(nmpc_batch* b, int B, const float* path, float* s, float* pose, float* vel, float* steer,
                         const float* u0, const int* status, float* traj, int* traj_len, int advance, void* stream);
 
+/* Stationary closed loop (bench / test harness): the fleet manager issues a robot a new goal or path when it
+ * has arrived (the end-of-trajectory test of processGoToPose / processFollowPath, NMPCNavControlROS.cpp:637-643 /
+ * :682-693, with |heading error|) or when its current one has been active for `ttl` ticks, and the node resets
+ * the controller as its goal / path callbacks do (reset_mpc -> {name}_acados_reset, NMPCNavControlROS.cpp:304-327):
+ * `reset` [B] is set for the next nmpc_batch_run. A new target depends only on (seed, start + robot index, event
+ * count) and the robot's pose: draw j of event e is u = (h >> 8) / 2^24 with h = nmpc_fleet_hash(seed,
+ * global index, 16 e + j) (the same 32-bit integer hash on host and device), so any sharding or stream grouping
+ * issues the same targets. Goal robots (path length < 0) get a goal at distance U(goal_r_lo, goal_r_hi) in a
+ * uniform direction with a uniform heading; path robots an arc starting within 0.2 m / 0.3 rad of the robot
+ * (curvature U(-kappa_max, kappa_max), speed U(speed_lo, speed_hi), length U(len_lo, len_hi)), progress s = 0.
+ * The new ttl is ttl_min + ((h >> 8) * (ttl_max - ttl_min + 1) >> 24). */
+typedef struct nmpc_fleet_renew {
+    unsigned int seed;
+    int start;                  /* global index of robot 0 of this call */
+    int ttl_min, ttl_max;       /* ticks a goal / path stays active (inclusive range) */
+    float goal_r_lo, goal_r_hi; /* m */
+    float kappa_max, speed_lo, speed_hi, len_lo, len_hi;
+    float pos_tol, ang_tol;     /* final_position_error (m) / final_orientation_error (rad), nmpc_nav_control.yaml:6-7 */
+    int* ev;                    /* [B] events so far (in/out) */
+    int* ttl;                   /* [B] ticks left (in/out) */
+    unsigned char* reset;       /* [B] out: 1 where this step issued a new goal / path */
+} nmpc_fleet_renew;
+int nmpc_fleet_sim_step_renew(nmpc_batch* b, int B, float* path, float* s, float* pose, float* vel, float* steer,
+                              const float* u0, const int* status, float* traj, int* traj_len,
+                              const nmpc_fleet_renew* renew, void* stream);
+/* The harness hash: lowbias32(lowbias32(lowbias32(seed ^ 0x9e3779b9) + index) + counter) (uint32 arithmetic). */
+unsigned int nmpc_fleet_hash(unsigned int seed, unsigned int index, unsigned int counter);
+
 const char* nmpc_last_error(void);
 const char* nmpc_version(void);
 

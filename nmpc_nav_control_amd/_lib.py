@@ -33,6 +33,15 @@ class ModelParams(ctypes.Structure):
     ]
 
 
+class FleetRenew(ctypes.Structure):
+    """Mirror of nmpc_fleet_renew (include/nmpc_amd/nmpc_batch.h): the harness's stationary goal / path renewal."""
+    _fields_ = [("seed", ctypes.c_uint), ("start", ctypes.c_int), ("ttl_min", ctypes.c_int), ("ttl_max", ctypes.c_int),
+                ("goal_r_lo", ctypes.c_float), ("goal_r_hi", ctypes.c_float), ("kappa_max", ctypes.c_float),
+                ("speed_lo", ctypes.c_float), ("speed_hi", ctypes.c_float), ("len_lo", ctypes.c_float),
+                ("len_hi", ctypes.c_float), ("pos_tol", ctypes.c_float), ("ang_tol", ctypes.c_float),
+                ("ev", c_void_p), ("ttl", c_void_p), ("reset", c_void_p)]
+
+
 class CodegenDesc(ctypes.Structure):
     """Mirror of nmpc_codegen_desc (include/nmpc_amd/nmpc_capsule.h)."""
     _fields_ = [("model", ctypes.c_int), ("N", ctypes.c_int), ("tf", ctypes.c_double),
@@ -59,7 +68,7 @@ BATCH_SYMBOLS = [
     "nmpc_model_dims", "nmpc_model_params_default", "nmpc_model_params_set_limits", "nmpc_batch_create",
     "nmpc_batch_destroy", "nmpc_batch_set_params", "nmpc_batch_get_params", "nmpc_batch_init_iterate",
     "nmpc_batch_solve", "nmpc_batch_solve_iterate", "nmpc_batch_run", "nmpc_batch_run_path", "nmpc_batch_state", "nmpc_batch_warm_state", "nmpc_batch_set_kernel", "nmpc_batch_set_schedule",
-    "nmpc_fleet_sim_step",
+    "nmpc_fleet_sim_step", "nmpc_fleet_sim_step_renew", "nmpc_fleet_hash",
     "nmpc_last_error", "nmpc_version", "nmpc_path_discretize", "nmpc_codegen_default", "nmpc_capsule_new",
     "nmpc_capsule_delete", "nmpc_capsule_create", "nmpc_capsule_reset", "nmpc_capsule_update_params",
     "nmpc_capsule_solve", "nmpc_capsule_batch_solve", "nmpc_capsule_free", "nmpc_capsule_print_stats",
@@ -109,6 +118,9 @@ def lib():
     L.nmpc_batch_state.argtypes = [vp, ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.POINTER(vp), c_int_p]
     L.nmpc_batch_warm_state.argtypes = [vp, ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.POINTER(ctypes.c_size_t)]
     L.nmpc_fleet_sim_step.argtypes = [vp, i, vp, vp, vp, vp, vp, vp, vp, vp, vp, i, vp]
+    L.nmpc_fleet_sim_step_renew.argtypes = [vp, i, vp, vp, vp, vp, vp, vp, vp, vp, vp, ctypes.POINTER(FleetRenew), vp]
+    L.nmpc_fleet_hash.argtypes = [ctypes.c_uint, ctypes.c_uint, ctypes.c_uint]
+    L.nmpc_fleet_hash.restype = ctypes.c_uint
     L.nmpc_path_discretize.argtypes = [i, vp, i, vp, vp, ctypes.c_double, i, i, vp, vp, vp]
     L.nmpc_codegen_default.argtypes = [i, ctypes.POINTER(CodegenDesc)]
     L.nmpc_last_error.restype = ctypes.c_char_p

@@ -8,7 +8,7 @@ import ctypes
 
 import torch
 
-from ._lib import KERNELS, MODEL_IDS, SCHEDULES, ModelParams, check, default_params, lib, model_dims
+from ._lib import KERNELS, MODEL_IDS, SCHEDULES, FleetRenew, ModelParams, check, default_params, lib, model_dims
 
 
 def _ptr(t, dtype=None, shape=None, name="argument"):
@@ -199,6 +199,27 @@ class BatchSolver:
             _ptr(vel, F32, (3, B), "vel"), _ptr(steer, F32, (B,), "steer"), _ptr(u0, F32, (self.nu, B), "u0"),
             _ptr(status, I32, (B,), "status"), _ptr(traj, F32, (self.N + 1, 3, B), "traj"),
             _ptr(traj_len, I32, (B,), "traj_len"), int(bool(advance)), _stream(stream)), "nmpc_fleet_sim_step")
+
+
+    def fleet_sim_step_renew(self, path, s, pose, vel, steer, u0, status, traj, traj_len, ev, ttl, reset, seed, start,
+                             renew, stream=None):
+        """fleet_sim_step (advance) followed by the stationary loop's goal / path renewal (nmpc_fleet_sim_step_renew):
+        ev, ttl int32 [B] in/out, reset uint8 [B] out (the next run's reset mask); renew: scenario.RENEW keys +
+        kappa_max, speed (lo, hi)."""
+        B = pose.shape[1]
+        if not 0 <= B <= self.capacity:
+            raise ValueError(f"batch {B} exceeds the capacity {self.capacity}")
+        R = FleetRenew(seed=int(seed) & 0xFFFFFFFF, start=int(start), ttl_min=int(renew["ttl_min"]),
+                       ttl_max=int(renew["ttl_max"]), goal_r_lo=renew["goal_r_lo"], goal_r_hi=renew["goal_r_hi"],
+                       kappa_max=renew["kappa_max"], speed_lo=renew["speed"][0], speed_hi=renew["speed"][1],
+                       len_lo=renew["len_lo"], len_hi=renew["len_hi"], pos_tol=renew["pos_tol"],
+                       ang_tol=renew["ang_tol"], ev=_ptr(ev, I32, (B,), "ev"), ttl=_ptr(ttl, I32, (B,), "ttl"),
+                       reset=_ptr(reset, U8, (B,), "reset"))
+        check(lib().nmpc_fleet_sim_step_renew(
+            self._h, B, _ptr(path, F32, (6, B), "path"), _ptr(s, F32, (B,), "s"), _ptr(pose, F32, (3, B), "pose"),
+            _ptr(vel, F32, (3, B), "vel"), _ptr(steer, F32, (B,), "steer"), _ptr(u0, F32, (self.nu, B), "u0"),
+            _ptr(status, I32, (B,), "status"), _ptr(traj, F32, (self.N + 1, 3, B), "traj"),
+            _ptr(traj_len, I32, (B,), "traj_len"), ctypes.byref(R), _stream(stream)), "nmpc_fleet_sim_step_renew")
 
 
 class _DeviceView:

@@ -12,6 +12,9 @@
 // copies the new iterate back. Device engines are shared per (model, N) and grow on demand.
 #include <hip/hip_runtime.h>
 
+#include "nmpc_trace.hpp"
+using nmpc::TraceRange;
+
 #include <atomic>
 #include <chrono>
 #include <cmath>
@@ -373,12 +376,16 @@ void solve_group(std::vector<nmpc_capsule_impl*>& cs, std::vector<Packed>& ps, c
             e.dev_warm[q] = 2;
         }
     };
-    if (ensure_engine(e, ps[idx[0]].prm, n, why)) return fail_all(why);
+    {
+        const TraceRange tr("capsule.engine");
+        if (ensure_engine(e, ps[idx[0]].prm, n, why)) return fail_all(why);
+    }
     const auto ta = std::chrono::steady_clock::now();
     const Blocks bl(n, N, nx, nu, ny);
     float *hx0 = e.hio + bl.x0, *hyref = e.hio + bl.yref, *hWe = e.hio + bl.We, *hxb = e.hio + bl.xb,
           *hub = e.hio + bl.ub;
     {
+        const TraceRange tr("capsule.pack");
         std::vector<const double*> x0s(n), yrefs(n), Wes(n), xbs(n), ubs(n);
         for (int q = 0; q < n; q++) {
             const Packed& P = ps[idx[q]];
@@ -404,19 +411,25 @@ void solve_group(std::vector<nmpc_capsule_impl*>& cs, std::vector<Packed>& ps, c
         e.hwarm[q] = (e.owner[q] == c->uid && c->warm_ok) ? 1 : 0;
         flags_differ |= e.hwarm[q] != e.dev_warm[q];
     }
-    if (flags_differ && (r = hipMemcpyAsync(e.dwarm, e.hwarm, (size_t)n, hipMemcpyHostToDevice, st)) != hipSuccess)
-        return fail_all(hipGetErrorString(r));
-    if ((r = hipMemcpyAsync(dio, e.hio, sizeof(float) * bl.in_floats, hipMemcpyHostToDevice, st)) != hipSuccess)
-        return fail_all(hipGetErrorString(r));
+    {
+        const TraceRange tr("capsule.h2d");
+        if (flags_differ && (r = hipMemcpyAsync(e.dwarm, e.hwarm, (size_t)n, hipMemcpyHostToDevice, st)) != hipSuccess)
+            return fail_all(hipGetErrorString(r));
+        if ((r = hipMemcpyAsync(dio, e.hio, sizeof(float) * bl.in_floats, hipMemcpyHostToDevice, st)) != hipSuccess)
+            return fail_all(hipGetErrorString(r));
+    }
     const auto t1 = std::chrono::steady_clock::now();
     if (nmpc_batch_solve_iterate(e.batch, n, dio + bl.x0, dio + bl.yref, ny, dio + bl.We, nullptr, dio + bl.xb,
                                  dio + bl.ub, n, reinterpret_cast<int*>(dio + bl.ost),
                                  reinterpret_cast<int*>(dio + bl.oit), dio + bl.ores, st) != NMPC_OK)
         return fail_all(nmpc_last_error());
-    if ((r = hipMemcpyAsync(e.hio + bl.xb, dio + bl.xb, sizeof(float) * (bl.io_words - bl.xb), hipMemcpyDeviceToHost,
-                            st)) != hipSuccess ||
-        (r = hipStreamSynchronize(st)) != hipSuccess)
-        return fail_all(hipGetErrorString(r));
+    {
+        const TraceRange tr("capsule.d2h_sync");  // the output copy queued behind the kernel, and the wait
+        if ((r = hipMemcpyAsync(e.hio + bl.xb, dio + bl.xb, sizeof(float) * (bl.io_words - bl.xb),
+                                hipMemcpyDeviceToHost, st)) != hipSuccess ||
+            (r = hipStreamSynchronize(st)) != hipSuccess)
+            return fail_all(hipGetErrorString(r));
+    }
     const float* const hres = e.hio + bl.ores;
     const int* const hst = reinterpret_cast<const int*>(e.hio + bl.ost);
     const int* const hit = reinterpret_cast<const int*>(e.hio + bl.oit);
@@ -445,6 +458,7 @@ void solve_group(std::vector<nmpc_capsule_impl*>& cs, std::vector<Packed>& ps, c
         xbs[q] = hst[q] == 0 ? c->xbar.data() : nullptr;
         ubs[q] = hst[q] == 0 ? c->ubar.data() : nullptr;
     }
+    const TraceRange tr("capsule.unpack");
     from_soa(hxb, n, (size_t)(N + 1) * nx, xbs);
     from_soa(hub, n, (size_t)N * nu, ubs);
 }
@@ -741,6 +755,9 @@ int nmpc_capsule_update_params(nmpc_solver_capsule* capsule, int stage, const do
 int nmpc_capsule_solve(nmpc_solver_capsule* capsule)
 {
     if (!capsule || !capsule->impl) return 4;
+    static const char* const names[3] = {"diff2amr_acados_solve", "omni4amr_acados_solve", "tric3amr_acados_solve"};
+    const int m = capsule->impl->model;
+    const TraceRange trace(m >= 0 && m < 3 ? names[m] : "acados_solve");
     std::vector<nmpc_capsule_impl*> cs{capsule->impl};
     batch_solve_impl(cs, nullptr);
     return capsule->impl->status;
@@ -749,6 +766,7 @@ int nmpc_capsule_solve(nmpc_solver_capsule* capsule)
 int nmpc_capsule_batch_solve(nmpc_solver_capsule** capsules, int* status_out, int n)
 {
     if (!capsules || n < 0) return -1;
+    const TraceRange trace("acados_batch_solve");
     std::vector<nmpc_capsule_impl*> cs(n);
     for (int i = 0; i < n; i++) cs[i] = capsules[i] ? capsules[i]->impl : nullptr;
     return batch_solve_impl(cs, status_out);

@@ -7,9 +7,27 @@
 //   path-following robots: nearest point on a circular-arc path, then samples spaced |v|*dt along it
 //     (PathDiscretizer.cpp:25-47: first sample one spacing ahead, padding with the path end, :55-60);
 //   go-to-pose robots: the goal pose alone (processGoToPose, NMPCNavControlROS.cpp:630-636).
+// With a renewal record (nmpc_fleet_sim_step_renew) the loop is stationary: after the plant step a robot that has
+// arrived or whose goal / path has been active for its ttl gets a new one from the harness hash and is reset on
+// its next solve (the goal / path callbacks, NMPCNavControlROS.cpp:304-327).
 #include "nmpc_kernels.hpp"
 
 namespace nmpc {
+
+__host__ __device__ inline unsigned int lowbias32(unsigned int h)
+{
+    h ^= h >> 16;
+    h *= 0x7feb352du;
+    h ^= h >> 15;
+    h *= 0x846ca68bu;
+    h ^= h >> 16;
+    return h;
+}
+__host__ __device__ inline unsigned int fleet_hash(unsigned int seed, unsigned int index, unsigned int counter)
+{
+    return lowbias32(lowbias32(lowbias32(seed ^ 0x9e3779b9u) + index) + counter);
+}
+
 namespace {
 
 __device__ inline void arc_pose(const float* path, size_t Bn, int i, float s, float* out)
@@ -32,10 +50,22 @@ __device__ inline void arc_pose(const float* path, size_t Bn, int i, float s, fl
     out[2] = th;
 }
 
+__device__ inline float wrap_pi(float a)
+{
+    a = fmodf(a + kPi, 2.0f * kPi);
+    return (a < 0.0f ? a + 2.0f * kPi : a) - kPi;
+}
+
+// draw j of event e of robot gi: a uniform in [0, 1) with 24 random bits (exact in fp32 and fp64)
+__device__ inline float fleet_u(const nmpc_fleet_renew& R, unsigned int gi, int e, int j)
+{
+    return (float)(fleet_hash(R.seed, gi, 16u * (unsigned int)e + (unsigned int)j) >> 8) * (1.0f / 16777216.0f);
+}
+
 template <class M>
-__global__ void k_fleet_sim(KParams P, int B, int stride, const float* path, float* s, float* pose, float* vel,
+__global__ void k_fleet_sim(KParams P, int B, int stride, float* path, float* s, float* pose, float* vel,
                             float* steer, const float* u0, const int* status, const float* carried, float* traj,
-                            int* traj_len, int advance)
+                            int* traj_len, int advance, nmpc_fleet_renew R)
 {
     constexpr int NX = M::NX, NU = M::NU;
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -79,6 +109,51 @@ __global__ void k_fleet_sim(KParams P, int B, int stride, const float* path, flo
             vel[(size_t)j * Bn + i] = nv[j];
         }
     }
+    if (R.ev && advance) {
+        // the fleet manager: arrival (the end-of-trajectory test of processGoToPose / processFollowPath,
+        // NMPCNavControlROS.cpp:637-643 / :682-693; |heading error| where the reference compares the signed
+        // normAngRad) or the ttl of the current goal / path ends -> a new one, and reset_mpc on the next solve
+        float end[3];
+        if (path[5 * Bn + i] < 0.0f) {
+            end[0] = path[i];
+            end[1] = path[Bn + i];
+            end[2] = path[2 * Bn + i];
+        } else {
+            arc_pose(path, Bn, i, path[5 * Bn + i], end);
+        }
+        const float dx = ps[0] - end[0], dy = ps[1] - end[1];
+        const bool arrived = (dx * dx + dy * dy <= R.pos_tol * R.pos_tol) && fabsf(wrap_pi(ps[2] - end[2])) <= R.ang_tol;
+        const int ttl = R.ttl[i] - 1;
+        if (arrived || ttl <= 0) {
+            const int e = R.ev[i] + 1;
+            const unsigned int gi = (unsigned int)(R.start + i);
+            const float ua = fleet_u(R, gi, e, 0), ub = fleet_u(R, gi, e, 1), uc = fleet_u(R, gi, e, 2);
+            float sa, ca;
+            __sincosf(2.0f * kPi * ua, &sa, &ca);
+            if (path[5 * Bn + i] < 0.0f) {
+                const float rr = R.goal_r_lo + (R.goal_r_hi - R.goal_r_lo) * ub;
+                path[i] = ps[0] + rr * ca;
+                path[Bn + i] = ps[1] + rr * sa;
+                path[2 * Bn + i] = kPi * (2.0f * uc - 1.0f);
+            } else {
+                const float rr = 0.2f * ub;
+                path[i] = ps[0] + rr * ca;
+                path[Bn + i] = ps[1] + rr * sa;
+                path[2 * Bn + i] = ps[2] + 0.3f * (2.0f * uc - 1.0f);
+                path[3 * Bn + i] = R.kappa_max * (2.0f * fleet_u(R, gi, e, 3) - 1.0f);
+                path[4 * Bn + i] = R.speed_lo + (R.speed_hi - R.speed_lo) * fleet_u(R, gi, e, 4);
+                path[5 * Bn + i] = R.len_lo + (R.len_hi - R.len_lo) * fleet_u(R, gi, e, 5);
+                s[i] = 0.0f;
+            }
+            const unsigned long long span = (unsigned long long)(R.ttl_max - R.ttl_min + 1);
+            R.ttl[i] = R.ttl_min + (int)((unsigned long long)(fleet_hash(R.seed, gi, 16u * (unsigned int)e + 15u) >> 8) * span >> 24);
+            R.ev[i] = e;
+            R.reset[i] = 1;
+        } else {
+            R.ttl[i] = ttl;
+            R.reset[i] = 0;
+        }
+    }
     const int N = P.N;
     const float len = path[5 * Bn + i];
     if (len < 0.0f) {
@@ -115,23 +190,31 @@ __global__ void k_fleet_sim(KParams P, int B, int stride, const float* path, flo
 }  // namespace
 
 template <class M>
-hipError_t launch_fleet_sim(const KParams& P, int B, int stride, const float* path, float* s, float* pose, float* vel,
+hipError_t launch_fleet_sim(const KParams& P, int B, int stride, float* path, float* s, float* pose, float* vel,
                             float* steer, const float* u0, const int* status, const float* carried, float* traj,
-                            int* traj_len, int advance, hipStream_t stream)
+                            int* traj_len, int advance, const nmpc_fleet_renew* renew, hipStream_t stream)
 {
     if (B <= 0) return hipSuccess;
     const int block = 256;
+    nmpc_fleet_renew R{};
+    if (renew) R = *renew;
     hipLaunchKernelGGL(k_fleet_sim<M>, dim3((B + block - 1) / block), dim3(block), 0, stream, P, B, stride, path, s,
-                       pose, vel, steer, u0, status, carried, traj, traj_len, advance);
+                       pose, vel, steer, u0, status, carried, traj, traj_len, advance, R);
     return hipGetLastError();
 }
 
 #define INST(M)                                                                                                      \
-    template hipError_t launch_fleet_sim<M>(const KParams&, int, int, const float*, float*, float*, float*, float*, \
-                                            const float*, const int*, const float*, float*, int*, int, hipStream_t);
+    template hipError_t launch_fleet_sim<M>(const KParams&, int, int, float*, float*, float*, float*, float*,       \
+                                            const float*, const int*, const float*, float*, int*, int,              \
+                                            const nmpc_fleet_renew*, hipStream_t);
 INST(Diff2)
 INST(Omni4)
 INST(Tric3)
 #undef INST
 
 }  // namespace nmpc
+
+extern "C" unsigned int nmpc_fleet_hash(unsigned int seed, unsigned int index, unsigned int counter)
+{
+    return nmpc::fleet_hash(seed, index, counter);
+}

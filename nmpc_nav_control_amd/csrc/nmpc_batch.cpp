@@ -11,6 +11,7 @@
 #include <string>
 
 #include "nmpc_kernels.hpp"
+#include "nmpc_trace.hpp"
 
 using namespace nmpc;
 
@@ -376,6 +377,7 @@ int nmpc_batch_solve(nmpc_batch* b, int B, const float* x0, const float* yref, i
                      const unsigned char* reset, float* u0, float* x1, float* xtraj, float* utraj, int* status,
                      int* qp_iter, float* qp_res, void* stream)
 {
+    const TraceRange trace("nmpc_batch_solve");
     if (!b) return set_err(NMPC_ERR_ARG, "batch is NULL");
     if (B < 0 || B > b->capacity) return set_err(NMPC_ERR_ARG, "B out of range [0, capacity]");
     if (B == 0) return NMPC_OK;
@@ -408,6 +410,7 @@ int nmpc_batch_solve_iterate(nmpc_batch* b, int B, const float* x0, const float*
                              const unsigned char* reset, float* xbar, float* ubar, int ld, int* status, int* qp_iter,
                              float* qp_res, void* stream)
 {
+    const TraceRange trace("nmpc_batch_solve_iterate");
     if (!b) return set_err(NMPC_ERR_ARG, "batch is NULL");
     if (B < 0 || B > b->capacity) return set_err(NMPC_ERR_ARG, "B out of range [0, capacity]");
     if (B == 0) return NMPC_OK;
@@ -437,6 +440,7 @@ int nmpc_batch_run(nmpc_batch* b, int B, const float* pose, const float* vel, co
                    const float* traj, const int* traj_len, const unsigned char* reset, float* cmd, float* u0,
                    int* status, int* qp_iter, float* qp_res, void* stream)
 {
+    const TraceRange trace("nmpc_batch_run");
     if (!b) return set_err(NMPC_ERR_ARG, "batch is NULL");
     if (B < 0 || B > b->capacity) return set_err(NMPC_ERR_ARG, "B out of range [0, capacity]");
     if (B == 0) return NMPC_OK;
@@ -468,6 +472,7 @@ int nmpc_batch_run_path(nmpc_batch* b, int B, const float* pose, const float* ve
                         double sample_period, int is_holonomic, const unsigned char* reset, float* traj_out,
                         float* cmd, float* u0, int* status, int* qp_iter, float* qp_res, void* stream)
 {
+    const TraceRange trace("nmpc_batch_run_path");
     if (!b) return set_err(NMPC_ERR_ARG, "batch is NULL");
     if (B < 0 || B > b->capacity) return set_err(NMPC_ERR_ARG, "B out of range [0, capacity]");
     if (B == 0) return NMPC_OK;
@@ -538,9 +543,11 @@ int nmpc_batch_warm_state(nmpc_batch* b, unsigned char** warm, float** scratch, 
     return NMPC_OK;
 }
 
-int nmpc_fleet_sim_step(nmpc_batch* b, int B, const float* path, float* s, float* pose, float* vel, float* steer,
-                        const float* u0, const int* status, float* traj, int* traj_len, int advance, void* stream)
+namespace {
+int fleet_sim(nmpc_batch* b, int B, float* path, float* s, float* pose, float* vel, float* steer, const float* u0,
+              const int* status, float* traj, int* traj_len, int advance, const nmpc_fleet_renew* renew, void* stream)
 {
+    const TraceRange trace("nmpc_fleet_sim_step");
     if (!b) return set_err(NMPC_ERR_ARG, "batch is NULL");
     if (B < 0 || B > b->capacity) return set_err(NMPC_ERR_ARG, "B out of range [0, capacity]");
     if (!path || !s || !pose || !vel || !traj || (advance && !u0)) return set_err(NMPC_ERR_ARG, "NULL argument");
@@ -549,18 +556,36 @@ int nmpc_fleet_sim_step(nmpc_batch* b, int B, const float* path, float* s, float
     switch (b->prm.model) {
     case NMPC_MODEL_DIFF2AMR:
         e = launch_fleet_sim<Diff2>(b->kp, B, b->capacity, path, s, pose, vel, steer, u0, status, b->carried, traj,
-                                    traj_len, advance, st);
+                                    traj_len, advance, renew, st);
         break;
     case NMPC_MODEL_OMNI4AMR:
         e = launch_fleet_sim<Omni4>(b->kp, B, b->capacity, path, s, pose, vel, steer, u0, status, b->carried, traj,
-                                    traj_len, advance, st);
+                                    traj_len, advance, renew, st);
         break;
     default:
         e = launch_fleet_sim<Tric3>(b->kp, B, b->capacity, path, s, pose, vel, steer, u0, status, b->carried, traj,
-                                    traj_len, advance, st);
+                                    traj_len, advance, renew, st);
         break;
     }
     return hip_err(e, "fleet_sim launch");
+}
+}  // namespace
+
+int nmpc_fleet_sim_step(nmpc_batch* b, int B, const float* path, float* s, float* pose, float* vel, float* steer,
+                        const float* u0, const int* status, float* traj, int* traj_len, int advance, void* stream)
+{
+    // without a renewal record the kernel never writes `path`
+    return fleet_sim(b, B, const_cast<float*>(path), s, pose, vel, steer, u0, status, traj, traj_len, advance,
+                     nullptr, stream);
+}
+
+int nmpc_fleet_sim_step_renew(nmpc_batch* b, int B, float* path, float* s, float* pose, float* vel, float* steer,
+                              const float* u0, const int* status, float* traj, int* traj_len,
+                              const nmpc_fleet_renew* renew, void* stream)
+{
+    if (!renew || !renew->ev || !renew->ttl || !renew->reset) return set_err(NMPC_ERR_ARG, "renew: NULL argument");
+    if (renew->ttl_min < 1 || renew->ttl_max < renew->ttl_min) return set_err(NMPC_ERR_ARG, "renew: ttl range");
+    return fleet_sim(b, B, path, s, pose, vel, steer, u0, status, traj, traj_len, 1, renew, stream);
 }
 
 int nmpc_path_discretize(int B, const nmpc_path_segment* segs, int seg_stride, const int* nseg,

@@ -64,9 +64,9 @@ size_t team_scratch_floats(int N, int stride);
 template <class M>
 hipError_t launch_sqp_rti_team(const KParams& P, const KArgs& a, int mode, hipStream_t stream);
 template <class M>
-hipError_t launch_fleet_sim(const KParams& P, int B, int stride, const float* path, float* s, float* pose, float* vel,
+hipError_t launch_fleet_sim(const KParams& P, int B, int stride, float* path, float* s, float* pose, float* vel,
                             float* steer, const float* u0, const int* status, const float* carried, float* traj,
-                            int* traj_len, int advance, hipStream_t stream);
+                            int* traj_len, int advance, const nmpc_fleet_renew* renew, hipStream_t stream);
 hipError_t launch_team_order(const int* key, int B, int layout, int* sorted, int* order, hipStream_t stream);
 hipError_t launch_path_discretize(int B, const nmpc_path_segment* segs, int seg_stride, const int* nseg,
                                   const double* nearest_u, double period, int num_poses, int holo, float* traj,

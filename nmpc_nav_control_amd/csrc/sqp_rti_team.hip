@@ -110,6 +110,12 @@ constexpr float kStatRelT = 1e-5f;
 // m * mu, which leaves a nearly active bound's multiplier at ~1e-5 and moves u0 by ~1e-3 through the weak input
 // curvature R dt (DESIGN.md "Stopping rule")
 constexpr float kCompMaxRatio = 30.0f;
+// primal infeasibility (status 4, the wrapper's exception path, NMPCNavControl.cpp:14-23): the bound multipliers
+// diverge while the bound residual cannot close. A feasible QP of this OCP keeps them at the size of its cost
+// weights (max 88 over 768 bench-loop QPs with renewals, against > 1e5 by IPM iteration 13-20 for QPs made
+// infeasible as the failure test does; tools/infeas_study.py); the oracle uses the same two constants
+constexpr float kInfeasLambda = 1e5f;
+constexpr float kInfeasRes = 1e-3f;
 #ifndef LIGHT_D
 #define LIGHT_D 4  // record buffers of the forward light sweeps (F0, F1)
 #endif
@@ -361,6 +367,9 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
     float* const tbase = a.scratch + (size_t)inst * (N + 1) * 16 * RS + (lv ? r : 0) * rec_lane<RS, QM>();
     // every lane's own slot (idle lanes: one nobody reads), for P0's unconditional record stores
     float* const tbase_own = a.scratch + (size_t)inst * (N + 1) * 16 * RS + r * rec_lane<RS, QM>();
+    // a record nobody reads (slot 15 of the robot's stage-N block: the idle slot of every model), the target of
+    // stores that lanes without work issue unconditionally
+    float* const tdummy = a.scratch + (size_t)inst * (N + 1) * 16 * RS + (size_t)N * 16 * RS + 15 * rec_lane<RS, QM>();
     // IPM warm start: the bound multipliers of the robot's previous successful solve are still in its records
     const bool warm = P.warm && a.warm && a.warm[inst] && !(a.reset && a.reset[inst]);
     constexpr int KS = 16 * RS;
@@ -803,6 +812,7 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
         for (int j = 0; j < NV; j++) Lrow[j] = 0.0;
         float pv = 0.0f, piv = 0.0f;
         float res_stat = 0.0f, res_ineq = 0.0f, sum_c = 0.0f, max_c = 0.0f, stat_scale = 1.0f, nanf_ = 0.0f;
+        float lam_max = 0.0f;
         bool fail = false;
         const bool act = lv && !done;
         const float a_upd = (it > 0 && !done) ? alpha : 0.0f;
@@ -852,6 +862,7 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
             res_ineq = fmaxf(res_ineq, fmaxf(fabsf(rl), fabsf(rr)));  // NaN: caught by nanf_ (ghat, sig)
             sum_c += ll * tl + lu * tu;
             max_c = fmaxf(max_c, fmaxf(ll * tl, lu * tu));
+            lam_max = fmaxf(lam_max, fmaxf(ll, lu));  // 0 on the kFar-sentinel slots
             const float lamdiff = ll - lu;
             const float sig = ll * itl + lu * itu;
             // predictor rhs (zero complementarity target); SD: the centring target tg_rhs (0 on kFar slots)
@@ -930,8 +941,22 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
             }
             piv = pi_new;
             STAMPF(6);
+#ifndef P1_MASKED_STORE
+            // Unconditional stores: lanes without work (idle slots, finished teams) write a record nobody reads.
+            // Under a lane mask the stores sit in a branch the wave may skip, and the compiler then placed an
+            // s_waitcnt vmcnt(0) at the loop header of the ping-pong sweep (it waited for the stores just issued
+            // and for the prefetch); unconditional, every wait in the loop is counted (tools/isa_waits.py)
+            float* const pk = act ? tbase + (size_t)k * KS : tdummy;
             if constexpr (MS) {
                 // slack / multiplier quad only where a bound lives (elsewhere it holds the constant sentinel)
+                rec_store_range<R::TL, R::TL + 4, RS, QM>(bnd ? pk : tdummy, rc);
+                if constexpr (R::TL > 0) rec_store_range<0, R::TL, RS, QM>(pk, rc);
+                if constexpr (R::TL + 4 < R::P1S1) rec_store_range<R::TL + 4, R::P1S1, RS, QM>(pk, rc);
+            } else {
+                rec_store_range<0, R::P1S1, RS, QM>(pk, rc);
+            }
+#else
+            if constexpr (MS) {
                 if (act && bnd) rec_store_range<R::TL, R::TL + 4, RS, QM>(tbase + (size_t)k * KS, rc);
                 if (act) {
                     if constexpr (R::TL > 0) rec_store_range<0, R::TL, RS, QM>(tbase + (size_t)k * KS, rc);
@@ -940,12 +965,14 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
             } else {
                 if (act) rec_store_range<0, R::P1S1, RS, QM>(tbase + (size_t)k * KS, rc);
             }
+#endif
             STAMPF(7);
         });
         if (it < kStampItsC) STAMP(2 + 4 * it);
         // team reductions
         sum_c = row_sum16(lv ? sum_c : 0.0f);
         max_c = row_max16(lv ? max_c : 0.0f);
+        lam_max = row_max16(lv ? lam_max : 0.0f);
         res_ineq = row_max16(lv ? res_ineq : 0.0f);
         res_stat = row_max16(lv ? res_stat : 0.0f);
         stat_scale = row_max16(stat_scale);
@@ -962,6 +989,9 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
                 stop = true;
             } else if (failf > 0.0f) {
                 status = (mu <= kBreakdownMuT && res_ineq <= P.tol_ineq * 10.0f) ? 0 : 4;
+                stop = true;
+            } else if (lam_max > kInfeasLambda && res_ineq > kInfeasRes) {
+                status = 4;  // primal infeasible: stop now instead of holding the wave for qp_iter_max iterations
                 stop = true;
             } else {
                 const bool stat_ok = res_stat <= P.tol_stat || res_stat <= kStatRelT * stat_scale;

@@ -18,15 +18,21 @@ import os
 import numpy as np
 import torch
 
-from .scenario import make_fleet
+from .scenario import RENEW, SPEED, kappa_max_of, make_fleet
 from .sharding import CommandGather, shard_range
 
 
 class Fleet:
-    """One model's robots on this rank: solver + closed-loop state, all resident on ``dev``."""
+    """One model's robots on this rank: solver + closed-loop state, all resident on ``dev``.
 
-    def __init__(self, model, B, N, seed, dev, start=0, stream=None, solver_factory=None, schedule=None):
+    renew: the stationary loop (scenario.RENEW, nmpc_fleet_sim_step_renew): an arrived robot, or one whose goal /
+    path has been active for its ttl, gets a new one and its next solve resets the controller (the reference's goal
+    / path callbacks call reset_mpc, NMPCNavControlROS.cpp:304-327); a dict overrides RENEW's keys (the tests use
+    short ttls). False: every robot keeps its first goal / path (the fleet parks), as round-2 benches ran."""
+
+    def __init__(self, model, B, N, seed, dev, start=0, stream=None, solver_factory=None, schedule=None, renew=True):
         self.model, self.B, self.N = model, B, N
+        self.seed, self.start = int(seed), int(start)
         self.dev = torch.device(dev)
         self.stream = stream  # None: the current stream; mixed fleets give each model its own HIP stream
         if solver_factory is None:
@@ -48,16 +54,30 @@ class Fleet:
         self.u0 = torch.zeros(self.solver.nu, B, device=self.dev)
         self.status = torch.zeros(B, dtype=torch.int32, device=self.dev)
         self.qp_iter = torch.zeros(B, dtype=torch.int32, device=self.dev)
+        self.renew = None
+        if renew:
+            self.renew = dict(RENEW, kappa_max=kappa_max_of(model), speed=SPEED.get(model, (0.2, 0.8)))
+            if isinstance(renew, dict):
+                self.renew.update(renew)
+        self.ev = t(fl["ev"], torch.int32)
+        self.ttl = t(np.minimum(fl["ttl"], self.renew["ttl_max"]) if self.renew else fl["ttl"], torch.int32)
+        self.reset = torch.zeros(B, dtype=torch.uint8, device=self.dev)  # set by the renewal for the next solve
         self.solver.fleet_sim_step(self.path, self.s, self.pose, self.vel, self.steer, None, None, self.traj,
                                    self.tlen, advance=False, stream=self.stream)
 
-    def solve(self, reset=None):
-        self.solver.run(self.pose, self.vel, self.traj, steer=self.steer, traj_len=self.tlen, reset=reset,
-                        cmd=self.cmd, u0=self.u0, status=self.status, qp_iter=self.qp_iter, stream=self.stream)
+    def solve(self):
+        self.solver.run(self.pose, self.vel, self.traj, steer=self.steer, traj_len=self.tlen,
+                        reset=self.reset if self.renew else None, cmd=self.cmd, u0=self.u0, status=self.status,
+                        qp_iter=self.qp_iter, stream=self.stream)
 
     def advance(self):
-        self.solver.fleet_sim_step(self.path, self.s, self.pose, self.vel, self.steer, self.u0, self.status,
-                                   self.traj, self.tlen, advance=True, stream=self.stream)
+        if self.renew:
+            self.solver.fleet_sim_step_renew(self.path, self.s, self.pose, self.vel, self.steer, self.u0, self.status,
+                                             self.traj, self.tlen, self.ev, self.ttl, self.reset, self.seed,
+                                             self.start, self.renew, stream=self.stream)
+        else:
+            self.solver.fleet_sim_step(self.path, self.s, self.pose, self.vel, self.steer, self.u0, self.status,
+                                       self.traj, self.tlen, advance=True, stream=self.stream)
 
     def tick(self):
         self.solve()
@@ -76,7 +96,8 @@ class Fleet:
                     pose=np.ascontiguousarray(host(self.pose).T), vel=np.ascontiguousarray(host(self.vel).T),
                     steer=host(self.steer) if self.steer is not None else None,
                     traj=np.ascontiguousarray(host(self.traj).transpose(2, 0, 1)),
-                    tlen=np.ascontiguousarray(self.tlen.cpu().numpy(), np.int32))
+                    tlen=np.ascontiguousarray(self.tlen.cpu().numpy(), np.int32),
+                    reset=(np.ascontiguousarray(self.reset.cpu().numpy(), np.uint8) if self.renew else None))
 
 
 class FleetNode:
@@ -98,7 +119,7 @@ class FleetNode:
     With one stream (a single model, groups = 1) both are the same sequential loop."""
 
     def __init__(self, models, N, seed, dev, rank=0, world=1, gather=False, solver_factory=None, groups=1,
-                 decoupled=None, schedule=None):
+                 decoupled=None, schedule=None, renew=True):
         self.dev = torch.device(dev)
         self.rank, self.world = rank, world
         cuda = self.dev.type == "cuda"
@@ -118,7 +139,7 @@ class FleetNode:
                 sched = schedule if schedule is not None else ("interleaved" if len(models) > 1 and stream is not None
                                                                else None)
                 self.fleets.append(Fleet(m, ghi - glo, N, seed + 100 * j, self.dev, start=lo + glo, stream=stream,
-                                         solver_factory=solver_factory, schedule=sched))
+                                         solver_factory=solver_factory, schedule=sched, renew=renew))
         self.B = sum(f.B for f in self.fleets)
         self.offs = [int(v) for v in np.cumsum([0] + [f.B for f in self.fleets])]
         self.gather = CommandGather(5, [self.B] * world, self.dev) if gather else None
@@ -127,6 +148,11 @@ class FleetNode:
         self.iters_sum = torch.zeros(self.B, dtype=torch.int64, device=self.dev)
         self.iters_max = torch.zeros(self.B, dtype=torch.int32, device=self.dev)
         self.fail_cnt = torch.zeros(self.B, dtype=torch.int64, device=self.dev)
+        # per-fleet histograms of the executed IPM iterations (robot-ticks; the tail of the window) and the
+        # count / iterations of the solves that followed a renewal (cold: reset iterate, cold IPM)
+        self.iter_hist = [torch.zeros(64, dtype=torch.int64, device=self.dev) for _ in self.fleets]
+        self.cold_cnt = torch.zeros(self.B, dtype=torch.int64, device=self.dev)
+        self.cold_iters = torch.zeros(self.B, dtype=torch.int64, device=self.dev)
 
     def tick_all(self):
         """One control tick of every robot of this rank (joined: with the fleet-wide tick boundary)."""
@@ -149,18 +175,20 @@ class FleetNode:
             main.wait_event(done)
 
     def accumulate_one(self, j):
-        """Statistics of fleet j's last tick, on fleet j's stream (decoupled streams) or the current one."""
+        """Statistics of fleet j's last solve, on fleet j's stream (or the current one); called between the solve
+        and the plant / renewal step, which rewrites the reset flags the solve ran with."""
         f = self.fleets[j]
         sl = slice(self.offs[j], self.offs[j + 1])
-        ctx = torch.cuda.stream(f.stream) if (self.decoupled and f.stream is not None) else _nullctx()
+        ctx = torch.cuda.stream(f.stream) if f.stream is not None else _nullctx()
         with ctx:
             self.iters_sum[sl] += f.qp_iter
             torch.maximum(self.iters_max[sl], f.qp_iter, out=self.iters_max[sl])
             self.fail_cnt[sl] += f.status != 0
-
-    def accumulate(self):
-        for j in range(len(self.fleets)):
-            self.accumulate_one(j)
+            self.iter_hist[j] += torch.bincount(f.qp_iter.clamp(0, 63).long(), minlength=64)
+            if f.renew:
+                cold = f.reset.to(torch.int64)  # the flags this solve ran with (advance() rewrites them)
+                self.cold_cnt[sl] += cold
+                self.cold_iters[sl] += cold * f.qp_iter
 
     def join(self):
         """Make the current stream wait for every fleet stream (end of a decoupled run)."""
@@ -173,8 +201,22 @@ class FleetNode:
 
     def reset_stats(self):
         self.join()
-        for t_ in (self.iters_sum, self.iters_max, self.fail_cnt):
+        for t_ in (self.iters_sum, self.iters_max, self.fail_cnt, self.cold_cnt, self.cold_iters, *self.iter_hist):
             t_.zero_()
+
+    def iter_stats(self):
+        """Executed IPM iterations over the robot-ticks since reset_stats: mean, p50, p99, p99.9, max (all fleets),
+        and the solves after a renewal (count, mean iterations)."""
+        h = torch.stack(self.iter_hist).sum(0).cpu().numpy().astype(np.float64)
+        n = h.sum()
+        if n == 0:
+            return {}
+        c = np.cumsum(h) / n
+        q = lambda p: int(np.searchsorted(c, p))  # noqa: E731
+        cold = int(self.cold_cnt.sum().item())
+        return {"mean": float((np.arange(64) * h).sum() / n), "p50": q(0.5), "p99": q(0.99), "p999": q(0.999),
+                "max": int(np.nonzero(h)[0].max()), "robot_ticks": int(n), "renewals": cold,
+                "cold_mean": (float(self.cold_iters.sum().item()) / cold) if cold else None}
 
     def gather_commands(self):
         """All-gather [u0 (padded to 4 rows); status] of every robot to every rank: [5][B * world]."""
@@ -198,8 +240,8 @@ class FleetNode:
                 f.solve()
                 if timer is not None:
                     timer.end(j, f.stream)
-                f.advance()
                 self.accumulate_one(j)
+                f.advance()
             return
         cuda = self.dev.type == "cuda"
         main = torch.cuda.current_stream(self.dev) if cuda else None
@@ -214,12 +256,12 @@ class FleetNode:
             f.solve()
             if timer is not None:
                 timer.end(j, f.stream if f.stream is not None else main)
+            self.accumulate_one(j)
             f.advance()
             if self.multi:
                 done = torch.cuda.Event()
                 done.record(f.stream)
                 main.wait_event(done)
-        self.accumulate()
         if self.gather is not None:
             self.gather_commands()
 

@@ -35,6 +35,10 @@ extern "C" {
 #define OC_NUMAX 4
 #define OC_NYMAX 15
 #define OC_NBMAX 8 /* bounded components per stage: nbu + nbx (omni4: 4 + 4) */
+/* IPM infeasibility exit (status 4): largest bound multiplier above OC_INFEAS_LAMBDA while the bound residual is
+ * above OC_INFEAS_RES (the device kernel uses the same two constants) */
+#define OC_INFEAS_LAMBDA 1e5
+#define OC_INFEAS_RES 1e-3
 
 typedef struct oc_params {
     int model, N;

@@ -11,7 +11,7 @@ import numpy as np
 import torch
 
 from helpers import plant_measure
-from nmpc_nav_control_amd.scenario import arc_pose
+from nmpc_nav_control_amd.scenario import arc_pose, renew_step
 from oracle.oracle import Oracle
 
 
@@ -65,9 +65,16 @@ class OracleFleetSolver:
         if qp_iter is not None:
             qp_iter.copy_(torch.from_numpy(it_o.astype(np.int32)))
 
-    def fleet_sim_step(self, path, s, pose, vel, steer, u0, status, traj, traj_len, advance=True, stream=None):
+    def fleet_sim_step_renew(self, path, s, pose, vel, steer, u0, status, traj, traj_len, ev, ttl, reset, seed, start,
+                             renew, stream=None):
+        """k_fleet_sim with its renewal record (scenario.renew_step after the plant step)."""
+        self.fleet_sim_step(path, s, pose, vel, steer, u0, status, traj, traj_len, advance=True,
+                            renew=(ev, ttl, reset, seed, start, renew))
+
+    def fleet_sim_step(self, path, s, pose, vel, steer, u0, status, traj, traj_len, advance=True, stream=None,
+                       renew=None):
         """numpy restatement of k_fleet_sim (fleet_sim.hip): plant RK4 step with the applied u0, measurement,
-        reference regeneration (arc path or goal pose)."""
+        goal / path renewal (optional), reference regeneration (arc path or goal pose)."""
         o, N = self.o, self.N
         P = path.numpy().astype(np.float64)
         B = pose.shape[1]
@@ -86,6 +93,15 @@ class OracleFleetSolver:
                 vs[:, i] = v3
                 if steer is not None:
                     steer[i] = stn
+            if renew is not None:
+                ev, ttl, reset, seed, start, rn = renew
+                Pn, sn, evn, ttln = P, s.numpy(), ev.numpy(), ttl.numpy()
+                reset[i] = renew_step(self.model, Pn, sn, ps[:, i].astype(np.float64), evn, ttln, seed, start, i,
+                                      renew={k: rn[k] for k in ("ttl_min", "ttl_max", "goal_r_lo", "goal_r_hi",
+                                                                 "len_lo", "len_hi", "pos_tol", "ang_tol")},
+                                      speed=rn["speed"])
+                path[:, i] = torch.from_numpy(P[:, i].astype(np.float32))
+                P[:, i] = path[:, i].numpy().astype(np.float64)
             if P[5, i] < 0:
                 traj[0, :, i] = torch.from_numpy(P[:3, i].astype(np.float32))
                 if traj_len is not None:

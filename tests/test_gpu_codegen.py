@@ -68,3 +68,57 @@ def test_generated_defaults_drive_the_solve(built, tmp_path):
     np.testing.assert_allclose(u0, ub_new[0], atol=1e-3)
     # the bound baked from a_max is active on the first input
     assert np.abs(u0).max() == pytest.approx(0.5, abs=1e-3)
+
+
+@pytest.mark.parametrize("geometry", ["diff", "omni4", "tric"])
+def test_reference_codegen_self_check(built, geometry):
+    """The only solve check the reference holds (scripts/<geometry>/generate_c_code.py: diff :58-66 and :79-83, the
+    omni4 / tric copies likewise): right after creating the solver from the shipped codegen yaml, one solve() from
+    the create iterate with x0 = [0, 0, pi, 0, ...], yref = 0 and the CODEGEN weights (Q / R / QN_diag of
+    config/nmpc_nav_control_acados_models.yaml, not the ROS override) at the shipped N = 80 must return status 0.
+    Here through the in-tree libacados_ocp_solver_<name>.so (generated from configs/acados_models.yaml, the same
+    values) with no setter called; u0 and the whole predicted state trajectory agree with the fp64 oracle
+    configured the same way."""
+    cfg = yaml.safe_load(open(os.path.join(ROOT, "configs", "acados_models.yaml")))
+    d = gen.load_parameters(geometry, cfg[f"{geometry}_params"])
+    name = d["name"]
+    assert d["N"] == 80
+    S = _lib.solver_lib(name)
+    L = _lib.lib()
+    os.environ.pop(f"NMPC_AMD_{name.upper()}_N", None)
+    cap = getattr(S, f"{name}_acados_create_capsule")()
+    assert getattr(S, f"{name}_acados_create")(cap) == 0
+    c = cap.contents
+    assert getattr(S, f"{name}_acados_solve")(cap) == 0  # generate_c_code.py:79-83 raises otherwise
+    o = Oracle(geometry, d["N"], dt=d["tf"] / d["N"], p=d["p"] + [0.0] * (3 - len(d["p"])),
+               W=d["W"] + [0.0] * (15 - len(d["W"])), W_e=d["W_e"] + [0.0] * (11 - len(d["W_e"])),
+               lbx=d["lbx"] + [0.0] * (4 - len(d["lbx"])), ubx=d["ubx"] + [0.0] * (4 - len(d["ubx"])),
+               lbu=d["lbu"] + [0.0] * (4 - len(d["lbu"])), ubu=d["ubu"] + [0.0] * (4 - len(d["ubu"])),
+               terminal_hack=0)
+    N, nx, nu = o.N, o.nx, o.nu
+    dptr = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+    xs = np.zeros((N + 1, nx))
+    us = np.zeros((N, nu))
+    for k in range(N + 1):
+        row = np.zeros(nx)
+        L.ocp_nlp_out_get(c.nlp_config, c.nlp_dims, c.nlp_out, k, b"x", dptr(row))
+        xs[k] = row
+        if k < N:
+            ur = np.zeros(nu)
+            L.ocp_nlp_out_get(c.nlp_config, c.nlp_dims, c.nlp_out, k, b"u", dptr(ur))
+            us[k] = ur
+    getattr(S, f"{name}_acados_free")(cap)
+    getattr(S, f"{name}_acados_free_capsule")(cap)
+    xb, ub = o.iterate_create()
+    x0 = xb[0].copy()
+    assert x0[2] == np.pi and np.count_nonzero(x0) == 1
+    st, stats, xb_new, ub_new = o.sqp_rti(xb, ub, x0, np.zeros((N + 1, o.ny)), np.array(d["W_e"]))
+    assert st == 0
+    print(f"\n{geometry} codegen self-check N={N}: oracle {stats['qp_iter']} IPM iterations; "
+          f"u0 {us[0]} err {np.abs(us[0] - ub_new[0]).max():.2e}, x err {np.abs(xs - xb_new).max():.2e}")
+    np.testing.assert_allclose(us, ub_new, atol=1e-3)
+    np.testing.assert_allclose(xs, xb_new, atol=1e-3)
+    if geometry != "tric":  # the robot turns towards the zero heading at full input (oracle: u0 = [2, -2] / [1]*4)
+        assert np.abs(us[0]).max() > 0.5
+    # tric at rest: theta' = (v / d) sin(alpha) has no first-order dependence on v or alpha at v = alpha = 0, so
+    # the linearised OCP cannot turn it and u0 = 0 (the oracle too)

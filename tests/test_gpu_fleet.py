@@ -33,7 +33,7 @@ def replay_and_compare(fleet, oracle, tick_fn):
     tick_fn()
     torch.cuda.synchronize()
     xb_o, ub_o, cr_o = sn["xbar"].copy(), sn["ubar"].copy(), sn["carried"].copy()
-    nf, cmd_o, u0_o, st_o, _ = oracle.batch_tick(sn["pose"], sn["vel"], sn["steer"], sn["traj"], sn["tlen"], None,
+    nf, cmd_o, u0_o, st_o, _ = oracle.batch_tick(sn["pose"], sn["vel"], sn["steer"], sn["traj"], sn["tlen"], sn["reset"],
                                                  cr_o, xb_o, ub_o, nthreads=NTHREADS)
     after = fleet.snapshot()
     st = fleet.status.cpu().numpy()
@@ -102,7 +102,7 @@ def test_mixed_fleet_concurrent_streams_full_replay(built):
         torch.cuda.synchronize()
         for f, o, sn in zip(node.fleets, oracles, snaps):
             xb_o, ub_o, cr_o = sn["xbar"].copy(), sn["ubar"].copy(), sn["carried"].copy()
-            _, cmd_o, u0_o, st_o, _ = o.batch_tick(sn["pose"], sn["vel"], sn["steer"], sn["traj"], sn["tlen"], None,
+            _, cmd_o, u0_o, st_o, _ = o.batch_tick(sn["pose"], sn["vel"], sn["steer"], sn["traj"], sn["tlen"], sn["reset"],
                                                    cr_o, xb_o, ub_o, nthreads=NTHREADS)
             st = f.status.cpu().numpy()
             assert (st == 0).all() and (st_o == 0).all(), f.model
@@ -171,13 +171,15 @@ def test_failure_stays_on_its_robot(built):
     """a NaN or a QP failure on one robot must not poison the others. In a B=4096 diff N=40 tick
     (the metric config) robot 7 gets a NaN pose (x0), robot 1001 NaN references (yref) and robot 2050 an
     infeasible QP (carried vel-ref 50 m/s against the 1 m/s bound at stage 1):
-      - the NaN robots report status 1 after their first IPM iteration, the infeasible one fails or runs to
-        qp_iter_max (status 0 at the cap, DESIGN.md "Stopping rule"); a failed robot gets a zero (stop) command
-        and keeps its carried refs and iterate: the reference throws (NMPCNavControl.cpp:14-23) and the node
-        stops the robot (NMPCNavControlROS.cpp:716-719);
+      - the NaN robots report status 1 after their first IPM iteration; the infeasible one reports status 4 (QP
+        failure) from the IPM's infeasibility exit (diverging bound multipliers with an open bound residual,
+        DESIGN.md "Stopping rule") well before qp_iter_max; a failed robot gets a zero (stop) command and keeps
+        its carried refs and iterate: the reference throws (NMPCNavControl.cpp:14-23) and the node stops the robot
+        (NMPCNavControlROS.cpp:716-719);
       - every other robot's u0, cmd, status, qp_iter, iterate and carried refs are bit-identical to the clean
         tick;
-      - with only the NaN robots injected the kernel time stays within 10 % of the clean tick."""
+      - with all three injected the kernel time stays within 10 % of the clean tick: one hard robot does not
+        hold the launch for 50 iterations."""
     N, B = 40, 4096
     f = Fleet("diff", B, N, SEED + 1, DEV)
     for _ in range(20):
@@ -207,7 +209,7 @@ def test_failure_stays_on_its_robot(built):
     bad = [bad_x0, bad_ref, bad_qp]
     st, it = dirty["status"].cpu().numpy(), dirty["qp_iter"].cpu().numpy()
     assert st[bad_x0] == 1 and st[bad_ref] == 1 and it[bad_x0] == 0 and it[bad_ref] == 0, (st[bad], it[bad])
-    assert st[bad_qp] != 0 or it[bad_qp] == 50, (st[bad_qp], it[bad_qp])
+    assert st[bad_qp] == 4 and it[bad_qp] < 30, (st[bad_qp], it[bad_qp])
     good = np.ones(B, bool)
     good[bad] = False
     g = torch.from_numpy(good).to(DEV)
@@ -221,10 +223,10 @@ def test_failure_stays_on_its_robot(built):
             assert torch.equal(dirty["C"][:, i], st0["C"][:, i] if i != bad_qp else dirty["C"][:, i])
             assert torch.equal(dirty["X"][:, i], st0["X"][:, i]) and torch.equal(dirty["U"][:, i], st0["U"][:, i])
 
-    t_nan = _timed_solve(f, lambda: inject(False))
-    print(f"\nclean {t_clean:.3f} ms, with 2 NaN robots {t_nan:.3f} ms; infeasible robot: status {st[bad_qp]}, "
-          f"qp_iter {it[bad_qp]}")
-    assert t_nan <= 1.10 * t_clean, (t_nan, t_clean)
+    t_bad = _timed_solve(f, lambda: inject(True))
+    print(f"\nclean {t_clean:.3f} ms (max qp_iter {int(clean['qp_iter'].max())}), with 2 NaN robots and the "
+          f"infeasible one {t_bad:.3f} ms; infeasible robot: status {st[bad_qp]}, qp_iter {it[bad_qp]}")
+    assert t_bad <= 1.10 * t_clean, (t_bad, t_clean)
 
 
 def test_reset_mode_keeps_carried_refs(built):
@@ -242,3 +244,46 @@ def test_reset_mode_keeps_carried_refs(built):
     torch.cuda.synchronize()
     X = xv.to_tensor().reshape(21, 7, 64)
     assert (cv.to_tensor() == 0).all() and (X[:, 2] == np.float32(np.pi)).all()
+
+
+def test_renewal_on_device(built):
+    """The stationary loop on the device (nmpc_fleet_sim_step_renew): short ttls (2-6 ticks) make every robot renew
+    its goal / path several times. Each renewal draws exactly the harness hash's values (ttl bit for bit; goal
+    distance, heading, arc length and speed to fp32 rounding), sets the robot's reset flag for its next solve,
+    and the reset solves match the fp64 oracle given the same flags (every robot replayed on the last tick)."""
+    from nmpc_nav_control_amd.scenario import fleet_ttl, fleet_u
+    lo, hi = 2, 6
+    N, B, seed = 40, 1024, SEED + 1
+    f = Fleet("diff", B, N, seed, DEV, renew=dict(ttl_min=lo, ttl_max=hi))
+    o = Oracle("diff", N)
+    gi = np.arange(B)
+    total = 0
+    for tick in range(12):
+        f.solve()
+        f.advance()
+        torch.cuda.synchronize()
+        st = f.status.cpu().numpy()
+        assert (st == 0).all(), (tick, np.nonzero(st)[0][:8])
+        r = f.reset.cpu().numpy().astype(bool)
+        ev, ttl = f.ev.cpu().numpy(), f.ttl.cpu().numpy()
+        path, pose, s = f.path.cpu().numpy(), f.pose.cpu().numpy(), f.s.cpu().numpy()
+        total += int(r.sum())
+        if not r.any():
+            continue
+        assert np.array_equal(ttl[r], fleet_ttl(seed, gi[r], ev[r], lo, hi))
+        g = r & (path[5] < 0)
+        p = r & (path[5] > 0)
+        u1 = fleet_u(seed, gi, ev, 1)
+        u2 = fleet_u(seed, gi, ev, 2)
+        dist = np.hypot(path[0] - pose[0], path[1] - pose[1])
+        assert np.abs(dist[g] - (0.3 + 1.2 * u1[g])).max() < 1e-5
+        assert np.abs(path[2, g] - np.pi * (2 * u2[g] - 1)).max() < 1e-5
+        assert (s[p] == 0).all() and np.abs(dist[p] - 0.2 * u1[p]).max() < 1e-5
+        assert np.abs(path[5, p] - (3.0 + 2.0 * fleet_u(seed, gi[p], ev[p], 5))).max() < 1e-5
+        assert np.abs(path[4, p] - (0.2 + 0.6 * fleet_u(seed, gi[p], ev[p], 4))).max() < 1e-5
+    assert total >= 2 * B, total
+    eu, ex, ec, st, st_o, _ = replay_and_compare(f, o, f.solve)
+    assert int(f.reset.sum()) > 0
+    assert (st == 0).all() and (st_o == 0).all()
+    print(f"\nrenewals {total} over 12 ticks; reset-tick replay: u0 err {eu:.2e}, x err {ex:.2e}")
+    assert eu <= TOL_U and ex <= TOL_X and ec <= TOL_U

@@ -151,7 +151,7 @@ class Emu:
                 np.einsum("bij,bj->bi", Q["B"][:, k], dz[:, k, :nu])
         return dz, ok
 
-    def solve(self, polish=None, verbose=False, single=None, start=None, eta_scale=1.0, lag2=None):
+    def solve(self, polish=None, verbose=False, single=None, start=None, eta_scale=1.0, lag2=None, trace=None):
         """Run the IPM on every robot. polish: None or dict(mu=threshold, rho=..., tol=...) -- after the
         residual test of an iteration whose mu is below the threshold, try the active-set polish; a robot whose
         polish passes its KKT test stops there. Returns per-robot iterations, polish attempts, solutions."""
@@ -180,6 +180,10 @@ class Emu:
             stop = (res_ineq <= self.tol_ineq) & ((stat_ok & (mu <= self.tol_comp) & cmax_ok) |
                                                   (mu <= 1e-2 * self.tol_comp) | (stalled & cmax_ok))
             stop |= it >= self.iter_max
+            if trace is not None:  # per-iteration state of every robot (infeasibility / stagnation studies)
+                lmax = np.where(self.bnd, np.maximum(ll, lu), 0.0).max(axis=(1, 2))
+                trace.append(dict(it=it, res_ineq=res_ineq, res_stat=res_stat, mu=mu, lmax=lmax,
+                                  alpha=alpha_prev.copy(), done=done.copy()))
             new = stop & ~done
             zsol[new] = z[new]
             iters[new] = it
