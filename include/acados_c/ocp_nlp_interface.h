@@ -25,7 +25,8 @@ typedef struct ocp_nlp_dims {
 typedef struct ocp_nlp_in { struct nmpc_capsule_impl* impl; } ocp_nlp_in;
 typedef struct ocp_nlp_out {
     struct nmpc_capsule_impl* impl;
-    double inf_norm_res; /* max-abs QP stationarity residual of the last solve (not an NLP residual) */
+    double inf_norm_res; /* max of the last QP's residuals at IPM exit (stationarity, bounds, complementarity);
+                            not acados' NLP residual (INTEGRATION.md "Semantic differences") */
     double total_cost;
     int sqp_iter;
 } ocp_nlp_out;

@@ -57,8 +57,12 @@ typedef struct nmpc_model_params {
     double qp_sigma_lo, qp_sigma_hi; /* 0.01, 0.5 */
     /* IPM warm start (default 1): a robot whose previous solve on this handle succeeded starts its bound
      * multipliers at max(lambda_previous, qp_warm_kappa / t) instead of qp_mu0 / t (the QP solution is the same;
-     * the IPM path is shorter). 0 gives acados' cold start every tick. Reset robots and nmpc_batch_init_iterate
-     * start cold. The capsule ABI always starts cold (its capsules do not own a slot). */
+     * the IPM path is shorter, so qp_iter counts are not acados'). This departs from the reference, whose
+     * generated HPIPM never sets qp_solver_warm_start (every QP there starts cold); 0 restores that. Reset robots,
+     * nmpc_batch_init_iterate and nmpc_batch_forget_warm start cold. The multipliers live in the handle's slot i
+     * of instance i: keep an instance's slot stable across calls (nmpc_batch_solve_iterate included) or clear it
+     * with nmpc_batch_forget_warm. The capsule ABI warm-starts a capsule only while it still owns its engine slot
+     * (its last solve there succeeded and no reset / create came in between), with kappa 0.01. */
     int qp_warm_start;
     double qp_warm_kappa; /* diff 0.2, omni4 / tric 0.01 */
 } nmpc_model_params;
@@ -162,6 +166,11 @@ int nmpc_batch_set_schedule(nmpc_batch* b, int mode);
 /* Device pointers of the resident state: xbar [(N+1)*NX][stride], ubar [N*NU][stride],
  * carried [NBX][stride]; stride = capacity. */
 int nmpc_batch_state(nmpc_batch* b, float** xbar, float** ubar, float** carried, int* stride);
+
+/* Forget the IPM warm start of instances [0, B) where mask[i] != 0 (mask NULL: all of them): their next solve
+ * starts its multipliers cold (qp_mu0 / t), as after a reset, while the iterate is kept. For callers that move
+ * instances between slots (a slot's multipliers belong to whatever instance solved there last). mask: device. */
+int nmpc_batch_forget_warm(nmpc_batch* b, int B, const unsigned char* mask, void* stream);
 
 /* Device pointers of the IPM warm-start state (qp_warm_start): warm [capacity] per-robot flags (1: the robot's
  * last solve succeeded) and the scratch records [scratch_bytes] that hold each robot's multipliers. With

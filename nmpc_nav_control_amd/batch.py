@@ -112,6 +112,13 @@ class BatchSolver:
         return (_DeviceView(w.value, (1, self.capacity), self.device, torch.uint8),
                 _DeviceView(sc.value, (1, nb.value // 4), self.device))
 
+    def forget_warm(self, mask=None, B=None, stream=None):
+        """Cold IPM start at the next solve for the robots where mask != 0 (None: all of them); the iterate stays
+        (nmpc_batch_forget_warm)."""
+        B = self.capacity if B is None else int(B)
+        check(lib().nmpc_batch_forget_warm(self._h, B, _ptr(mask, U8, (B,), "mask"), _stream(stream)),
+              "nmpc_batch_forget_warm")
+
     def save_state(self):
         """Device copies of everything a solve reads from the handle (iterate, carried refs, warm start)."""
         return [v.to_tensor() for v in self.state() + self.warm_state()]
@@ -141,7 +148,8 @@ class BatchSolver:
     def solve_iterate(self, x0, yref, xbar, ubar, We=None, reset=None, status=None, qp_iter=None, qp_res=None,
                       stream=None):
         """nmpc_batch_solve with a caller-held iterate: xbar [(N+1)*NX][ld], ubar [N*NU][ld] are read and overwritten
-        with the new iterate in place (nmpc_batch_solve_iterate)."""
+        with the new iterate in place (nmpc_batch_solve_iterate). The IPM warm start still comes from the handle's
+        slot i: keep instance i in slot i across calls, or call forget_warm after reordering."""
         B = x0.shape[1]
         if not 0 <= B <= self.capacity:
             raise ValueError(f"batch {B} exceeds the capacity {self.capacity}")

@@ -446,7 +446,10 @@ void solve_group(std::vector<nmpc_capsule_impl*>& cs, std::vector<Packed>& ps, c
         nmpc_capsule_impl* c = cs[idx[q]];
         c->status = hst[q];
         c->qp_iter = hit[q];
-        c->out.inf_norm_res = hres[q];  // row 0 of qp_res: max |QP stationarity residual| at IPM exit
+        // max of the QP's residuals at IPM exit: stationarity, bound residual, complementarity (qp_res rows 0-2; the
+        // dynamics hold exactly in the dynamics-feasible IPM). acados' inf_norm_res is the NLP residual, which
+        // RTI does not refresh and the reference never uses (NMPCNavControlDiff.cpp:146)
+        c->out.inf_norm_res = std::fmax(std::fmax(hres[q], hres[(size_t)n + q]), hres[(size_t)2 * n + q]);
         c->sqp_iter = 1;
         c->out.sqp_iter = 1;
         c->time_tot = tt;

@@ -158,6 +158,12 @@ __global__ void k_init_iterate(float* xbar, float* ubar, float* carried, unsigne
         for (int j = 0; j < nbx; j++) carried[(size_t)j * stride + i] = 0.0f;
 }
 
+__global__ void k_forget_warm(unsigned char* warm, const unsigned char* mask, int B)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < B && (!mask || mask[i])) warm[i] = 0;
+}
+
 int check_params(const nmpc_model_params* prm)
 {
     int nx, nu, nbx, nbu, np;
@@ -532,6 +538,15 @@ int nmpc_batch_state(nmpc_batch* b, float** xbar, float** ubar, float** carried,
     if (carried) *carried = b->carried;
     if (stride) *stride = b->capacity;
     return NMPC_OK;
+}
+
+int nmpc_batch_forget_warm(nmpc_batch* b, int B, const unsigned char* mask, void* stream)
+{
+    if (!b) return set_err(NMPC_ERR_ARG, "batch is NULL");
+    if (B < 0 || B > b->capacity) return set_err(NMPC_ERR_ARG, "B out of range [0, capacity]");
+    if (B == 0) return NMPC_OK;
+    hipLaunchKernelGGL(k_forget_warm, dim3((B + 255) / 256), dim3(256), 0, (hipStream_t)stream, b->warm, mask, B);
+    return hip_err(hipGetLastError(), "forget_warm launch");
 }
 
 int nmpc_batch_warm_state(nmpc_batch* b, unsigned char** warm, float** scratch, size_t* scratch_bytes)

@@ -56,7 +56,8 @@ struct KArgs {
     unsigned char* warm;  // [stride] resident: 1 if the robot's last solve succeeded (its records hold its
                           // multipliers), or nullptr (cold start, nothing written)
     int dense;      // the launch has more waves than the device has SIMDs (selects the team kernel variant)
-    int split;      // one wave per robot, P0's integrations spread over its four rows (small batches)
+    int split;      // one 256-lane block per robot: P0's integrations spread over its 16 rows (4 waves, stage k on
+                    // row k mod 16, joined by a block barrier); small batches
 };
 
 template <class M>

@@ -453,8 +453,8 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
 
     // ---- P0: linearisation (lane v: nominal step + column v), gradient, bounds, feasible initial iterate --
     // Split launches: the RK4 integrations and every global load of P0 do not depend on each other; only the
-    // initial-iterate simulation (and the reference unwrap) is a recursion over the stages. The wave's four
-    // rows take stages row, row + 4, ... and leave each lane's stage inputs in LDS ([k][field][lane], SF
+    // initial-iterate simulation (and the reference unwrap) is a recursion over the stages. The block's 16 rows
+    // (4 waves) take stages row, row + 16, ... and, after a block barrier, leave each lane's stage inputs in LDS ([k][field][lane], SF
     // fields: zbar, yref entry, warm multipliers, defect b_k = xn_i - xbar_{k+1,i}, the NGV varying Jacobian
     // rows) and run-mode reference poses in row 0's pose slice; row 0 then runs the serial pass from LDS only.
     constexpr int SF = 5 + NGV;

@@ -1,5 +1,6 @@
-"""Split launches (KArgs::split, small batches: one wave per robot, P0's integrations spread over the wave's four
-rows, the serial initial-iterate pass reading its stage inputs from LDS) against the unsplit team launch of the
+"""Split launches (KArgs::split, small batches: one 256-lane block per robot, P0's integrations spread over the
+block's 16 rows (4 waves, stages row, row + 16, ..., joined by a block barrier), the serial initial-iterate pass
+reading its stage inputs from LDS) against the unsplit team launch of the
 same inputs (NMPC_AMD_SPLIT_MAX=0 at handle creation), in every kernel mode: solve (the capsule ABI's path,
 NMPCNavControlDiff.cpp:142), run with caller poses, and run_path (getNextNPoses in the launch). Both launches run
 the same fp32 IPM from the same linearisation, so they agree to fp32 rounding (the RK4 code is the same function
