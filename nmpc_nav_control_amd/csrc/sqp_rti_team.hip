@@ -59,6 +59,12 @@ __device__ unsigned long long g_stamps_c1[256][kStampIts];
 #define STAMPC1() ((void)0)
 #endif
 
+#ifndef NMPC_DZ_IN_RECORD
+constexpr bool kDzPlane = true;
+#else
+constexpr bool kDzPlane = false;  // A/B: the round-2 layout, DZ a field of the lane record
+#endif
+
 template <class M, bool SD = false>
 struct TeamRec {
     static constexpr int NX = M::NX, NU = M::NU, NV = NX + NU, NGV = M::NGV;
@@ -80,17 +86,22 @@ struct TeamRec {
     static constexpr int LB = L2 ? 8 : ((NU == 2) ? 9 : 12), UB = LB + 1;  // bounds relative to the SQP iterate
     static constexpr int GV = L2 ? 10 : ((NU == 2) ? 12 : 14);      // NGV varying rows of column v of [B A]
     static constexpr int NL = GV + NGV;                             // prefix read by the light sweeps
-    static constexpr int DZ = NL, GR = NL + 1;                      // combined direction, cost gradient (P1 only)
+    // combined direction, cost gradient (P1 only). DZ plane (default): the forward sweep writes one float per lane
+    // and stage; in the lane record that dirtied a whole 32-byte sector per lane (8x the bytes), so DZ lives in a
+    // dense plane [robot][stage][16 lanes] (64 B per team and stage, 2 sectors for 9 lanes) and its register slot
+    // sits past the record's stored fields
+    static constexpr int GR = kDzPlane ? NL : NL + 1;
     static constexpr int RU = L2 ? GR + 1 : LM + NU;                // u residual (corrector sweeps)
     static constexpr int DZA = L2 ? GR + 2 : Z + 1 + ((NU == 2) ? 2 : 0);  // affine direction
+    static constexpr int DZ = kDzPlane ? (L2 ? GR + 3 : GR + 1) : NL;
     static constexpr int P1L0 = L2 ? Z : ((NU == 2) ? TL : Z), P1L1 = GR + 1;  // P1 loads
     static constexpr int P1S1 = L2 ? 8 : 12;                        // P1 stores [0, P1S1)
     static_assert(NU == 2 || NU == 4, "layouts for NU = 2 and 4");
     static_assert(L2 || (RU < ((NU == 2) ? TL : Z) && DZA < P1S1), "P1 store block holds RU and DZA");
     static_assert(LU < P1S1 && Z < P1S1 && LM + NU <= P1S1, "P1 store block");
     static constexpr int NF = NL, NB = NL;
-    static constexpr int RS = (GR + 1 + 3) / 4 * 4 > ((RU > DZA ? RU : DZA) + 1 + 3) / 4 * 4
-                                  ? (GR + 1 + 3) / 4 * 4 : ((RU > DZA ? RU : DZA) + 1 + 3) / 4 * 4;  // dwordx4
+    static constexpr int MAXF = (GR > RU ? GR : RU) > (DZA > DZ ? DZA : DZ) ? (GR > RU ? GR : RU) : (DZA > DZ ? DZA : DZ);
+    static constexpr int RS = (MAXF + 1 + 3) / 4 * 4;  // dwordx4 records (and the register image of one)
     static constexpr int NQ = RS / 4;
     static_assert(NV <= 16, "a team holds at most 16 variables");
     static_assert(TL % 4 == 0, "bound quad aligned");
@@ -99,7 +110,8 @@ struct TeamRec {
 template <class M>
 size_t team_scratch_floats(int N, int stride)
 {
-    return (size_t)stride * (N + 1) * 16 * TeamRec<M>::RS + 64;
+    // the lane records [robot][stage][slot][RS], then the DZ plane [robot][stage][16]
+    return (size_t)stride * (N + 1) * 16 * (TeamRec<M>::RS + (kDzPlane ? 1 : 0)) + 64;
 }
 
 namespace {
@@ -370,6 +382,8 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
     // a record nobody reads (slot 15 of the robot's stage-N block: the idle slot of every model), the target of
     // stores that lanes without work issue unconditionally
     float* const tdummy = a.scratch + (size_t)inst * (N + 1) * 16 * RS + (size_t)N * 16 * RS + 15 * rec_lane<RS, QM>();
+    // this lane's DZ in the dense plane after the records: dzbase + k * 16 (every lane its own float)
+    float* const dzbase = a.scratch + (size_t)a.stride * (N + 1) * 16 * RS + (size_t)inst * (N + 1) * 16 + r;
     // IPM warm start: the bound multipliers of the robot's previous successful solve are still in its records
     const bool warm = P.warm && a.warm && a.warm[inst] && !(a.reset && a.reset[inst]);
     constexpr int KS = 16 * RS;
@@ -645,6 +659,7 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
         // (profiles/r02/ab/uncond_stores.txt)
         if constexpr (NV > 12) rec_store<RS, QM>(tbase_own + (size_t)k * KS, rec);
         else if (lv) rec_store<RS, QM>(tbase + (size_t)k * KS, rec);
+        if constexpr (kDzPlane) dzbase[(size_t)k * 16] = 0.0f;  // P1 of iteration 0 applies a zero step
         // dynamics-feasible initial states: dx_{k+1} = A dx_k + b_k (inputs start at du = 0, dx_0 = x0 - xbar_0);
         // row i of [B A] dz: NGV row sums over the columns + the constant rows held in grow
         if (k < N) {
@@ -746,18 +761,24 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
     // copies between them), and the loads are never predicated: a conditional load or a buffer copy would make
     // the compiler move the in-flight registers, which waits for the load. Lanes that do not sweep (idle slots,
     // converged teams) re-read one fixed record instead; past k1 the pointer stays on k1.
+    // P1's loads of one stage: its record fields and (DZ plane) the lane's DZ; dz points at the plane entry of
+    // the stage whose record p points at (p - tbase = k KS <=> dz - dzbase = 16 k)
+    auto p1_load = [&](const float* p, float (&v)[RS]) {
+        rec_load_range<R::P1L0, R::P1L1, RS, QM>(p, v);
+        if constexpr (kDzPlane) v[R::DZ] = dzbase[(p - tbase) / KS * 16];
+    };
     auto sweep = [&](int k0, int k1, int dir, bool ld, auto&& body) {  // 2 buffers (compute-heavy P1)
         const ptrdiff_t step = ld ? (ptrdiff_t)KS * dir : 0;
         const float* p = tbase + (size_t)k0 * KS;
         float ra[RS], rb[RS];
-        rec_load_range<R::P1L0, R::P1L1, RS, QM>(p, ra);
+        p1_load(p, ra);
         for (int k = k0;; k += 2 * dir) {
             const float* p1 = (k == k1) ? p : p + step;
-            rec_load_range<R::P1L0, R::P1L1, RS, QM>(p1, rb);
+            p1_load(p1, rb);
             body(k, ra);
             if (k == k1) break;
             const float* p2 = (k + dir == k1) ? p1 : p1 + step;
-            rec_load_range<R::P1L0, R::P1L1, RS, QM>(p2, ra);
+            p1_load(p2, ra);
             body(k + dir, rb);
             if (k + dir == k1) break;
             p = p2;
@@ -772,12 +793,17 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
         float buf[D][RS];
         const float* p = tbase + (size_t)k0 * KS;
         int kl = k0;
-        rec_load_range<F0, F, RS, QM>(p, buf[0]);
+        // P1 with P1_D > 2 buffers also takes DZ from the plane (the light sweeps read only the prefix)
+        auto load = [&](const float* pp, float (&v)[RS]) {
+            rec_load_range<F0, F, RS, QM>(pp, v);
+            if constexpr (kDzPlane && F == R::P1L1) v[R::DZ] = dzbase[(pp - tbase) / KS * 16];
+        };
+        load(p, buf[0]);
         sfor<1, D>([&](auto ic) {
             constexpr int i = decltype(ic)::value;
             p = (kl == k1) ? p : p + step;
             kl = (kl == k1) ? kl : kl + dir;
-            rec_load_range<F0, F, RS, QM>(p, buf[i]);
+            load(p, buf[i]);
         });
         for (int k = k0;; k += D * dir) {
             bool stop = false;
@@ -791,7 +817,7 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
                 }
                 p = (kl == k1) ? p : p + step;
                 kl = (kl == k1) ? kl : kl + dir;
-                rec_load_range<F0, F, RS, QM>(p, buf[i]);
+                load(p, buf[i]);
             });
             if (stop) break;
         }
@@ -1138,7 +1164,10 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
                         s2 += bnd ? d.dll * d.dtl + d.dlu * d.dtu : 0.0f;
                     }
                 }
-                if (ld && valid) tbase[(size_t)k * KS + (!corr ? rec_off<RS, QM>(R::DZA) : rec_off<RS, QM>(R::DZ))] = dz;
+                if (ld && valid) {
+                    if (corr && kDzPlane) dzbase[(size_t)k * 16] = dz;
+                    else tbase[(size_t)k * KS + (!corr ? rec_off<RS, QM>(R::DZA) : rec_off<RS, QM>(R::DZ))] = dz;
+                }
                 if (k < N) dxs = dyn(rc, valid ? dz : 0.0f);
             });
             };
@@ -1176,17 +1205,35 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
 
     // ---- full SQP step + outputs ----------------------------------------------------------------------
     if (status == 0) {
-        for (int k = 0; k <= N; k++) {
-            const float z = lv ? tbase[(size_t)k * KS + rec_off<RS, QM>(R::Z)] : 0.0f;
-            if (is_x) {
-                const float nv = (k == 0) ? x0_lane : XB(k, xi) + z;
-                XB(k, xi) = nv;
-                if (a.xtraj) a.xtraj[((size_t)k * NX + xi) * Bn + inst] = nv;
+        // one unconditional load of z and of the iterate entry, one store per lane and stage (lanes without an
+        // entry -- idle slots, u at stage N -- read and write the dummy record): under lane masks every wait in
+        // this loop was a vmcnt(0), one memory round trip per stage
+        // this lane's entry of stage k (clamped: stages past N repeat stage N's, read-only below)
+        auto entry = [&](int k) -> float* {
+            const int kk = k <= N ? k : N;
+            return is_x ? &XB(kk, xi) : ((is_u && kk < N) ? &UBAR(kk, r) : tdummy);
+        };
+        constexpr int EC = 8;  // stages per batch: EC loads of each kind in flight, then EC stores
+        for (int k0 = 0; k0 <= N; k0 += EC) {
+            float zs[EC], vs[EC];
+#pragma unroll
+            for (int j = 0; j < EC; j++) {
+                const int kk = (k0 + j) <= N ? k0 + j : N;
+                zs[j] = tbase[(size_t)kk * KS + rec_off<RS, QM>(R::Z)];
+                vs[j] = *entry(k0 + j);
             }
-            if (is_u && k < N) {
-                const float nv = UBAR(k, r) + z;
-                UBAR(k, r) = nv;
-                if (a.utraj) a.utraj[((size_t)k * NU + r) * Bn + inst] = nv;
+#pragma unroll
+            for (int j = 0; j < EC; j++) {
+                const int k = k0 + j;
+                const float nv = (is_x && k == 0) ? x0_lane : vs[j] + zs[j];
+                if (k <= N) *entry(k) = nv;
+            }
+        }
+        if (a.xtraj || a.utraj) {
+            __threadfence_block();
+            for (int k = 0; k <= N; k++) {
+                if (is_x && a.xtraj) a.xtraj[((size_t)k * NX + xi) * Bn + inst] = XB(k, xi);
+                if (is_u && k < N && a.utraj) a.utraj[((size_t)k * NU + r) * Bn + inst] = UBAR(k, r);
             }
         }
     }
