@@ -40,7 +40,8 @@ CONFIGS = {
     "omni4": dict(idx=2, models=[("omni4", 4096)], N=40, desc="omni4amr (11x4) N=40 batch=4096"),
     "tric": dict(idx=3, models=[("tric", 8192)], N=60, groups=2, desc="tric3amr N=60 batch=8192, alpha bounds active"),
     # whole fleet: 65536 robots over 8 GPUs -> 8192 per GPU, a third of each model; the three models' streams run
-    # decoupled at N=1 (2.94 -> 3.71 M it/s against a fleet-wide tick boundary) and joined under --gather
+    # decoupled (2.94 -> 3.71 M it/s against a fleet-wide tick boundary), also under the per-tick gather (staged
+    # per stream, FleetNode)
     "mixed": dict(idx=4, models=[("diff", 2731), ("omni4", 2731), ("tric", 2730)], N=40,
                   desc="mixed fleet diff+omni4+tric, 8192 per GPU (65536 on 8 GPUs)"),
 }

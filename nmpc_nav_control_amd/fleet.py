@@ -111,23 +111,29 @@ class FleetNode:
     Launches on several streams (several models, or groups > 1) run concurrently. ``decoupled`` picks how the
     streams advance:
       * joined (False): every tick starts after the previous tick of every stream ended (one fleet-wide tick
-        boundary per step; required by the per-tick command all-gather);
-      * decoupled (True): each stream runs its own closed loop (solve -> plant/reference step -> statistics)
-        with no cross-stream wait; the step boundary is only a count. A solve launch ends with its slowest
-        wave (its hardest robot: up to 19 IPM iterations against a mean of 7), and while it drains, the SIMDs
-        its finished waves freed run the next launches of the other streams.
-    With one stream (a single model, groups = 1) both are the same sequential loop."""
+        boundary per step);
+      * decoupled (True, the default with several streams): each stream runs its own closed loop (solve ->
+        plant/reference step -> statistics) with no cross-stream wait; the step boundary is only a count. A
+        solve launch ends with its slowest wave (its hardest robot), and while it drains, the SIMDs its finished
+        waves freed run the next launches of the other streams.
+    With one stream (a single model, groups = 1) both are the same sequential loop.
+
+    gather: the per-tick all-gather of [u0; status] of every robot to every rank (RCCL over xGMI). Joined ticks
+    gather at the tick boundary; decoupled streams stage their commands into a double-buffered slot when their
+    own tick is done, and a gather stream all-gathers the slot once every fleet's part of that tick has arrived
+    (a fleet waits only before overwriting a slot whose gather, two ticks back, has not finished). On the CPU
+    (gloo tests) the same code runs without streams."""
 
     def __init__(self, models, N, seed, dev, rank=0, world=1, gather=False, solver_factory=None, groups=1,
                  decoupled=None, schedule=None, renew=True):
         self.dev = torch.device(dev)
         self.rank, self.world = rank, world
         cuda = self.dev.type == "cuda"
+        self.cuda = cuda
         self.groups = max(1, int(groups))
         self.multi = (len(models) > 1 or self.groups > 1) and cuda
-        self.decoupled = (self.multi and not gather) if decoupled is None else (bool(decoupled) and self.multi)
-        if self.decoupled and gather:
-            raise ValueError("the per-tick command gather needs joined ticks")
+        # CPU: decoupled=True runs the decoupled code path (staged gather) sequentially, for the gloo tests
+        self.decoupled = self.multi if decoupled is None else (bool(decoupled) and (self.multi or not cuda))
         self.fleets = []
         for j, (m, B) in enumerate(models):
             lo, hi = shard_range(B * world, rank, world)
@@ -144,6 +150,11 @@ class FleetNode:
         self.offs = [int(v) for v in np.cumsum([0] + [f.B for f in self.fleets])]
         self.gather = CommandGather(5, [self.B] * world, self.dev) if gather else None
         self.gathered = None
+        self.tick_no = 0
+        if gather and self.decoupled and cuda:
+            self.gstream = torch.cuda.Stream(self.dev)
+            self.ev_staged = [[torch.cuda.Event() for _ in range(self.gather.slots)] for _ in self.fleets]
+            self.ev_gdone = [torch.cuda.Event() for _ in range(self.gather.slots)]
         # executed IPM iterations and failures, accumulated on the device
         self.iters_sum = torch.zeros(self.B, dtype=torch.int64, device=self.dev)
         self.iters_max = torch.zeros(self.B, dtype=torch.int32, device=self.dev)
@@ -191,12 +202,12 @@ class FleetNode:
                 self.cold_iters[sl] += cold * f.qp_iter
 
     def join(self):
-        """Make the current stream wait for every fleet stream (end of a decoupled run)."""
+        """Make the current stream wait for every fleet stream and the gather stream (end of a decoupled run)."""
         if self.multi:
             main = torch.cuda.current_stream(self.dev)
-            for f in self.fleets:
+            for st in [f.stream for f in self.fleets] + ([self.gstream] if hasattr(self, "gstream") else []):
                 done = torch.cuda.Event()
-                done.record(f.stream)
+                done.record(st)
                 main.wait_event(done)
 
     def reset_stats(self):
@@ -218,6 +229,31 @@ class FleetNode:
                 "max": int(np.nonzero(h)[0].max()), "robot_ticks": int(n), "renewals": cold,
                 "cold_mean": (float(self.cold_iters.sum().item()) / cold) if cold else None}
 
+    def _stage(self, j, f, slot):
+        """Fleet j's [u0 (rows nu..3 stay 0); status] of this tick into staging slot `slot`, on its stream, after
+        the gather that last read the slot (two ticks back) has finished."""
+        ctx = torch.cuda.stream(f.stream) if (self.cuda and f.stream is not None) else _nullctx()
+        with ctx:
+            if self.cuda and self.tick_no >= self.gather.slots:
+                torch.cuda.current_stream(self.dev).wait_event(self.ev_gdone[slot])
+            sb = self.gather.stage_bufs[slot]
+            lo, hi = self.offs[j], self.offs[j + 1]
+            sb[:f.u0.shape[0], lo:hi].copy_(f.u0)
+            sb[4, lo:hi].copy_(f.status)
+            if self.cuda:
+                self.ev_staged[j][slot].record(torch.cuda.current_stream(self.dev))
+
+    def _collect(self, slot):
+        """All-gather staging slot `slot` on the gather stream once every fleet's part has been staged."""
+        ctx = torch.cuda.stream(self.gstream) if self.cuda else _nullctx()
+        with ctx:
+            if self.cuda:
+                for evs in self.ev_staged:
+                    self.gstream.wait_event(evs[slot])
+            self.gathered = self.gather.collect(slot)
+            if self.cuda:
+                self.ev_gdone[slot].record(self.gstream)
+
     def gather_commands(self):
         """All-gather [u0 (padded to 4 rows); status] of every robot to every rank: [5][B * world]."""
         if self.gather is not None:
@@ -234,6 +270,7 @@ class FleetNode:
         launch on the stream it runs on (bench.py records HIP events there). Joined streams start every fleet
         from one point of the current stream, so ``start`` is called once, with j = -1."""
         if self.decoupled:
+            slot = self.tick_no % 2
             for j, f in enumerate(self.fleets):
                 if timer is not None:
                     timer.start(j, f.stream)
@@ -241,7 +278,12 @@ class FleetNode:
                 if timer is not None:
                     timer.end(j, f.stream)
                 self.accumulate_one(j)
+                if self.gather is not None:
+                    self._stage(j, f, slot)
                 f.advance()
+            if self.gather is not None:
+                self._collect(slot)
+            self.tick_no += 1
             return
         cuda = self.dev.type == "cuda"
         main = torch.cuda.current_stream(self.dev) if cuda else None

@@ -69,23 +69,43 @@ class TimedRegion:
 
 class CommandGather:
     """All-gather of per-robot commands [rows][B_rank] to every rank (rank 0 keeps the fleet view).
-    Ranks may hold different robot counts: buffers are padded to the largest shard."""
+    Ranks may hold different robot counts: buffers are padded to the largest shard.
 
-    def __init__(self, rows, counts, device):
+    Two uses:
+      * joined ticks: ``gather(parts)`` (or calling the object) copies the parts into the staging buffer and
+        all-gathers it at once;
+      * decoupled streams (FleetNode): each fleet copies its part into staging slot ``slot`` on its own stream
+        when its tick is done (``stage``), and ``collect(slot)`` all-gathers that slot on the gather stream once
+        every part has arrived. ``slots`` staging buffers rotate so that a fleet can run its next ticks while
+        the gather of an earlier one is in flight."""
+
+    def __init__(self, rows, counts, device, slots=2):
         self.rows, self.counts = rows, list(counts)
         self.pad = max(self.counts)
-        self.src = torch.zeros(rows, self.pad, device=device)
-        self.bufs = [torch.zeros_like(self.src) for _ in self.counts]
+        self.slots = slots
+        self.stage_bufs = [torch.zeros(rows, self.pad, device=device) for _ in range(slots)]
+        self.recv = [[torch.zeros(rows, self.pad, device=device) for _ in self.counts] for _ in range(slots)]
+        self.src = self.stage_bufs[0]
+        self.bufs = self.recv[0]
+
+    def stage(self, slot, off, part):
+        """Copy one fleet's [r][b] part into staging slot `slot` at robot offset `off` (caller's stream)."""
+        self.stage_bufs[slot][:part.shape[0], off:off + part.shape[1]].copy_(part)
+
+    def collect(self, slot):
+        """All-gather staging slot `slot` (on the current stream) -> [rows][total]."""
+        src, bufs = self.stage_bufs[slot], self.recv[slot]
+        if dist.is_initialized() and dist.get_world_size() > 1:
+            dist.all_gather(bufs, src)
+        else:
+            bufs[0].copy_(src)
+        return torch.cat([b[:, :c] for b, c in zip(bufs, self.counts)], dim=1)
 
     def __call__(self, parts):
         """parts: list of [r_i][b_i] tensors (per model) concatenated along robots; returns [rows][total]."""
         off = 0
         self.src.zero_()
         for p in parts:
-            self.src[:p.shape[0], off:off + p.shape[1]] = p
+            self.stage(0, off, p)
             off += p.shape[1]
-        if dist.is_initialized() and dist.get_world_size() > 1:
-            dist.all_gather(self.bufs, self.src)
-        else:
-            self.bufs[0].copy_(self.src)
-        return torch.cat([b[:, :c] for b, c in zip(self.bufs, self.counts)], dim=1)
+        return self.collect(0)

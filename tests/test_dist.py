@@ -74,18 +74,19 @@ MIXED = [("diff", 3), ("omni4", 2), ("tric", 3)]  # robots per rank and model (w
 MIX_N, MIX_TICKS, MIX_SEED = 8, 3, 20250824 + 4
 
 
-def _node(world, rank, models):
+def _node(world, rank, models, decoupled=False):
     from cpu_fleet_solver import OracleFleetSolver
     from nmpc_nav_control_amd.fleet import FleetNode
     return FleetNode(models, MIX_N, MIX_SEED, torch.device("cpu"), rank=rank, world=world, gather=True,
-                     solver_factory=OracleFleetSolver)
+                     solver_factory=OracleFleetSolver, decoupled=decoupled)
 
 
-def _fleet_worker(rank, world, port, out):
+def _fleet_worker(rank, world, port, out, decoupled=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        node = _node(world, rank, MIXED)
+        node = _node(world, rank, MIXED, decoupled)
+        assert node.decoupled == decoupled
         logs = []
         with TimedRegion() as tr:
             for _ in range(MIX_TICKS):
@@ -98,12 +99,16 @@ def _fleet_worker(rank, world, port, out):
         dist.destroy_process_group()
 
 
-def test_gloo_world2_fleet_node_equals_single(tmp_path):
+@pytest.mark.parametrize("decoupled", [False, True])
+def test_gloo_world2_fleet_node_equals_single(tmp_path, decoupled):
     """World 2 over gloo runs bench.py's FleetNode (mixed diff+omni4+tric fleet, per-rank instance shards,
     per-tick all-gather of u0 + status through sharding.CommandGather) with the oracle behind the solver
-    interface; the gathered fleet commands equal a single-process node holding the whole fleet, bit for bit."""
+    interface; the gathered fleet commands equal a single-process joined node holding the whole fleet, bit for
+    bit. decoupled=True runs the decoupled-stream code path (each fleet stages its commands into a double-buffered
+    slot after its own tick, the gather collects the slot), which on the GPU keeps the streams' closed loops
+    independent while gathering every tick (bench.py's mixed config at world > 1)."""
     out = str(tmp_path / "fleet.npz")
-    mp.spawn(_fleet_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    mp.spawn(_fleet_worker, args=(2, _free_port(), out, decoupled), nprocs=2, join=True)
     got = np.load(out)
     single = _node(1, 0, [(m, 2 * b) for m, b in MIXED])
     ref = []

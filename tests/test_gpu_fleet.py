@@ -287,3 +287,18 @@ def test_renewal_on_device(built):
     assert (st == 0).all() and (st_o == 0).all()
     print(f"\nrenewals {total} over 12 ticks; reset-tick replay: u0 err {eu:.2e}, x err {ex:.2e}")
     assert eu <= TOL_U and ex <= TOL_X and ec <= TOL_U
+
+
+def test_decoupled_gather_on_device(built):
+    """The whole-fleet command gather with decoupled streams (bench.py's mixed config at world > 1; here world 1,
+    the same stream and event code): every tick's gathered [u0; status] equals the fleets' own outputs of that
+    tick, while the three models' closed loops run on their own streams without a tick boundary."""
+    node = FleetNode([("diff", 512), ("omni4", 256), ("tric", 300)], 40, SEED + 4, DEV, gather=True)
+    assert node.decoupled and node.multi and node.gather is not None
+    for _ in range(6):
+        node.step()
+        torch.cuda.synchronize()
+        exp = torch.cat([torch.cat([f.u0, torch.zeros(4 - f.u0.shape[0], f.B, device=DEV), f.status.float()[None]])
+                         for f in node.fleets], dim=1)
+        assert torch.equal(node.gathered, exp)
+    assert int(node.fail_cnt.sum()) == 0
