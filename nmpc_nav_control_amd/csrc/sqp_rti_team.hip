@@ -679,16 +679,30 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
         // per stage). Nothing is in flight past this point but the loop's own stores: the waits the compiler
         // would otherwise place inside the loop for the loads above (len, x0) wait on those stores too.
         __builtin_amdgcn_s_waitcnt(0);
+        // the stage inputs are read from LDS one stage ahead (each dependent LDS read costs a round trip of the
+        // one wave that runs this pass)
+        struct Stg {
+            float v[5], g[NGV], t[3];
+        };
+        auto lds_ld = [&](int k, Stg& o) {
+            const int kk = k <= N ? k : N;
+            const float* const st = s_stg + (size_t)kk * SF * 16 + r;
+#pragma unroll
+            for (int f = 0; f < 5; f++) o.v[f] = st[f * 16];
+#pragma unroll
+            for (int i = 0; i < NGV; i++) o.g[i] = st[(5 + i) * 16];
+#pragma unroll
+            for (int j = 0; j < 3; j++) o.t[j] = (mode == kModeRun) ? my_traj[kk * 3 + j] : 0.0f;
+        };
+        Stg cur, nxt;
+        lds_ld(0, cur);
         for (int k = 0; k <= N; k++) {
-            const float* const st = s_stg + (size_t)k * SF * 16 + r;
-            float trk[3] = {0.0f, 0.0f, 0.0f}, g[NX];
-            if (mode == kModeRun) {
+            lds_ld(k + 1, nxt);
+            float g[NX];
 #pragma unroll
-                for (int j = 0; j < 3; j++) trk[j] = my_traj[k * 3 + j];
-            }
-#pragma unroll
-            for (int i = 0; i < NX; i++) g[i] = (i < NGV && k < N) ? st[(5 + (i < NGV ? i : 0)) * 16] : 0.0f;
-            p0_body(k, st[0], st[16], trk, make_float2(st[32], st[48]), g, st[64]);
+            for (int i = 0; i < NX; i++) g[i] = (i < NGV && k < N) ? cur.g[i < NGV ? i : 0] : 0.0f;
+            p0_body(k, cur.v[0], cur.v[1], cur.t, make_float2(cur.v[2], cur.v[3]), g, cur.v[4]);
+            cur = nxt;
         }
     } else {
         float2 lprev = load_l(0);
