@@ -1,0 +1,214 @@
+// team_common.hpp -- device helpers shared by the solve kernels (sqp_rti_team.hip: one 16-lane team per robot;
+// sqp_rti_rowpar.hip: one wave per robot with stage-parallel phases): IPM constants, the fused fp64 DPP blocks of
+// the Riccati step, the RK4 sensitivity column, lane-record access, bound directions and the step bound.
+#pragma once
+
+#include "nmpc_kernels.hpp"
+#include "team_asm_gen.hpp"
+#include "team_dpp.hpp"
+
+namespace nmpc {
+namespace {
+
+constexpr float kBreakdownMuT = 1e-6f;
+constexpr float kStatRelT = 1e-5f;
+// largest single complementarity product at exit, relative to tol_comp: the mean (mu) alone lets one pair keep
+// m * mu, which leaves a nearly active bound's multiplier at ~1e-5 and moves u0 by ~1e-3 through the weak input
+// curvature R dt (DESIGN.md "Stopping rule")
+constexpr float kCompMaxRatio = 30.0f;
+// primal infeasibility (status 4, the wrapper's exception path, NMPCNavControl.cpp:14-23): the bound multipliers
+// diverge while the bound residual cannot close. A feasible QP of this OCP keeps them at the size of its cost
+// weights (max 88 over 768 bench-loop QPs with renewals, against > 1e5 by IPM iteration 13-20 for QPs made
+// infeasible as the failure test does; tools/infeas_study.py); the oracle uses the same two constants
+constexpr float kInfeasLambda = 1e5f;
+constexpr float kInfeasRes = 1e-3f;
+constexpr float kFar = 1e30f;  // sentinel bound / slack of unbounded slots (z + kFar - kFar == 0 in fp32)
+
+// generated whole-block fused-DPP kernels (team_asm_gen.hpp), dispatched on the model shape
+template <int NX, int NU>
+__device__ __forceinline__ void pg_block(double (&acc)[NX], const double (&prow)[NX + NU], const double (&gd)[NX])
+{
+    if constexpr (NX == 7 && NU == 2) pg_block_7_2(acc, prow, gd);
+    else pg_block_11_4(acc, prow, gd);
+}
+template <int NX, int NU>
+__device__ __forceinline__ void mrow_pg_block(double (&acc)[NX + NU], double& md0, const double (&pg)[NX],
+                                              const double (&gd)[NX])
+{
+    if constexpr (NX == 7 && NU == 2) mrow_pg_block_7_2(acc, md0, pg, gd);
+    else mrow_pg_block_11_4(acc, md0, pg, gd);
+}
+template <int NX, int NU, int J>
+__device__ __forceinline__ void chol_update(double (&lr)[NX + NU], double lj, double& piv)
+{
+    if constexpr (NX == 7 && NU == 2) chol_update_7_2<J>(lr, lj, piv);
+    else chol_update_11_4<J>(lr, lj, piv);
+}
+template <int NX, int NU>
+__device__ __forceinline__ float dot_x(float acc, float a, const float (&b)[NX])  // acc + sum_l bc_{NU+l}(a) b[l]
+{
+    if constexpr (NX == 7 && NU == 2) return dot_x_7_2(acc, a, b);
+    else return dot_x_11_4(acc, a, b);
+}
+template <int NX, int NU>
+__device__ __forceinline__ float dot_v(float acc, float a, const float (&b)[NX + NU])  // acc + sum_v bc_v(a) b[v]
+{
+    if constexpr (NX == 7 && NU == 2) return dot_v_7_2(acc, a, b);
+    else return dot_v_11_4(acc, a, b);
+}
+
+template <class M>
+__device__ __forceinline__ int xcomp(int xi)
+{
+#pragma unroll
+    for (int c = 0; c < M::NBX; c++)
+        if (M::idxbx(c) == xi) return c;
+    return -1;
+}
+
+// Column `col` (slot convention: col < NU input col, else state col - NU) of the RK4 map's sensitivity at
+// (x, u), propagated by one lane through the four stages, together with the nominal step xn.
+template <class M>
+__device__ __forceinline__ void rk4_column(const float* x, const float* u, const KParams& P, int col, float* xn,
+                                           float* g)
+{
+    constexpr int NX = M::NX, NU = M::NU;
+    const float h = P.dt;
+    float xs[NX], k[NX], acc[NX], s0[NX], s[NX], dacc[NX];
+#pragma unroll
+    for (int i = 0; i < NX; i++) {
+        xs[i] = x[i];
+        s0[i] = (col == NU + i) ? 1.0f : 0.0f;
+        s[i] = s0[i];
+    }
+    const float cst[3] = {0.5f, 0.5f, 1.0f};
+    const float wgt[4] = {1.0f, 2.0f, 2.0f, 1.0f};
+#pragma unroll
+    for (int st = 0; st < 4; st++) {
+        M::f(xs, u, P, k);
+        float S1[NX][1], D1[NX][1];
+#pragma unroll
+        for (int i = 0; i < NX; i++) S1[i][0] = s[i];
+        M::template jvp<1>(xs, S1, P, D1);  // Jx s (the input block of the models is [0; I] on the last NU rows)
+        float dk[NX];
+#pragma unroll
+        for (int i = 0; i < NX; i++) dk[i] = D1[i][0];
+#pragma unroll
+        for (int q = 0; q < NU; q++) dk[NX - NU + q] += (col == q) ? 1.0f : 0.0f;
+#pragma unroll
+        for (int i = 0; i < NX; i++) {
+            acc[i] = (st == 0) ? k[i] : acc[i] + wgt[st] * k[i];
+            dacc[i] = (st == 0) ? dk[i] : dacc[i] + wgt[st] * dk[i];
+        }
+        if (st < 3) {
+            const float ch = cst[st] * h;
+#pragma unroll
+            for (int i = 0; i < NX; i++) {
+                xs[i] = x[i] + ch * k[i];
+                s[i] = s0[i] + ch * dk[i];
+            }
+        }
+    }
+    const float h6 = h * (1.0f / 6.0f);
+#pragma unroll
+    for (int i = 0; i < NX; i++) {
+        xn[i] = x[i] + h6 * acc[i];
+        g[i] = s0[i] + h6 * dacc[i];
+    }
+}
+
+// Record access. A lane's record is NQ quads of 4 floats, QS floats apart, in one of two stage-block layouts:
+//   slot-major [slot][RS] (QS = 4): a lane's record is contiguous;
+//   quad-major [quad][slot 0..15][4] (QS = 64): quad i of a team's 16 slots is 256 contiguous bytes, so a
+//     dwordx4 access of a team touches 2 cache lines instead of one per two slots.
+// Measured per model in same-box A/B runs (ms per tick): omni4 (15 slots, 80-B records) 2.17 slot-major ->
+// 1.74 quad-major; diff 1.55 -> 1.57 and tric 4.48 -> 4.62 (9 slots) favour slot-major. RQM picks quad-major for
+// teams of more than 12 slots.
+template <int NV>
+constexpr bool rec_quad_major()
+{
+    return NV > 12;
+}
+template <int RS, bool QM>
+constexpr int rec_qs() { return QM ? 64 : 4; }  // floats between a lane's consecutive quads
+template <int RS, bool QM>
+constexpr int rec_lane() { return QM ? 4 : RS; }  // floats between the records of consecutive slots
+template <int RS, bool QM>
+constexpr int rec_off(int f) { return (f / 4) * rec_qs<RS, QM>() + f % 4; }  // offset of field f in a lane's record
+
+
+// floats [F0, F1) of a record, one access per quad piece (a piece never crosses a quad)
+template <int F0, int F1, int RS, bool QM>
+__device__ __forceinline__ void rec_load_range(const float* p, float (&v)[RS])
+{
+    constexpr int QS = rec_qs<RS, QM>();
+    sfor<F0 / 4, (F1 + 3) / 4>([&](auto qc) {
+        constexpr int q = decltype(qc)::value;
+        constexpr int a = (F0 > 4 * q) ? F0 : 4 * q, b = (F1 < 4 * q + 4) ? F1 : 4 * q + 4, L = b - a;
+        static_assert(L != 2 || a % 2 == 0, "dwordx2 piece 8-byte aligned");
+        const float* pq = p + q * QS + (a - 4 * q);
+        if constexpr (L == 4) {
+            const float4 t = *reinterpret_cast<const float4*>(pq);
+            v[a] = t.x; v[a + 1] = t.y; v[a + 2] = t.z; v[a + 3] = t.w;
+        } else if constexpr (L == 3) {
+            const float3 t = *reinterpret_cast<const float3*>(pq);
+            v[a] = t.x; v[a + 1] = t.y; v[a + 2] = t.z;
+        } else if constexpr (L == 2) {
+            const float2 t = *reinterpret_cast<const float2*>(pq);
+            v[a] = t.x; v[a + 1] = t.y;
+        } else {
+            v[a] = pq[0];
+        }
+    });
+}
+
+template <int F0, int F1, int RS, bool QM>
+__device__ __forceinline__ void rec_store_range(float* p, const float (&v)[RS])
+{
+    constexpr int QS = rec_qs<RS, QM>();
+    sfor<F0 / 4, (F1 + 3) / 4>([&](auto qc) {
+        constexpr int q = decltype(qc)::value;
+        constexpr int a = (F0 > 4 * q) ? F0 : 4 * q, b = (F1 < 4 * q + 4) ? F1 : 4 * q + 4, L = b - a;
+        static_assert(L != 2 || a % 2 == 0, "dwordx2 piece 8-byte aligned");
+        float* pq = p + q * QS + (a - 4 * q);
+        if constexpr (L == 4) *reinterpret_cast<float4*>(pq) = make_float4(v[a], v[a + 1], v[a + 2], v[a + 3]);
+        else if constexpr (L == 3) *reinterpret_cast<float3*>(pq) = make_float3(v[a], v[a + 1], v[a + 2]);
+        else if constexpr (L == 2) *reinterpret_cast<float2*>(pq) = make_float2(v[a], v[a + 1]);
+        else pq[0] = v[a];
+    });
+}
+
+template <int RS, bool QM>
+__device__ __forceinline__ void rec_store(float* p, const float (&v)[RS])
+{
+    rec_store_range<0, RS, RS, QM>(p, v);
+}
+
+// Newton directions of one bounded variable (lower slack tl / multiplier ll, upper tu / lu) for a step dz with
+// complementarity targets tgl, tgu:  dt = dz + r (primal),  l*dt + t*dl = tg - l*t  (linearised complementarity).
+struct BoundDir {
+    float dtl, dtu, dll, dlu;
+};
+__device__ __forceinline__ BoundDir bound_dir(float dz, float rl, float rr, float tl, float tu, float ll, float lu,
+                                              float itl, float itu, float tgl, float tgu)
+{
+    BoundDir d;
+    d.dtl = dz + rl;
+    d.dtu = -dz + rr;
+    d.dll = (tgl - ll * (tl + rl) - ll * dz) * itl;
+    d.dlu = (tgu - lu * (tu + rr) + lu * dz) * itu;
+    return d;
+}
+
+// Largest step keeping v + a dv >= 0, folded into amax. t = -v / dv is a bound only for dv < 0 (v >= 0): then
+// t >= +0; for dv >= 0 it is <= -0, -inf or a NaN. As unsigned integers non-negative floats keep their order and
+// every negative float (and -0) is larger than +inf, so one unsigned min drops the non-bounds without a compare /
+// select (same-box A/B against the branch form: diff 1.403 -> 1.398 ms, tric 4.386 -> 4.358 ms)
+__device__ __forceinline__ float step_bound_r(float amax, float v, float dv)
+{
+    const float t = -v * frcp(dv);
+    return __uint_as_float(min(__float_as_uint(amax), __float_as_uint(t)));
+}
+
+}  // namespace
+}  // namespace nmpc
