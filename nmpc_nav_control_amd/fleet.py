@@ -162,6 +162,7 @@ class FleetNode:
         # per-fleet histograms of the executed IPM iterations (robot-ticks; the tail of the window) and the
         # count / iterations of the solves that followed a renewal (cold: reset iterate, cold IPM)
         self.iter_hist = [torch.zeros(64, dtype=torch.int64, device=self.dev) for _ in self.fleets]
+        self._ones = torch.ones(max([f.B for f in self.fleets] + [1]), dtype=torch.int64, device=self.dev)
         self.cold_cnt = torch.zeros(self.B, dtype=torch.int64, device=self.dev)
         self.cold_iters = torch.zeros(self.B, dtype=torch.int64, device=self.dev)
 
@@ -195,7 +196,8 @@ class FleetNode:
             self.iters_sum[sl] += f.qp_iter
             torch.maximum(self.iters_max[sl], f.qp_iter, out=self.iters_max[sl])
             self.fail_cnt[sl] += f.status != 0
-            self.iter_hist[j] += torch.bincount(f.qp_iter.clamp(0, 63).long(), minlength=64)
+            # scatter_add, not bincount: torch.bincount sizes its output from the data (a device -> host sync)
+            self.iter_hist[j].scatter_add_(0, f.qp_iter.clamp(0, 63).long(), self._ones[:f.B])
             if f.renew:
                 cold = f.reset.to(torch.int64)  # the flags this solve ran with (advance() rewrites them)
                 self.cold_cnt[sl] += cold
