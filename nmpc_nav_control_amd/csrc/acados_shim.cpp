@@ -455,9 +455,11 @@ void solve_group(std::vector<nmpc_capsule_impl*>& cs, std::vector<Packed>& ps, c
         c->time_tot = tt;
         c->time_qp = tq;
         c->time_lin = 0.0;
-        c->warm_ok = hst[q] == 0;
+        // the kernel's epilogue rule: warm = qp_warm_start && status == 0 && the IPM converged before its cap
+        const bool conv = hst[q] == 0 && hit[q] < ps[idx[0]].prm.qp_iter_max;
+        c->warm_ok = conv;
         e.owner[q] = c->uid;
-        e.dev_warm[q] = hst[q] == 0 ? 1 : 0;  // the kernel's epilogue: warm = qp_warm_start && status == 0
+        e.dev_warm[q] = conv ? 1 : 0;
         xbs[q] = hst[q] == 0 ? c->xbar.data() : nullptr;
         ubs[q] = hst[q] == 0 ? c->ubar.data() : nullptr;
     }

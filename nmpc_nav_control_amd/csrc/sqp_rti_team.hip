@@ -443,8 +443,11 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
             rec[R::TL] = tl;
             rec[R::TU] = tu;
             // cold: t lambda = mu0; warm: the previous multipliers, floored at kappa / t
-            const float ll0 = warm ? fmaxf(lp.x, P.warm_kappa / tl) : P.mu0 / tl;
-            const float lu0 = warm ? fmaxf(lp.y, P.warm_kappa / tu) : P.mu0 / tu;
+            // (previous multipliers capped at kWarmLambdaCap: a feasible QP of this OCP ends with multipliers of
+            // the size of its weights, < 1e2; a runaway value from a struggling solve would start the IPM at a huge
+            // complementarity)
+            const float ll0 = warm ? fmaxf(fminf(lp.x, kWarmLambdaCap), P.warm_kappa / tl) : P.mu0 / tl;
+            const float lu0 = warm ? fmaxf(fminf(lp.y, kWarmLambdaCap), P.warm_kappa / tu) : P.mu0 / tu;
             rec[R::LL] = ll0;
             rec[R::LU] = lu0;
             sum_c0 += ll0 * tl + lu0 * tu;
@@ -1065,7 +1068,8 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
         if (a.status) a.status[inst] = status;
         if (a.qp_iter) a.qp_iter[inst] = it_done;
         if (a.iter_key) a.iter_key[inst] = it_done;
-        if (a.warm) a.warm[inst] = (P.warm && status == 0) ? 1 : 0;
+        // warm-start the next solve only from a solve that converged (not from one that ran to qp_iter_max)
+        if (a.warm) a.warm[inst] = (P.warm && status == 0 && it_done < P.iter_max) ? 1 : 0;
         if (a.qp_res) {
 #pragma unroll
             for (int j = 0; j < 3; j++) a.qp_res[(size_t)j * Bn + inst] = exit_res[j];

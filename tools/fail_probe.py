@@ -22,9 +22,14 @@ def main():
     f = Fleet(m, B, cfg["N"], DEFAULT_SEED + cfg["idx"], torch.device("cuda", 0))
     res = torch.zeros(3, B, device="cuda")
     keep = {}
+    wv, sv = f.solver.warm_state()
+    nx, nu = f.solver.nx, f.solver.nu
+    RS = 16 if (m != "tric" and nu == 2) else 20  # TeamRec<M, SD>::RS of the product layout
     for t in range(ticks):
         torch.cuda.synchronize()
         sn = f.snapshot()
+        scratch = sv.to_tensor()  # the records before this solve (warm multipliers)
+        warm = wv.to_tensor()
         f.solver.run(f.pose, f.vel, f.traj, steer=f.steer, traj_len=f.tlen, reset=f.reset, cmd=f.cmd, u0=f.u0,
                      status=f.status, qp_iter=f.qp_iter, qp_res=res, stream=f.stream)
         torch.cuda.synchronize()
@@ -37,6 +42,9 @@ def main():
             for k, v in sn.items():
                 if v is not None:
                     keep[key + "_" + k] = np.asarray(v[i])
+            blk = (cfg["N"] + 1) * 16 * RS
+            keep[key + "_records"] = scratch[0, i * blk:(i + 1) * blk].cpu().numpy().reshape(cfg["N"] + 1, 16, RS)
+            keep[key + "_warm"] = np.array([int(warm[0, i])])
             print(f"tick {t} robot {i}: status {st[i]} qp_iter {it[i]} res {res[:, i].cpu().numpy()} "
                   f"reset {sn['reset'][i] if sn['reset'] is not None else None}", flush=True)
         f.advance()
