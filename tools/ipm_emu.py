@@ -81,7 +81,9 @@ class Emu:
                 np.einsum("bij,bj->bi", Q["B"][:, k], dz[:, k, :nu])
         return dz
 
-    def init(self, start=None):
+    def init(self, start=None, warm=None):
+        """warm: (ll_prev, lu_prev, kappa, cap) [B][N+1][nv] previous multipliers -> the device's warm start
+        max(min(lambda_prev, cap), kappa / t); the first centring target then uses the measured mu."""
         B, N, nv, nu = self.B, self.N, self.nv, self.nu
         z = np.zeros((B, N + 1, nv))
         z[:, 0, nu:] = self.Q["dx0"]
@@ -95,6 +97,10 @@ class Emu:
         tu = np.where(bnd, np.maximum(self.ub - z, self.thr0), 1e30)
         ll = np.where(bnd, self.mu0 / tl, 0.0)
         lu = np.where(bnd, self.mu0 / tu, 0.0)
+        if warm is not None:
+            lp, up, kap, cap = warm
+            ll = np.where(bnd, np.maximum(np.minimum(lp, cap), kap / tl), 0.0)
+            lu = np.where(bnd, np.maximum(np.minimum(up, cap), kap / tu), 0.0)
         return z, tl, tu, ll, lu
 
     def adjoint(self, z, lam):
@@ -151,12 +157,13 @@ class Emu:
                 np.einsum("bij,bj->bi", Q["B"][:, k], dz[:, k, :nu])
         return dz, ok
 
-    def solve(self, polish=None, verbose=False, single=None, start=None, eta_scale=1.0, lag2=None, trace=None):
+    def solve(self, polish=None, verbose=False, single=None, start=None, eta_scale=1.0, lag2=None, trace=None,
+              warm=None, sd_hi=0.5):
         """Run the IPM on every robot. polish: None or dict(mu=threshold, rho=..., tol=...) -- after the
         residual test of an iteration whose mu is below the threshold, try the active-set polish; a robot whose
         polish passes its KKT test stops there. Returns per-robot iterations, polish attempts, solutions."""
         B, bnd = self.B, self.bnd
-        z, tl, tu, ll, lu = self.init(start)
+        z, tl, tu, ll, lu = self.init(start, warm)
         done = np.zeros(B, bool)
         iters = np.zeros(B, int)
         attempts = np.zeros(B, int)
