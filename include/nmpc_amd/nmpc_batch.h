@@ -65,6 +65,10 @@ typedef struct nmpc_model_params {
      * (its last solve there succeeded and no reset / create came in between), with kappa 0.01. */
     int qp_warm_start;
     double qp_warm_kappa; /* diff 0.2, omni4 / tric 0.01 */
+    /* Warm-start only after a solve that converged within this many IPM iterations (default 12; 0 = qp_iter_max).
+     * A robot whose QP was hard last tick starts its next IPM cold: warm-started multipliers speed up the easy
+     * majority but lengthen exactly the hard QPs that set the launch time (DESIGN.md "Algorithm and precision"). */
+    int qp_warm_iter_max;
 } nmpc_model_params;
 
 enum { NMPC_IPM_MEHROTRA = 0, NMPC_IPM_SINGLE = 1 };

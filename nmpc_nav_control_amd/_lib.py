@@ -29,7 +29,7 @@ class ModelParams(ctypes.Structure):
         ("qp_tol_stat", ctypes.c_double), ("qp_tol_ineq", ctypes.c_double), ("qp_tol_comp", ctypes.c_double),
         ("qp_mu0", ctypes.c_double), ("qp_thr0", ctypes.c_double), ("qp_tau", ctypes.c_double),
         ("qp_ipm", ctypes.c_int), ("qp_sigma_lo", ctypes.c_double), ("qp_sigma_hi", ctypes.c_double),
-        ("qp_warm_start", ctypes.c_int), ("qp_warm_kappa", ctypes.c_double),
+        ("qp_warm_start", ctypes.c_int), ("qp_warm_kappa", ctypes.c_double), ("qp_warm_iter_max", ctypes.c_int),
     ]
 
 

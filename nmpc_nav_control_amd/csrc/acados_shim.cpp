@@ -456,7 +456,9 @@ void solve_group(std::vector<nmpc_capsule_impl*>& cs, std::vector<Packed>& ps, c
         c->time_qp = tq;
         c->time_lin = 0.0;
         // the kernel's epilogue rule: warm = qp_warm_start && status == 0 && the IPM converged before its cap
-        const bool conv = hst[q] == 0 && hit[q] < ps[idx[0]].prm.qp_iter_max;
+        const nmpc_model_params& pp = ps[idx[0]].prm;
+        const bool conv = hst[q] == 0 && hit[q] < pp.qp_iter_max &&
+                          hit[q] <= (pp.qp_warm_iter_max > 0 ? pp.qp_warm_iter_max : pp.qp_iter_max);
         c->warm_ok = conv;
         e.owner[q] = c->uid;
         e.dev_warm[q] = conv ? 1 : 0;

@@ -95,6 +95,8 @@ KParams to_kparams(const nmpc_model_params& p, int nx, int nu, int nbx, int nbu)
     k.warm_kappa = (float)p.qp_warm_kappa;
     if (const char* v = std::getenv("NMPC_AMD_WARM")) k.warm = std::atoi(v) != 0;
     if (const char* v = std::getenv("NMPC_AMD_WARM_KAPPA")) k.warm_kappa = std::strtof(v, nullptr);
+    k.warm_iter_max = p.qp_warm_iter_max > 0 ? p.qp_warm_iter_max : p.qp_iter_max;
+    if (const char* v = std::getenv("NMPC_AMD_WARM_ITER_MAX")) k.warm_iter_max = std::atoi(v);
     return k;
 }
 
@@ -176,6 +178,7 @@ int check_params(const nmpc_model_params* prm)
         return set_err(NMPC_ERR_ARG, "qp_ipm must be NMPC_IPM_MEHROTRA or NMPC_IPM_SINGLE");
     if (prm->qp_warm_start != 0 && prm->qp_warm_start != 1) return set_err(NMPC_ERR_ARG, "qp_warm_start must be 0 or 1");
     if (prm->qp_warm_start && !(prm->qp_warm_kappa > 0.0)) return set_err(NMPC_ERR_ARG, "qp_warm_kappa must be > 0");
+    if (prm->qp_warm_iter_max < 0) return set_err(NMPC_ERR_ARG, "qp_warm_iter_max must be >= 0");
     if (prm->qp_ipm == NMPC_IPM_SINGLE &&
         !(prm->qp_sigma_lo > 0.0 && prm->qp_sigma_lo <= prm->qp_sigma_hi && prm->qp_sigma_hi <= 1.0))
         return set_err(NMPC_ERR_ARG, "qp_sigma_lo / qp_sigma_hi need 0 < lo <= hi <= 1");
@@ -263,6 +266,10 @@ int nmpc_model_params_default(int model, int N, nmpc_model_params* prm)
     // worst case: 29 against 39 iterations), omni4 and tric 0.01 (+7 % / +4 % against 0.05)
     prm->qp_warm_start = 1;
     prm->qp_warm_kappa = (model == NMPC_MODEL_DIFF2AMR) ? 0.2 : 0.01;
+    // warm start only after an easy solve: on 3 x 4096 stationary bench QPs (tools/warm_study.py, renewals in
+    // the loop) warm after <= 12 iterations gives mean 8.78 / per-tick max 22, 21, 21 IPM iterations against
+    // 8.60 / 30, 25, 27 for warm always and 9.38 / 22, 21, 21 for cold
+    prm->qp_warm_iter_max = 12;
     return NMPC_OK;
 }
 

@@ -31,6 +31,7 @@ struct KParams {
     // warm start of the bound multipliers from the robot's previous solve (KArgs::warm flags)
     int warm;
     float warm_kappa;
+    int warm_iter_max;  // a solve that needed more IPM iterations starts the next one cold
 };
 
 enum ModelId { kDiff = 0, kOmni4 = 1, kTric = 2 };

@@ -1069,7 +1069,8 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
         if (a.qp_iter) a.qp_iter[inst] = it_done;
         if (a.iter_key) a.iter_key[inst] = it_done;
         // warm-start the next solve only from a solve that converged (not from one that ran to qp_iter_max)
-        if (a.warm) a.warm[inst] = (P.warm && status == 0 && it_done < P.iter_max) ? 1 : 0;
+        // and only from an easy one (P.warm_iter_max, 12 by default: warm multipliers lengthen the hard QPs)
+        if (a.warm) a.warm[inst] = (P.warm && status == 0 && it_done < P.iter_max && it_done <= P.warm_iter_max) ? 1 : 0;
         if (a.qp_res) {
 #pragma unroll
             for (int j = 0; j < 3; j++) a.qp_res[(size_t)j * Bn + inst] = exit_res[j];
