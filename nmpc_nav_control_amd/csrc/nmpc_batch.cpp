@@ -266,10 +266,12 @@ int nmpc_model_params_default(int model, int N, nmpc_model_params* prm)
     // worst case: 29 against 39 iterations), omni4 and tric 0.01 (+7 % / +4 % against 0.05)
     prm->qp_warm_start = 1;
     prm->qp_warm_kappa = (model == NMPC_MODEL_DIFF2AMR) ? 0.2 : 0.01;
-    // warm start only after an easy solve: on 3 x 4096 stationary bench QPs (tools/warm_study.py, renewals in
-    // the loop) warm after <= 12 iterations gives mean 8.78 / per-tick max 22, 21, 21 IPM iterations against
-    // 8.60 / 30, 25, 27 for warm always and 9.38 / 22, 21, 21 for cold
-    prm->qp_warm_iter_max = 12;
+    // diff: warm start only after an easy solve. On 3 x 4096 stationary bench QPs (tools/warm_study.py, renewals
+    // in the loop) warm after <= 12 iterations gives mean 8.78 / per-tick max 22, 21, 21 IPM iterations against
+    // 8.60 / 30, 25, 27 for warm always and 9.38 / 22, 21, 21 for cold; same-box A/B (profiles/r03/ab/warm_iter.txt)
+    // metric 3.00 -> 3.73 M it/s (cold 3.75, <= 10: 3.74, <= 16: 3.19), diff1024 0.87 -> 1.02 M. omni4 and tric
+    // (kappa 0.01) lose with the rule (omni4 2.88 -> 2.47, tric 3.06 -> 2.82, mixed 4.52 -> 3.96 M): always warm
+    prm->qp_warm_iter_max = (model == NMPC_MODEL_DIFF2AMR) ? 12 : 0;
     return NMPC_OK;
 }
 
