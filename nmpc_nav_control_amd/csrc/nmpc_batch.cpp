@@ -26,7 +26,10 @@ struct nmpc_batch {
     float* scratch = nullptr;
     int sched = NMPC_SCHED_AUTO;
     int n_simd = 1024;           // SIMDs of the device (4 per CU)
-    int split_max = 256;         // launches of at most this many robots run one wave per robot (KArgs::split)
+    int split_max = 256;         // team-kernel launches of at most this many robots run one block per robot (split)
+    // launches of at most this many robots (single-direction IPM, not run_path) run k_sqp_rti_rowpar: one wave
+    // per robot with its stage-independent work spread over the wave's 4 rows (latency)
+    int rowpar_max = 1024;
     int* iter_key = nullptr;     // [capacity] last executed IPM iterations per robot (written by the team kernel)
     int* order = nullptr;        // [capacity] team slot -> robot
     unsigned char* warm = nullptr;  // [capacity] the robot's last solve succeeded: its scratch records hold its
@@ -112,15 +115,28 @@ size_t scratch_floats(int model, int N, int stride)
 template <class M>
 hipError_t launch_m(nmpc_batch* b, const KArgs& a, int mode, hipStream_t s)
 {
-    (void)b;
+    if (a.rowpar) return launch_sqp_rti_rowpar<M>(b->kp, a, mode, s);
     return launch_sqp_rti_team<M>(b->kp, a, mode, s);
 }
 
+template <class M>
+bool rowpar_ok(const nmpc_batch* b, const KArgs& a, int mode)
+{
+    return b->kp.ipm == NMPC_IPM_SINGLE && !a.segs && a.B <= b->rowpar_max &&
+           rowpar_lds_bytes<M>(b->prm.N, mode) <= 65536;
+}
+
 // Team placement before a team-kernel launch (schedule.hip); fills a.order / a.iter_key
-hipError_t schedule(nmpc_batch* b, KArgs& a, hipStream_t s)
+hipError_t schedule(nmpc_batch* b, KArgs& a, int mode, hipStream_t s)
 {
     a.iter_key = b->iter_key;
     a.warm = b->warm;
+    switch (b->prm.model) {
+    case NMPC_MODEL_DIFF2AMR: a.rowpar = rowpar_ok<Diff2>(b, a, mode); break;
+    case NMPC_MODEL_OMNI4AMR: a.rowpar = rowpar_ok<Omni4>(b, a, mode); break;
+    default: a.rowpar = rowpar_ok<Tric3>(b, a, mode); break;
+    }
+    if (a.rowpar) return hipSuccess;  // one robot per wave: nothing to place
     a.dense = ((a.B + 3) / 4 > b->n_simd) ? 1 : 0;  // 4 teams per wave
     // small batches leave most of the chip idle: one wave per robot, whose spare rows integrate P0's stages
     a.split = (!a.dense && a.B <= b->split_max) ? 1 : 0;
@@ -134,7 +150,7 @@ hipError_t schedule(nmpc_batch* b, KArgs& a, hipStream_t s)
 
 hipError_t launch(nmpc_batch* b, KArgs& a, int mode, hipStream_t s)
 {
-    const hipError_t e = schedule(b, a, s);
+    const hipError_t e = schedule(b, a, mode, s);
     if (e != hipSuccess) return e;
     switch (b->prm.model) {
     case NMPC_MODEL_DIFF2AMR: return launch_m<Diff2>(b, a, mode, s);
@@ -313,6 +329,7 @@ int nmpc_batch_create(const nmpc_model_params* prm, int capacity, nmpc_batch** o
             if (std::strcmp(sv, names[i]) == 0) b->sched = i;
     }
     if (const char* v = std::getenv("NMPC_AMD_SPLIT_MAX")) b->split_max = std::atoi(v);  // A/B: 0 = never split
+    if (const char* v = std::getenv("NMPC_AMD_ROWPAR_MAX")) b->rowpar_max = std::atoi(v);  // A/B: 0 = never
     const int N = prm->N;
     const size_t S = (size_t)capacity;
     hipError_t e;

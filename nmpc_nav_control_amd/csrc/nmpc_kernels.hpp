@@ -56,6 +56,7 @@ struct KArgs {
     unsigned char* warm;  // [stride] resident: 1 if the robot's last solve succeeded (its records hold its
                           // multipliers), or nullptr (cold start, nothing written)
     int dense;      // the launch has more waves than the device has SIMDs (selects the team kernel variant)
+    int rowpar;     // launched as k_sqp_rti_rowpar (one wave per robot)
     int split;      // one 256-lane block per robot: P0's integrations spread over its 16 rows (4 waves, stage k on
                     // row k mod 16, joined by a block barrier); small batches
 };
@@ -64,6 +65,11 @@ template <class M>
 size_t team_scratch_floats(int N, int stride);
 template <class M>
 hipError_t launch_sqp_rti_team(const KParams& P, const KArgs& a, int mode, hipStream_t stream);
+// small batches: one wave per robot, stage-parallel phases over its four rows (sqp_rti_rowpar.hip)
+template <class M>
+hipError_t launch_sqp_rti_rowpar(const KParams& P, const KArgs& a, int mode, hipStream_t stream);
+template <class M>
+size_t rowpar_lds_bytes(int N, int mode);
 template <class M>
 hipError_t launch_fleet_sim(const KParams& P, int B, int stride, float* path, float* s, float* pose, float* vel,
                             float* steer, const float* u0, const int* status, const float* carried, float* traj,

@@ -1,0 +1,725 @@
+// sqp_rti_rowpar.hip -- batched SQP-RTI step for small batches: one wavefront per robot, the stage-independent
+// work spread over the wave's four DPP rows, only the recursions over the horizon serial.
+//
+// The same single-direction IPM as k_sqp_rti_team (sqp_rti_team.hip, SD rule; DESIGN.md "Algorithm and
+// precision"), the same records, warm start and stopping rule, reorganised for latency. In the team kernel one
+// 16-lane team runs every stage of every sweep in turn: per IPM iteration 81 x ~350 instructions of P1 and
+// 81 x ~130 of the forward sweep at N = 80, one robot's solve being the reference's whole deployment
+// (NMPCNavControlROS.cpp:713 -> NMPCNavControlDiff.cpp:142). Most of that work does not depend on the
+// neighbouring stage: applying the step, the slacks / multipliers, the residuals, the barrier weights and the
+// rhs terms before the Riccati step (phase A), and the bound directions, the step bound and the complementarity
+// polynomial after the forward recursion (phase D). Here row q of the wave (lanes 16q .. 16q+15, lane 16q + v
+// owns variable v as in a team) runs those phases for stages q, q+4, ...; the Riccati factorisation (phase B:
+// fp64 P G, G'P G, input-block Cholesky, rhs) and the forward recursion of the directions (phase C) are the only
+// stage-serial passes, and every row computes them identically (same records, same DPP broadcasts inside its
+// row), so no row waits on another and stores of the serial phases are identical from all rows. P0 likewise:
+// the RK4 linearisation of stage k on row k mod 4, then the serial initial-iterate pass from LDS.
+// One robot per wave also makes every loop exit wave-uniform (no lockstep teams).
+#include "nmpc_kernels.hpp"
+#include "team_common.hpp"
+
+namespace nmpc {
+
+// Record layout: TeamRec<M, true> (the team kernel's single-direction layout: the warm-start multipliers LL / LU,
+// the DZ plane and the record stride are shared, so a handle may alternate kernels between solves) plus three
+// fields the team kernel leaves unused under the single-direction rule (its RU / DZA slots and the DZ register
+// slot): SIG (barrier weight), C0 (h z + g - (l_lo - l_up), the stationarity term without the adjoint) and GH
+// (the bound part of the rhs), written by phase A for phase B.
+template <class M>
+struct RowRec {
+    using T = TeamRec<M, true>;
+    static constexpr int NX = M::NX, NU = M::NU, NV = NX + NU, NGV = M::NGV;
+    static constexpr int LR = T::LR, LM = T::LM, Z = T::Z, TL = T::TL, TU = T::TU, LL = T::LL, LU = T::LU;
+    static constexpr int LB = T::LB, UB = T::UB, GV = T::GV, GR = T::GR, RS = T::RS;
+    static constexpr int SIG = GR + 1, C0 = GR + 2, GH = GR + 3;
+    static_assert(GH < RS, "phase-A fields fit the team record");
+    static_assert(T::L2 ? (SIG == T::RU && C0 == T::DZA) : (SIG > T::DZA && SIG > T::RU),
+                  "phase-A fields reuse only slots the single-direction team kernel leaves unused");
+    static_assert(LM + NU <= Z && Z < TL, "LR / LM below Z");
+};
+
+namespace {
+
+template <int F0, int F1, int RS, bool QM>
+__device__ __forceinline__ void ld_range(const float* p, float (&v)[RS])
+{
+    rec_load_range<F0, F1, RS, QM>(p, v);
+}
+
+// cross-row reductions of the wave (the four rows hold disjoint stages in the stage-parallel phases)
+__device__ __forceinline__ float wave_sum_rows(float v)
+{
+    v += __shfl_xor(v, 16);
+    return v + __shfl_xor(v, 32);
+}
+__device__ __forceinline__ float wave_max_rows(float v)
+{
+    v = fmaxf(v, __shfl_xor(v, 16));
+    return fmaxf(v, __shfl_xor(v, 32));
+}
+__device__ __forceinline__ float wave_min_rows(float v)
+{
+    v = fminf(v, __shfl_xor(v, 16));
+    return fminf(v, __shfl_xor(v, 32));
+}
+
+template <class M>
+__global__ __launch_bounds__(64, 1) void k_sqp_rti_rowpar(KParams P, KArgs a, int mode)
+{
+    using R = RowRec<M>;
+    constexpr int NX = M::NX, NU = M::NU, NV = R::NV, NGV = R::NGV, RS = R::RS;
+    constexpr bool QM = rec_quad_major<NV>();
+    constexpr int ROWS = 4;
+    const int inst = (int)blockIdx.x;
+    if (inst >= a.B) return;
+    const int lane = (int)threadIdx.x;
+    const int q = lane >> 4;  // row: stage-parallel phases take stages q, q + 4, ...
+    const int r = lane & 15;  // slot: variable r of the stage (as a team lane)
+    const int N = P.N;
+    const size_t S = (size_t)a.stride;
+    const size_t Bn = (size_t)a.B;
+    const bool lv = r < NV;
+    const bool is_u = r < NU;
+    const bool is_x = lv && !is_u;
+    const int xi = is_x ? r - NU : 0;
+    const int cx = is_x ? xcomp<M>(xi) : -1;
+    const bool has_b = is_u || cx >= 0;
+    const float sc = P.dt;
+    const float w_lane = is_u ? P.W[NX + r] : (is_x ? P.W[xi] : 0.0f);
+    const float h_stage = sc * w_lane;
+    float lo_b = 0.0f, hi_b = 0.0f;
+#pragma unroll
+    for (int j = 0; j < NU; j++)
+        if (r == j) { lo_b = P.lbu[j]; hi_b = P.ubu[j]; }
+#pragma unroll
+    for (int c = 0; c < M::NBX; c++)
+        if (cx == c) { lo_b = P.lbx[c]; hi_b = P.ubx[c]; }
+    constexpr int KS = 16 * RS;
+    const int NR = (N + 1 + ROWS - 1) / ROWS;  // rounds of the stage-parallel phases
+    float* const rbase = a.scratch + (size_t)inst * (N + 1) * KS;
+    float* const tbase = rbase + (lv ? r : 0) * rec_lane<RS, QM>();   // idle slots read slot 0
+    float* const tbase_own = rbase + r * rec_lane<RS, QM>();          // every lane's own slot
+    float* const tdummy = rbase + (size_t)N * KS + 15 * rec_lane<RS, QM>();  // nobody reads it
+    float* const dzbase = a.scratch + (size_t)a.stride * (N + 1) * KS + (size_t)inst * (N + 1) * 16 + r;
+    const bool warm = P.warm && a.warm && a.warm[inst] && !(a.reset && a.reset[inst]);
+
+#define XB(k, j) a.xbar[((size_t)(k) * NX + (j)) * S + inst]
+#define UBAR(k, j) a.ubar[((size_t)(k) * NU + (j)) * S + inst]
+
+    // ---- reset ({name}_acados_reset: zero iterate) ----------------------------------------------------------
+    if (a.reset && a.reset[inst]) {
+        for (int e = lane; e < (N + 1) * NX; e += 64) XB(e / NX, e % NX) = 0.0f;
+        for (int e = lane; e < N * NU; e += 64) UBAR(e / NU, e % NU) = 0.0f;
+        __threadfence_block();
+    }
+
+    // ---- x0 -----------------------------------------------------------------------------------------------
+    float x0[NX];
+    float pose_th = 0.0f;
+    if (mode == kModeRun) {
+        const float pose[3] = {a.pose[inst], a.pose[Bn + inst], a.pose[2 * Bn + inst]};
+        const float vel[3] = {a.vel[inst], a.vel[Bn + inst], a.vel[2 * Bn + inst]};
+        const float steer = a.steer ? a.steer[inst] : 0.0f;
+        x0[0] = pose[0];
+        x0[1] = pose[1];
+        x0[2] = pose[2];
+        pose_th = pose[2];
+        M::direct_kin(vel, steer, P, x0 + 3);
+#pragma unroll
+        for (int i = 0; i < M::NBX; i++) x0[M::idxbx(i)] = a.carried[(size_t)i * S + inst];
+    } else {
+#pragma unroll
+        for (int j = 0; j < NX; j++) x0[j] = a.x0[(size_t)j * Bn + inst];
+    }
+    float x0_lane = 0.0f;
+#pragma unroll
+    for (int j = 0; j < NX; j++)
+        if (xi == j) x0_lane = x0[j];
+    float we_lane = 0.0f;
+    if (is_x) we_lane = (mode != kModeRun && a.We) ? a.We[(size_t)xi * Bn + inst] : P.We[xi];
+
+    // ---- P0a: RK4 linearisation of stage k on row k mod 4 -> LDS [k][field][lane] -----------------------------
+    // fields: zbar, yref entry, warm multipliers (2), defect b_k, the NGV varying Jacobian rows; run mode also the
+    // stage's reference pose in my_traj
+    constexpr int SF = 5 + NGV;
+    extern __shared__ float s_row[];
+    float* const s_stg = s_row;
+    float* const my_traj = s_row + (size_t)(N + 1) * SF * 16;
+    const int len = (mode == kModeRun) ? (a.traj_len ? a.traj_len[inst] : N + 1) : 0;
+    {
+        struct In {
+            float x[NX], u[NU], y, xnext, tq;
+            float2 l;
+        };
+        auto ld = [&](int k, In& v) {
+            const int kk = k <= N ? k : N;
+#pragma unroll
+            for (int j = 0; j < NX; j++) v.x[j] = XB(kk, j);
+            const int ku = kk < N ? kk : N - 1;
+#pragma unroll
+            for (int j = 0; j < NU; j++) v.u[j] = UBAR(ku, j);
+            v.xnext = XB(kk < N ? kk + 1 : N, xi);
+            v.y = 0.0f;
+            v.tq = 0.0f;
+            if (mode != kModeRun) {
+                const int j = is_u ? NX + r : xi;
+                v.y = (lv && j < a.ny_in) ? a.yref[((size_t)kk * a.ny_in + j) * Bn + inst] : 0.0f;
+            } else if (r < 3) {
+                const int kt = kk < len ? kk : (len > 0 ? len - 1 : 0);
+                v.tq = a.traj[((size_t)kt * 3 + r) * Bn + inst];
+            }
+            v.l = warm ? *reinterpret_cast<const float2*>(tbase + (size_t)kk * KS + rec_off<RS, QM>(R::LL))
+                       : make_float2(0.0f, 0.0f);
+        };
+        In cur, nxt;
+        ld(q, cur);
+        // wave-uniform trip count: rows past the last stage repeat stage N and write nothing
+        for (int j = 0; j < NR; j++) {
+            const int k = j * ROWS + q;
+            ld(k + ROWS, nxt);
+            const bool kv = k <= N;
+            if (mode == kModeRun && r < 3 && kv) my_traj[k * 3 + r] = cur.tq;
+            float xn[NX], g[NX];
+#pragma unroll
+            for (int i = 0; i < NX; i++) { xn[i] = 0.0f; g[i] = 0.0f; }
+            float bk = 0.0f;
+            if (k < N) {  // (rows past the end: k > N)
+                rk4_column<M>(cur.x, cur.u, P, lv ? r : NU, xn, g);
+#pragma unroll
+                for (int i = 0; i < NX; i++)
+                    if (is_x && xi == i) bk = xn[i] - cur.xnext;
+            }
+            float zb = 0.0f;
+#pragma unroll
+            for (int j = 0; j < NU; j++)
+                if (r == j) zb = cur.u[j];
+#pragma unroll
+            for (int j = 0; j < NX; j++)
+                if (is_x && xi == j) zb = cur.x[j];
+            if (kv) {
+                float* const st = s_stg + (size_t)k * SF * 16 + r;
+                st[0] = zb;
+                st[16] = cur.y;
+                st[32] = cur.l.x;
+                st[48] = cur.l.y;
+                st[64] = bk;
+#pragma unroll
+                for (int i = 0; i < NGV; i++) st[(5 + i) * 16] = g[i];
+            }
+            cur = nxt;
+        }
+    }
+    // constant rows of [B A] (rows >= NGV) from stage 0 (every row, identically)
+    float gcol[NX], grow[NV];
+    {
+        float xb0[NX], ub0[NU], xn0[NX], g0[NX];
+#pragma unroll
+        for (int j = 0; j < NX; j++) xb0[j] = XB(0, j);
+#pragma unroll
+        for (int j = 0; j < NU; j++) ub0[j] = UBAR(0, j);
+        rk4_column<M>(xb0, ub0, P, lv ? r : NU, xn0, g0);
+#pragma unroll
+        for (int i = 0; i < NX; i++) gcol[i] = (lv && i >= NGV) ? g0[i] : 0.0f;
+        sfor<0, NV>([&](auto vc) {
+            constexpr int v = decltype(vc)::value;
+            float sv = 0.0f;
+#pragma unroll
+            for (int i = NGV; i < NX; i++) {
+                const float t = bc<v>(gcol[i]);
+                if (is_x && xi == i) sv = t;
+            }
+            grow[v] = sv;
+        });
+    }
+    __syncthreads();  // one wave per block: the stage inputs of every row are in LDS
+
+    // ---- P0b: the serial pass (every row identically): reference unwrap / pad, gradient, bounds, slacks,
+    // multipliers, the record, and the dynamics-feasible initial iterate dx_{k+1} = A dx_k + b_k --------------
+    float dx = is_x ? x0_lane - XB(0, xi) : 0.0f;
+    float sum_c0 = 0.0f;
+    {
+        float ref_x = 0.0f, ref_y = 0.0f, ref_t = pose_th, prv_x = 0.0f, prv_y = 0.0f, prv_t = 0.0f;
+        struct Stg {
+            float v[5], g[NGV], t[3];
+        };
+        auto lds_ld = [&](int k, Stg& o) {
+            const int kk = k <= N ? k : N;
+            const float* const st = s_stg + (size_t)kk * SF * 16 + r;
+#pragma unroll
+            for (int f = 0; f < 5; f++) o.v[f] = st[f * 16];
+#pragma unroll
+            for (int i = 0; i < NGV; i++) o.g[i] = st[(5 + i) * 16];
+#pragma unroll
+            for (int j = 0; j < 3; j++) o.t[j] = (mode == kModeRun) ? my_traj[kk * 3 + j] : 0.0f;
+        };
+        Stg cur, nxt;
+        lds_ld(0, cur);
+        for (int k = 0; k <= N; k++) {
+            lds_ld(k + 1, nxt);
+            float yr = cur.v[1];
+            if (mode == kModeRun) {
+                if (k < len) {
+                    ref_x = cur.t[0];
+                    ref_y = cur.t[1];
+                    float th = cur.t[2];
+                    const float d = th - ref_t;
+                    if (d > kPi) th -= 2.0f * kPi;
+                    else if (d < -kPi) th += 2.0f * kPi;
+                    ref_t = th;
+                }
+                if (k == N - 1) { prv_x = ref_x; prv_y = ref_y; prv_t = ref_t; }
+                yr = (is_x && xi == 0) ? ref_x : ((is_x && xi == 1) ? ref_y : ((is_x && xi == 2) ? ref_t : 0.0f));
+            }
+            const float zbar = cur.v[0];
+            float rec[RS];
+#pragma unroll
+            for (int f = 0; f < RS; f++) rec[f] = 0.0f;
+            const bool vu = is_u && k < N, vx = is_x && k >= 1;
+            const bool valid = vu || vx;
+            if (vu) rec[R::GR] = sc * w_lane * (zbar - yr);
+            if (vx) {
+                float w = sc * w_lane;
+                if (k == N) {
+                    w = we_lane;
+                    if (mode == kModeRun && P.terminal_hack && xi < 3) {  // NMPCNavControlDiff.cpp:127-139
+                        const bool eq = (ref_x == prv_x) && (ref_y == prv_y) && (ref_t == prv_t);
+                        w = (eq ? 100.0f : 1.0f) * w_lane;
+                        we_lane = w;
+                    }
+                }
+                rec[R::GR] = w * (zbar - yr);
+            }
+            const float z = vx ? dx : 0.0f;
+            rec[R::Z] = z;
+            rec[R::TL] = kFar;
+            rec[R::TU] = kFar;
+            rec[R::LB] = -kFar;
+            rec[R::UB] = kFar;
+            if (valid && has_b) {
+                const float lb = lo_b - zbar, ubd = hi_b - zbar;
+                const float tl = fmaxf(z - lb, P.thr0), tu = fmaxf(ubd - z, P.thr0);
+                rec[R::LB] = lb;
+                rec[R::UB] = ubd;
+                rec[R::TL] = tl;
+                rec[R::TU] = tu;
+                const float ll0 = warm ? fmaxf(fminf(cur.v[2], kWarmLambdaCap), P.warm_kappa / tl) : P.mu0 / tl;
+                const float lu0 = warm ? fmaxf(fminf(cur.v[3], kWarmLambdaCap), P.warm_kappa / tu) : P.mu0 / tu;
+                rec[R::LL] = ll0;
+                rec[R::LU] = lu0;
+                sum_c0 += ll0 * tl + lu0 * tu;
+            }
+#pragma unroll
+            for (int i = 0; i < NGV; i++) rec[R::GV + i] = (k < N && lv) ? cur.g[i] : 0.0f;
+            rec_store<RS, QM>(tbase_own + (size_t)k * KS, rec);  // idle lanes: their own unused slot
+            dzbase[(size_t)k * 16] = 0.0f;
+            if (k < N) {
+                const float dzd = is_x ? dx : 0.0f;
+                float nx_ = dot_v<NX, NU>(0.0f, dzd, grow);
+#pragma unroll
+                for (int i = 0; i < NGV; i++) {
+                    const float sr = row_sum16(lv ? cur.g[i] * dzd : 0.0f);
+                    if (xi == i) nx_ = sr;
+                }
+                dx = is_x ? nx_ + cur.v[4] : 0.0f;
+            }
+            cur = nxt;
+        }
+    }
+    __threadfence_block();  // the records before the stage-parallel phase A reads them on other rows
+
+    double onehot[NV];
+#pragma unroll
+    for (int j = 0; j < NV; j++) onehot[j] = (r == j) ? 1.0 : 0.0;
+    double gcol64[NX];
+#pragma unroll
+    for (int i = 0; i < NX; i++) gcol64[i] = (double)gcol[i];
+    const int m = N * NU + N * M::NBX;
+    const float inv_m2 = 0.5f / (float)m;
+    sum_c0 = row_sum16(lv ? sum_c0 : 0.0f);
+
+    auto column = [&](const float (&rc)[RS], float (&Gc)[NX]) {
+#pragma unroll
+        for (int i = 0; i < NX; i++) Gc[i] = (i < NGV) ? rc[R::GV + (i < NGV ? i : 0)] : gcol[i];
+    };
+    auto dyn = [&](const float (&rc)[RS], float dzv) -> float {
+        float nx_ = 0.0f;
+#pragma unroll
+        for (int i = 0; i < NGV; i++) {
+            const float s = row_sum16(lv ? rc[R::GV + i] * dzv : 0.0f);
+            if (xi == i) nx_ = s;
+        }
+        const float cr = dot_v<NX, NU>(0.0f, dzv, grow);
+        return (xi >= NGV) ? cr : nx_;
+    };
+    // serial sweep k0 -> k1 with the next stage's fields [F0, F1) (+ the DZ plane) in flight (ping-pong buffers,
+    // loads never predicated: the loop is wave-uniform)
+    auto serial = [&](auto f0c, auto f1c, auto dzc, int k0, int k1, int dir, auto&& body) {
+        constexpr int F0 = decltype(f0c)::value, F1 = decltype(f1c)::value;
+        constexpr bool DZ = decltype(dzc)::value;
+        static_assert(!DZ, "the serial phases read no DZ");
+        auto load = [&](int k, float (&v)[RS]) { ld_range<F0, F1, RS, QM>(tbase + (size_t)k * KS, v); };
+        float ra[RS], rb[RS];
+        load(k0, ra);
+        for (int k = k0;; k += 2 * dir) {
+            const int k_1 = (k == k1) ? k : k + dir;
+            load(k_1, rb);
+            body(k, ra);
+            if (k == k1) break;
+            const int k_2 = (k_1 == k1) ? k_1 : k_1 + dir;
+            load(k_2, ra);
+            body(k + dir, rb);
+            if (k + dir == k1) break;
+        }
+    };
+
+    // ---- interior-point iterations (single-direction rule) -----------------------------------------------------
+    int status = 0, it_done = 0;
+    float exit_res[3] = {0.0f, 0.0f, 0.0f};
+    float alpha = 0.0f, sigma_mu = 0.0f, mu_prev = 3.0e38f;
+    float tg_rhs = P.sd_hi * sum_c0 * inv_m2;
+    for (int it = 0;; it++) {
+        // phase A (stage-parallel): apply the previous step, residuals, barrier weight, rhs terms
+        const float a_upd = (it > 0) ? alpha : 0.0f;
+        float res_ineq = 0.0f, sum_c = 0.0f, max_c = 0.0f, lam_max = 0.0f, sc0 = 1.0f, nanf_ = 0.0f;
+        for (int j = 0; j < NR; j++) {
+            const int kr = j * ROWS + q;
+            const bool kv = kr <= N;       // rows past the last stage redo stage N into the dummy record
+            const int k = kv ? kr : N;
+            float rc[RS];
+            ld_range<R::Z, R::GR + 1, RS, QM>(tbase + (size_t)k * KS, rc);
+            const float dz = dzbase[(size_t)k * 16];
+            const bool vu = is_u && k < N && kv;
+            const bool vx = is_x && k >= 1 && kv;
+            const bool valid = vu || vx;
+            const bool bnd = valid && has_b;
+            float z = rc[R::Z];
+            float tl = rc[R::TL], tu = rc[R::TU], ll = rc[R::LL], lu = rc[R::LU];
+            const float lb = rc[R::LB], ubd = rc[R::UB];
+            {
+                const float rl = z - lb - tl, rr = ubd - z - tu;
+                const float itl = frcp(tl), itu = frcp(tu);
+                const BoundDir d = bound_dir(dz, rl, rr, tl, tu, ll, lu, itl, itu, sigma_mu, sigma_mu);
+                const float ab = bnd ? a_upd : 0.0f, av = valid ? a_upd : 0.0f;
+                tl += ab * d.dtl;
+                tu += ab * d.dtu;
+                ll += ab * d.dll;
+                lu += ab * d.dlu;
+                z += av * dz;
+            }
+            const float rl = z - lb - tl, rr = ubd - z - tu;
+            const float itl = frcp(tl), itu = frcp(tu);
+            res_ineq = fmaxf(res_ineq, kv ? fmaxf(fabsf(rl), fabsf(rr)) : 0.0f);
+            sum_c += kv ? ll * tl + lu * tu : 0.0f;
+            max_c = fmaxf(max_c, kv ? fmaxf(ll * tl, lu * tu) : 0.0f);
+            lam_max = fmaxf(lam_max, kv ? fmaxf(ll, lu) : 0.0f);
+            const float lamdiff = ll - lu;
+            const float sig = ll * itl + lu * itu;
+            const float gh = ll * rl * itl + ll - lu * rr * itu - lu - tg_rhs * itl + tg_rhs * itu;
+            const float g = rc[R::GR];
+            const float hz = ((k < N) ? h_stage : we_lane) * z;
+            const float c0 = hz + g - lamdiff;
+            if (vu) sc0 = fmaxf(sc0, fmaxf(fabsf(g), fabsf(lamdiff)));
+            if (kv && (sig != sig || gh != gh || c0 != c0)) nanf_ = 1.0f;
+            rc[R::Z] = z;
+            rc[R::TL] = tl;
+            rc[R::TU] = tu;
+            rc[R::LL] = ll;
+            rc[R::LU] = lu;
+            rc[R::SIG] = sig;
+            rc[R::C0] = c0;
+            rc[R::GH] = valid ? gh : 0.0f;
+            float* const pk = (lv && kv) ? tbase + (size_t)k * KS : tdummy;
+            rec_store_range<R::Z, R::LU + 1, RS, QM>(pk, rc);
+            rec_store_range<R::SIG, R::GH + 1, RS, QM>(pk, rc);
+        }
+        __threadfence_block();
+        sum_c = wave_sum_rows(row_sum16(lv ? sum_c : 0.0f));
+        max_c = wave_max_rows(row_max16(lv ? max_c : 0.0f));
+        lam_max = wave_max_rows(row_max16(lv ? lam_max : 0.0f));
+        res_ineq = wave_max_rows(row_max16(lv ? res_ineq : 0.0f));
+        sc0 = wave_max_rows(row_max16(sc0));
+        nanf_ = wave_max_rows(row_max16(nanf_));
+        const float mu = sum_c * inv_m2;
+
+        // phase B (serial, N -> 0): adjoint, fp64 classic Riccati step, rhs / forward substitution
+        double Lrow[NV];
+#pragma unroll
+        for (int j = 0; j < NV; j++) Lrow[j] = 0.0;
+        float pv = 0.0f, piv = 0.0f, res_stat = 0.0f, cpi_max = 0.0f;
+        bool fail = false;
+        if (!(nanf_ > 0.0f || mu != mu)) {
+            serial(std::integral_constant<int, R::GV>{}, std::integral_constant<int, R::GH + 1>{},
+                   std::false_type{}, N, 0, -1, [&](int k, float (&rc)[RS]) {
+                const bool vu = is_u && k < N;
+                const bool vx = is_x && k >= 1;
+                const bool valid = vu || vx;
+                float Gc[NX];
+                column(rc, Gc);
+                const float cpi = (k < N) ? dot_x<NX, NU>(0.0f, piv, Gc) : 0.0f;
+                const float base = rc[R::C0] + cpi;
+                res_stat = fmaxf(res_stat, vu ? fabsf(base) : 0.0f);
+                cpi_max = fmaxf(cpi_max, vu ? fabsf(cpi) : 0.0f);
+                const float sig = rc[R::SIG];
+                const float ghat = valid ? (vu ? rc[R::GH] + base : rc[R::GH]) : 0.0f;
+                const float pi_new = vx ? base : 0.0f;
+                if (ghat != ghat) nanf_ = 1.0f;
+                if (k == N) {
+                    const double d = is_x ? (double)fmaxf(we_lane + sig, 0.0f) : 0.0;
+#pragma unroll
+                    for (int j = 0; j < NV; j++) Lrow[j] = (is_x && j == r) ? d : 0.0;
+                    pv = is_x ? ghat : 0.0f;
+                } else {
+                    double Gd[NX];
+#pragma unroll
+                    for (int l = 0; l < NX; l++) Gd[l] = (l < NGV) ? (double)Gc[l] : gcol64[l];
+                    double pg[NX];
+#pragma unroll
+                    for (int i = 0; i < NX; i++) pg[i] = 0.0;
+                    pg_block<NX, NU>(pg, Lrow, Gd);
+                    const double dg = valid ? (double)h_stage + (double)sig : 1.0;
+                    double Lr[NV];
+#pragma unroll
+                    for (int j = 0; j < NV; j++) Lr[j] = onehot[j] * dg;
+                    double pivot;
+                    mrow_pg_block<NX, NU>(Lr, pivot, pg, Gd);
+                    sfor<0, NU>([&](auto jc) {
+                        constexpr int j = decltype(jc)::value;
+                        if (!(pivot > 0.0)) fail = true;
+                        const double rd = drsq(fmax(pivot, 1e-300));
+                        const double lj = (r >= j) ? Lr[j] * rd : 0.0;
+                        Lr[j] = lj;
+                        chol_update<NX, NU, j>(Lr, lj, pivot);
+                    });
+                    float Lm[NU];
+#pragma unroll
+                    for (int qq = 0; qq < NU; qq++) {
+                        Lm[qq] = (float)Lr[qq];
+                        rc[R::LM + qq] = Lm[qq];
+                    }
+                    float y = dot_x<NX, NU>(ghat, pv, Gc);
+                    float my_lr = 0.0f;
+                    sfor<0, NU>([&](auto jc) {
+                        constexpr int j = decltype(jc)::value;
+                        const float lrj = bc<j>(y * frcp(Lm[j]));
+                        if (r == j) my_lr = lrj;
+                        y -= Lm[j] * lrj;
+                    });
+                    rc[R::LR] = my_lr;
+                    pv = is_x ? y : 0.0f;
+#pragma unroll
+                    for (int j = 0; j < NV; j++) Lrow[j] = Lr[j];
+                    // LR, LM (every row stores the same values; idle slots store into the dummy record)
+                    rec_store_range<R::LR, R::LM + NU, RS, QM>(lv ? tbase + (size_t)k * KS : tdummy, rc);
+                }
+                piv = pi_new;
+            });
+        }
+        res_stat = row_max16(lv ? res_stat : 0.0f);
+        const float stat_scale = fmaxf(sc0, row_max16(lv ? cpi_max : 0.0f));
+        nanf_ = row_max16(nanf_);
+        const float failf = row_max16(fail ? 1.0f : 0.0f);
+        // stopping rule of k_sqp_rti_team (DESIGN.md "Stopping rule")
+        exit_res[0] = res_stat;
+        exit_res[1] = res_ineq;
+        exit_res[2] = mu;
+        bool stop = false;
+        if (nanf_ > 0.0f || mu != mu) {
+            status = 1;
+            stop = true;
+        } else if (failf > 0.0f) {
+            status = (mu <= kBreakdownMuT && res_ineq <= P.tol_ineq * 10.0f) ? 0 : 4;
+            stop = true;
+        } else if (lam_max > kInfeasLambda && res_ineq > kInfeasRes) {
+            status = 4;
+            stop = true;
+        } else {
+            const bool stat_ok = res_stat <= P.tol_stat || res_stat <= kStatRelT * stat_scale;
+            const bool cmax_ok = max_c <= kCompMaxRatio * P.tol_comp;
+            const bool stalled = mu <= P.tol_comp && mu > 0.5f * mu_prev;
+            if (res_ineq <= P.tol_ineq &&
+                ((stat_ok && mu <= P.tol_comp && cmax_ok) || mu <= 1e-2f * P.tol_comp || (stalled && cmax_ok)))
+                stop = true;
+            if (it >= P.iter_max) stop = true;
+        }
+        mu_prev = mu;
+        if (stop) {
+            it_done = it;
+            break;
+        }
+        __threadfence_block();
+
+        // phase C (serial, 0 -> N): the direction's input part from the stored factor, its state part from the
+        // dynamics; every row the same (identical DZ stores)
+        sigma_mu = tg_rhs;
+        {
+            float dxs = 0.0f;
+            serial(std::integral_constant<int, 0>{}, std::integral_constant<int, R::GV + NGV>{}, std::false_type{},
+                   0, N, 1, [&](int k, float (&rc)[RS]) {
+                const bool vu = is_u && k < N;
+                const bool vx = is_x && k >= 1;
+                const bool valid = vu || vx;
+                float du_all[NU];
+#pragma unroll
+                for (int qq = 0; qq < NU; qq++) du_all[qq] = 0.0f;
+                if (k < N) {
+                    float w[NU];
+                    sfor<0, NU>([&](auto qc) {
+                        constexpr int qq = decltype(qc)::value;
+                        w[qq] = bc<qq>(rc[R::LR]) + ((k > 0) ? row_sum16(is_x ? rc[R::LM + qq] * dxs : 0.0f) : 0.0f);
+                    });
+                    sfor<0, NU>([&](auto qqc) {
+                        constexpr int qq = NU - 1 - decltype(qqc)::value;
+                        float sq = w[qq];
+                        sfor<qq + 1, NU>([&](auto jc) {
+                            constexpr int j = decltype(jc)::value;
+                            sq -= bc<j>(rc[R::LM + qq]) * du_all[j];
+                        });
+                        du_all[qq] = sq * frcp(bc<qq>(rc[R::LM + qq]));
+                    });
+#pragma unroll
+                    for (int qq = 0; qq < NU; qq++) du_all[qq] = -du_all[qq];
+                }
+                float dz = 0.0f;
+#pragma unroll
+                for (int qq = 0; qq < NU; qq++)
+                    if (r == qq) dz = du_all[qq];
+                dz = is_x ? ((k >= 1) ? dxs : 0.0f) : dz;
+                dz = valid ? dz : 0.0f;
+                dzbase[(size_t)k * 16] = dz;  // every lane its own entry (idle lanes: 0)
+                if (k < N) dxs = dyn(rc, dz);
+            });
+        }
+        __threadfence_block();
+
+        // phase D (stage-parallel): bound directions, fraction-to-boundary step bound, complementarity polynomial
+        float amax = 1e30f, s1 = 0.0f, s2 = 0.0f;
+        for (int j = 0; j < NR; j++) {
+            const int kr = j * ROWS + q;
+            const bool kv = kr <= N;
+            const int k = kv ? kr : N;
+            float rc[RS];
+            ld_range<R::Z, R::UB + 1, RS, QM>(tbase + (size_t)k * KS, rc);
+            const float dz = dzbase[(size_t)k * 16];
+            const bool valid = kv && ((is_u && k < N) || (is_x && k >= 1));
+            const bool bnd = valid && has_b;
+            const float z = rc[R::Z];
+            const float tl = rc[R::TL], tu = rc[R::TU], ll = rc[R::LL], lu = rc[R::LU];
+            const float rl = z - rc[R::LB] - tl, rr = rc[R::UB] - z - tu;
+            const float itl = frcp(tl), itu = frcp(tu);
+            const BoundDir d = bound_dir(dz, rl, rr, tl, tu, ll, lu, itl, itu, sigma_mu, sigma_mu);
+            if (kv) {
+                amax = step_bound_r(amax, tl, d.dtl);
+                amax = step_bound_r(amax, tu, d.dtu);
+                amax = step_bound_r(amax, ll, d.dll);
+                amax = step_bound_r(amax, lu, d.dlu);
+            }
+            s1 += bnd ? ll * d.dtl + tl * d.dll + lu * d.dtu + tu * d.dlu : 0.0f;
+            s2 += bnd ? d.dll * d.dtl + d.dlu * d.dtu : 0.0f;
+        }
+        amax = wave_min_rows(row_min16(lv ? amax : 1e30f));
+        s1 = wave_sum_rows(row_sum16(lv ? s1 : 0.0f));
+        s2 = wave_sum_rows(row_sum16(lv ? s2 : 0.0f));
+        alpha = fminf(1.0f, P.tau * amax);
+        const float mu_next = fmaxf((sum_c + alpha * s1 + alpha * alpha * s2) * inv_m2, 0.0f);
+        const float om = 1.0f - alpha;
+        tg_rhs = fminf(fmaxf(om * om, P.sd_lo), P.sd_hi) * mu_next;
+    }
+
+    // ---- full SQP step + outputs (row 0 stores; the other rows' entries point at the dummy record) -------------
+    if (status == 0) {
+        auto entry = [&](int k) -> float* {
+            const int kk = k <= N ? k : N;
+            return (q == 0 && is_x) ? &XB(kk, xi) : ((q == 0 && is_u && kk < N) ? &UBAR(kk, r) : tdummy);
+        };
+        constexpr int EC = 8;
+        for (int k0 = 0; k0 <= N; k0 += EC) {
+            float zs[EC], vs[EC];
+#pragma unroll
+            for (int j = 0; j < EC; j++) {
+                const int kk = (k0 + j) <= N ? k0 + j : N;
+                zs[j] = tbase[(size_t)kk * KS + rec_off<RS, QM>(R::Z)];
+                vs[j] = *entry(k0 + j);
+            }
+#pragma unroll
+            for (int j = 0; j < EC; j++) {
+                const int k = k0 + j;
+                const float nv = (is_x && k == 0) ? x0_lane : vs[j] + zs[j];
+                if (k <= N) *entry(k) = nv;
+            }
+        }
+        if (a.xtraj || a.utraj) {
+            __threadfence_block();
+            for (int k = 0; k <= N; k++) {
+                if (q == 0 && is_x && a.xtraj) a.xtraj[((size_t)k * NX + xi) * Bn + inst] = XB(k, xi);
+                if (q == 0 && is_u && k < N && a.utraj) a.utraj[((size_t)k * NU + r) * Bn + inst] = UBAR(k, r);
+            }
+        }
+    }
+    __threadfence_block();
+    if (lane == 0) {
+        float u0[NU];
+#pragma unroll
+        for (int j = 0; j < NU; j++) {
+            u0[j] = UBAR(0, j);
+            if (a.u0) a.u0[(size_t)j * Bn + inst] = u0[j];
+        }
+        if (a.x1) {
+#pragma unroll
+            for (int j = 0; j < NX; j++) a.x1[(size_t)j * Bn + inst] = XB(1, j);
+        }
+        if (a.status) a.status[inst] = status;
+        if (a.qp_iter) a.qp_iter[inst] = it_done;
+        if (a.iter_key) a.iter_key[inst] = it_done;
+        if (a.warm) a.warm[inst] = (P.warm && status == 0 && it_done < P.iter_max && it_done <= P.warm_iter_max) ? 1 : 0;
+        if (a.qp_res) {
+#pragma unroll
+            for (int j = 0; j < 3; j++) a.qp_res[(size_t)j * Bn + inst] = exit_res[j];
+        }
+        if (mode == kModeRun && status == 0) {
+            float rr[M::NBX], cmd[3];
+#pragma unroll
+            for (int i = 0; i < M::NBX; i++) {
+                rr[i] = x0[M::idxbx(i)] + u0[i] * P.dt_ctrl;
+                a.carried[(size_t)i * S + inst] = rr[i];
+            }
+            M::inverse_kin(rr, P, cmd);
+            if (a.cmd) {
+#pragma unroll
+                for (int j = 0; j < 3; j++) a.cmd[(size_t)j * Bn + inst] = cmd[j];
+            }
+        } else if (mode == kModeRun && a.cmd) {
+#pragma unroll
+            for (int j = 0; j < 3; j++) a.cmd[(size_t)j * Bn + inst] = 0.0f;
+        }
+    }
+#undef XB
+#undef UBAR
+}
+
+}  // namespace
+
+template <class M>
+size_t rowpar_lds_bytes(int N, int mode)
+{
+    return (size_t)(N + 1) * 16 * (5 + M::NGV) * sizeof(float) + (mode == kModeRun ? (size_t)(N + 1) * 3 * sizeof(float) : 0);
+}
+
+template <class M>
+hipError_t launch_sqp_rti_rowpar(const KParams& P, const KArgs& a, int mode, hipStream_t stream)
+{
+    if (a.B <= 0) return hipSuccess;
+    const size_t lds = rowpar_lds_bytes<M>(P.N, mode);
+    if (lds > 65536 || P.ipm != 1 || a.segs) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((k_sqp_rti_rowpar<M>), dim3(a.B), dim3(64), lds, stream, P, a, mode);
+    return hipGetLastError();
+}
+
+#define INST(M)                                                                                                      \
+    template hipError_t launch_sqp_rti_rowpar<M>(const KParams&, const KArgs&, int, hipStream_t);                   \
+    template size_t rowpar_lds_bytes<M>(int, int);
+INST(Diff2)
+INST(Omni4)
+INST(Tric3)
+#undef INST
+
+}  // namespace nmpc

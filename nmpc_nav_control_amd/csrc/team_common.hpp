@@ -8,6 +8,55 @@
 #include "team_dpp.hpp"
 
 namespace nmpc {
+
+#ifndef NMPC_DZ_IN_RECORD
+constexpr bool kDzPlane = true;
+#else
+constexpr bool kDzPlane = false;  // A/B: the round-2 layout, DZ a field of the lane record
+#endif
+
+template <class M, bool SD = false>
+struct TeamRec {
+    static constexpr int NX = M::NX, NU = M::NU, NV = NX + NU, NGV = M::NGV;
+    // Mehrotra field order: P1's write-only outputs first (LR, LM, RU: P1 never loads them, so no record load is
+    // issued into registers P1 overwrites), then the bound quad, the iterate and the rest the light sweeps read
+    // (prefix [0, NL)), then the P1-only inputs (DZ, GR). P1 loads [P1L0, P1L1) and stores [0, P1S1).
+    // Same-box A/B against the round-1 order (P1 rewrote a prefix it also loaded, and the compiler reused the
+    // dead lanes of those loads, waiting on them): kernel ms diff N=40 B=4096 1.430 -> 1.404, omni4 1.664 ->
+    // 1.655 (profiles/r02/ab/abwb.txt).
+    // Single-direction order (SD, NU = 2): no sweep reads RU (the corrector's u residual) or DZA (the affine
+    // direction), so they move to the end: P1 stores 2 quads instead of 3 and the forward sweep loads 3 quads
+    // instead of 3.5 (same-box A/B, single-direction rule: diff N=40 B=4096 3.43 -> 3.53 M it/s, B=1024 +1.2 %,
+    // tric even; the NU = 4 analogue cost omni4 1.8 %, so omni4 keeps the Mehrotra order; profiles/r02/ab/layout.txt)
+    static constexpr bool L2 = SD && NU == 2;
+    static constexpr int LR = 0, LM = 1;  // Luu^-1 rhs, row v of the input columns
+    static constexpr int Z = L2 ? 3 : ((NU == 2) ? 8 : 6);          // QP iterate
+    static constexpr int TL = (NU == 2) ? 4 : 8;                    // bound quad TL TU LL LU
+    static constexpr int TU = TL + 1, LL = TL + 2, LU = TL + 3;
+    static constexpr int LB = L2 ? 8 : ((NU == 2) ? 9 : 12), UB = LB + 1;  // bounds relative to the SQP iterate
+    static constexpr int GV = L2 ? 10 : ((NU == 2) ? 12 : 14);      // NGV varying rows of column v of [B A]
+    static constexpr int NL = GV + NGV;                             // prefix read by the light sweeps
+    // combined direction, cost gradient (P1 only). DZ plane (default): the forward sweep writes one float per lane
+    // and stage; in the lane record that dirtied a whole 32-byte sector per lane (8x the bytes), so DZ lives in a
+    // dense plane [robot][stage][16 lanes] (64 B per team and stage, 2 sectors for 9 lanes) and its register slot
+    // sits past the record's stored fields
+    static constexpr int GR = kDzPlane ? NL : NL + 1;
+    static constexpr int RU = L2 ? GR + 1 : LM + NU;                // u residual (corrector sweeps)
+    static constexpr int DZA = L2 ? GR + 2 : Z + 1 + ((NU == 2) ? 2 : 0);  // affine direction
+    static constexpr int DZ = kDzPlane ? (L2 ? GR + 3 : GR + 1) : NL;
+    static constexpr int P1L0 = L2 ? Z : ((NU == 2) ? TL : Z), P1L1 = GR + 1;  // P1 loads
+    static constexpr int P1S1 = L2 ? 8 : 12;                        // P1 stores [0, P1S1)
+    static_assert(NU == 2 || NU == 4, "layouts for NU = 2 and 4");
+    static_assert(L2 || (RU < ((NU == 2) ? TL : Z) && DZA < P1S1), "P1 store block holds RU and DZA");
+    static_assert(LU < P1S1 && Z < P1S1 && LM + NU <= P1S1, "P1 store block");
+    static constexpr int NF = NL, NB = NL;
+    static constexpr int MAXF = (GR > RU ? GR : RU) > (DZA > DZ ? DZA : DZ) ? (GR > RU ? GR : RU) : (DZA > DZ ? DZA : DZ);
+    static constexpr int RS = (MAXF + 1 + 3) / 4 * 4;  // dwordx4 records (and the register image of one)
+    static constexpr int NQ = RS / 4;
+    static_assert(NV <= 16, "a team holds at most 16 variables");
+    static_assert(TL % 4 == 0, "bound quad aligned");
+};
+
 namespace {
 
 constexpr float kBreakdownMuT = 1e-6f;

@@ -27,13 +27,21 @@ def t(a, dtype=torch.float32):
     return torch.from_numpy(np.ascontiguousarray(a)).to(device=DEV, dtype=dtype)
 
 
+def handle(monkeypatch, model, N, cap, **env):
+    """A handle created under the launch-choice overrides `env` (read at creation)."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, str(v))
+    h = BatchSolver(model, N, cap, params=default_params(model, N))
+    for k in env:
+        monkeypatch.delenv(k)
+    return h
+
+
 def pair(monkeypatch, model, N, cap):
-    """(split, unsplit) handles of the same model and horizon."""
-    a = BatchSolver(model, N, cap, params=default_params(model, N))
-    monkeypatch.setenv("NMPC_AMD_SPLIT_MAX", "0")
-    b = BatchSolver(model, N, cap, params=default_params(model, N))
-    monkeypatch.delenv("NMPC_AMD_SPLIT_MAX")
-    return a, b
+    """(split, unsplit) team-kernel handles of the same model and horizon (the row-parallel kernel, which takes
+    these batch sizes by default, switched off)."""
+    return (handle(monkeypatch, model, N, cap, NMPC_AMD_ROWPAR_MAX=0),
+            handle(monkeypatch, model, N, cap, NMPC_AMD_ROWPAR_MAX=0, NMPC_AMD_SPLIT_MAX=0))
 
 
 def close(u, v):
@@ -110,3 +118,75 @@ def test_split_run_and_run_path_equal_unsplit(built, monkeypatch, holo):
             assert close(a["u0"], b["u0"]) <= TOL, (tick, kind)
             assert close(a["cmd"], b["cmd"]) <= TOL, (tick, kind)
         assert torch.equal(res["path"][0]["traj"], traj) and torch.equal(res["path"][1]["traj"], traj), tick
+
+
+# ---- the row-parallel kernel (k_sqp_rti_rowpar, the default for batches up to 1024 robots) against the team
+# kernel: the same IPM and stopping rule, with sums over stages in another order (4 rows), so the two agree to
+# fp32 rounding amplified by the IPM's exit (an iteration more or less); both are checked against the oracle by
+# the parity tests
+TOL_RP = 3e-4
+
+
+@pytest.mark.parametrize("model", ["diff", "omni4", "tric"])
+@pytest.mark.parametrize("N,B", [(80, 13), (40, 64), (2, 5), (1, 3)])
+def test_rowpar_solve_matches_team(built, monkeypatch, model, N, B):
+    o, rec = oracle_closed_loop(model, N, B, 2)
+    nx, nu = o.nx, o.nu
+    rp = handle(monkeypatch, model, N, 64)
+    tm = handle(monkeypatch, model, N, 64, NMPC_AMD_ROWPAR_MAX=0, NMPC_AMD_SPLIT_MAX=0)
+    x0 = t(np.stack([r[0] for r in rec]).T)
+    yref = t(np.stack([r[1] for r in rec]).transpose(1, 2, 0))
+    We = t(np.stack([r[2] for r in rec]).T)
+    for s in (rp, tm):
+        xv, uv, _ = s.state()
+        X, U = xv.to_tensor(), uv.to_tensor()
+        X[:, :B] = t(np.stack([r[3] for r in rec]).reshape(B, -1).T)
+        U[:, :B] = t(np.stack([r[4] for r in rec]).reshape(B, -1).T)
+        xv.copy_from(X)
+        uv.copy_from(U)
+    for tick in range(3):
+        outs = []
+        for s in (rp, tm):
+            o_ = dict(u0=torch.zeros(nu, B, device=DEV), xtraj=torch.zeros((N + 1) * nx, B, device=DEV),
+                      status=torch.full((B,), -7, dtype=torch.int32, device=DEV),
+                      qp_iter=torch.zeros(B, dtype=torch.int32, device=DEV))
+            s.solve(x0, yref, We=We, u0=o_["u0"], xtraj=o_["xtraj"], status=o_["status"], qp_iter=o_["qp_iter"])
+            outs.append(o_)
+        torch.cuda.synchronize()
+        assert (outs[0]["status"] == 0).all() and (outs[1]["status"] == 0).all(), tick
+        assert close(outs[0]["u0"], outs[1]["u0"]) <= TOL_RP, (tick, close(outs[0]["u0"], outs[1]["u0"]))
+        assert close(outs[0]["xtraj"], outs[1]["xtraj"]) <= TOL_RP, tick
+        assert (outs[0]["qp_iter"] - outs[1]["qp_iter"]).abs().max() <= 3, tick
+
+
+def test_rowpar_run_matches_team(built, monkeypatch):
+    """run mode (pose / velocity packing, reference unwrap and padding with traj_len shorter than the horizon, the
+    diff terminal-weight hack, carry and command) over warm-started ticks: row-parallel against team kernel."""
+    N, B = 40, 24
+    rng = np.random.default_rng(11)
+    segs, nseg, nu = random_paths(B, seed=11, max_segs=4, reverse_frac=0.2)
+    nu[:] = rng.uniform(0, 0.3, B)
+    exp_traj, _ = path_discretize(segs, nseg, nu, 1 / 40, N + 1, False)
+    pose = exp_traj[:, 0, :].copy()
+    pose[:, :2] += rng.uniform(-0.1, 0.1, (B, 2))
+    vel = np.zeros((B, 3))
+    vel[:, 0] = rng.uniform(0.0, 0.5, B)
+    P, V = t(pose.T), t(vel.T)
+    S, NS, NU = t(segs, torch.float64), t(nseg, torch.int32), t(nu, torch.float64)
+    tlen = t(np.where(np.arange(B) % 3 == 0, 1, np.where(np.arange(B) % 3 == 1, N // 2, N + 1)), torch.int32)
+    hs = (handle(monkeypatch, "diff", N, B), handle(monkeypatch, "diff", N, B, NMPC_AMD_ROWPAR_MAX=0))
+    for tick in range(4):
+        traj = discretize(S, NS, NU, 1 / 40, N + 1, False)
+        res = []
+        for h in hs:
+            o_ = dict(u0=torch.zeros(2, B, device=DEV), cmd=torch.zeros(3, B, device=DEV),
+                      status=torch.full((B,), -7, dtype=torch.int32, device=DEV))
+            h.run(P, V, traj, traj_len=tlen, cmd=o_["cmd"], u0=o_["u0"], status=o_["status"])
+            res.append(o_)
+        torch.cuda.synchronize()
+        a, b = res
+        assert (a["status"] == 0).all() and (b["status"] == 0).all(), tick
+        assert close(a["u0"], b["u0"]) <= TOL_RP, (tick, close(a["u0"], b["u0"]))
+        assert close(a["cmd"], b["cmd"]) <= TOL_RP, tick
+        ca, cb = hs[0].state()[2].to_tensor(), hs[1].state()[2].to_tensor()
+        assert close(ca[:, :B], cb[:, :B]) <= TOL_RP, tick
