@@ -128,11 +128,11 @@ def test_follow_path_tick_on_device_matches_oracle(built):
 
 
 @pytest.mark.parametrize("holo", [False, True])
-def test_run_path_one_launch_equals_two_launches(built, holo):
+def test_run_path_one_launch_equals_two_launches(built, monkeypatch, holo):
     """nmpc_batch_run_path (getNextNPoses in the solve kernel: a path-following tick in one launch,
     NMPCNavControlROS.cpp:666-668 -> :713) against nmpc_path_discretize followed by nmpc_batch_run: the poses
     are bit-identical (both fp64 marches without contraction, path_march.hpp) and so is every output of the
-    solve; over three ticks of warm-started solves."""
+    solve; over three ticks of warm-started solves (team kernel both ways)."""
     N, B = 40, 1000
     rng = np.random.default_rng(5)
     segs, nseg, nu = random_paths(B, seed=5, max_segs=4, reverse_frac=0.2)
@@ -146,7 +146,10 @@ def test_run_path_one_launch_equals_two_launches(built, holo):
     d = lambda a, dt=torch.float32: torch.from_numpy(np.ascontiguousarray(a)).to(DEV, dt)  # noqa: E731
     P, V = d(pose.T), d(vel.T)
     S, NS, NU = d(segs, torch.float64), d(nseg, torch.int32), d(nu, torch.float64)
+    # the same (team) kernel both ways: run_path always runs it, run would take the row-parallel kernel at this size
+    monkeypatch.setenv("NMPC_AMD_ROWPAR_MAX", "0")
     two, one = BatchSolver("diff", N, B, device=DEV), BatchSolver("diff", N, B, device=DEV)
+    monkeypatch.delenv("NMPC_AMD_ROWPAR_MAX")
     out = {k: [torch.zeros(r, B, device=DEV) for _ in range(2)] for k, r in (("u0", 2), ("cmd", 3))}
     st = [torch.zeros(B, dtype=torch.int32, device=DEV) for _ in range(2)]
     it = [torch.zeros(B, dtype=torch.int32, device=DEV) for _ in range(2)]
