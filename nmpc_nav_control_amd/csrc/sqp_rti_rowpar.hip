@@ -38,6 +38,23 @@ struct RowRec {
     static_assert(LM + NU <= Z && Z < TL, "LR / LM below Z");
 };
 
+#ifdef NMPC_STAMPS
+// diagnostic build only: s_memtime after each phase, robots 0..255, lane 0: [0] start, [1] P0a, [2] P0b, then per
+// IPM iteration it: [3 + 4 it + 0..3] after phases A, B, C, D
+constexpr int kRpIts = 64;
+__device__ unsigned long long g_rp_stamps[256][3 + 4 * kRpIts];
+#define RP_STAMP(slot)                                                                                           \
+    do {                                                                                                         \
+        if (lane == 0 && inst < 256 && (slot) < 3 + 4 * kRpIts) g_rp_stamps[inst][(slot)] = __builtin_amdgcn_s_memtime(); \
+    } while (0)
+extern "C" int nmpc_debug_stamps_rowpar(unsigned long long* host)
+{
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_rp_stamps), sizeof(g_rp_stamps), 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -2;
+}
+#else
+#define RP_STAMP(slot) ((void)0)
+#endif
+
 namespace {
 
 template <int F0, int F1, int RS, bool QM>
@@ -102,6 +119,7 @@ __global__ __launch_bounds__(64, 1) void k_sqp_rti_rowpar(KParams P, KArgs a, in
     float* const tdummy = rbase + (size_t)N * KS + 15 * rec_lane<RS, QM>();  // nobody reads it
     float* const dzbase = a.scratch + (size_t)a.stride * (N + 1) * KS + (size_t)inst * (N + 1) * 16 + r;
     const bool warm = P.warm && a.warm && a.warm[inst] && !(a.reset && a.reset[inst]);
+    RP_STAMP(0);
 
 #define XB(k, j) a.xbar[((size_t)(k) * NX + (j)) * S + inst]
 #define UBAR(k, j) a.ubar[((size_t)(k) * NU + (j)) * S + inst]
@@ -232,6 +250,7 @@ __global__ __launch_bounds__(64, 1) void k_sqp_rti_rowpar(KParams P, KArgs a, in
         });
     }
     __syncthreads();  // one wave per block: the stage inputs of every row are in LDS
+    RP_STAMP(1);
 
     // ---- P0b: the serial pass (every row identically): reference unwrap / pad, gradient, bounds, slacks,
     // multipliers, the record, and the dynamics-feasible initial iterate dx_{k+1} = A dx_k + b_k --------------
@@ -326,6 +345,7 @@ __global__ __launch_bounds__(64, 1) void k_sqp_rti_rowpar(KParams P, KArgs a, in
         }
     }
     __threadfence_block();  // the records before the stage-parallel phase A reads them on other rows
+    RP_STAMP(2);
 
     double onehot[NV];
 #pragma unroll
@@ -440,6 +460,7 @@ __global__ __launch_bounds__(64, 1) void k_sqp_rti_rowpar(KParams P, KArgs a, in
         sc0 = wave_max_rows(row_max16(sc0));
         nanf_ = wave_max_rows(row_max16(nanf_));
         const float mu = sum_c * inv_m2;
+        RP_STAMP(3 + 4 * it);
 
         // phase B (serial, N -> 0): adjoint, fp64 classic Riccati step, rhs / forward substitution
         double Lrow[NV];
@@ -514,6 +535,7 @@ __global__ __launch_bounds__(64, 1) void k_sqp_rti_rowpar(KParams P, KArgs a, in
                 piv = pi_new;
             });
         }
+        RP_STAMP(4 + 4 * it);
         res_stat = row_max16(lv ? res_stat : 0.0f);
         const float stat_scale = fmaxf(sc0, row_max16(lv ? cpi_max : 0.0f));
         nanf_ = row_max16(nanf_);
@@ -590,6 +612,7 @@ __global__ __launch_bounds__(64, 1) void k_sqp_rti_rowpar(KParams P, KArgs a, in
             });
         }
         __threadfence_block();
+        RP_STAMP(5 + 4 * it);
 
         // phase D (stage-parallel): bound directions, fraction-to-boundary step bound, complementarity polynomial
         float amax = 1e30f, s1 = 0.0f, s2 = 0.0f;
@@ -623,6 +646,7 @@ __global__ __launch_bounds__(64, 1) void k_sqp_rti_rowpar(KParams P, KArgs a, in
         const float mu_next = fmaxf((sum_c + alpha * s1 + alpha * alpha * s2) * inv_m2, 0.0f);
         const float om = 1.0f - alpha;
         tg_rhs = fminf(fmaxf(om * om, P.sd_lo), P.sd_hi) * mu_next;
+        RP_STAMP(6 + 4 * it);
     }
 
     // ---- full SQP step + outputs (row 0 stores; the other rows' entries point at the dummy record) -------------

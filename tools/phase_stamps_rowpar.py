@@ -1,0 +1,52 @@
+"""Per-phase cycles of the row-parallel kernel (diag build, NMPC_STAMPS): P0a / P0b and per IPM iteration the
+phases A (stage-parallel update), B (serial Riccati), C (serial forward), D (stage-parallel step).
+usage (GPU box): python tools/phase_stamps_rowpar.py [model] [B] [N] [ticks]"""
+import ctypes
+import os
+import sys
+
+import numpy as np
+import torch
+
+root = os.environ.get("GRAFT_REPO_ROOT", "/root/repo")
+os.environ["NMPC_AMD_LIB"] = os.environ.get("STAMPS_LIB") or os.path.join(root, "nmpc_nav_control_amd/lib/diag/libnmpc_amd.so")
+sys.path.insert(0, root)
+from nmpc_nav_control_amd._lib import lib  # noqa: E402
+from nmpc_nav_control_amd.fleet import Fleet  # noqa: E402
+from nmpc_nav_control_amd.scenario import DEFAULT_SEED  # noqa: E402
+
+model = sys.argv[1] if len(sys.argv) > 1 else "diff"
+B = int(sys.argv[2]) if len(sys.argv) > 2 else 4
+N = int(sys.argv[3]) if len(sys.argv) > 3 else 80
+T = int(sys.argv[4]) if len(sys.argv) > 4 else 30
+f = Fleet(model, B, N, DEFAULT_SEED + 1, torch.device("cuda", 0))
+for _ in range(T):
+    f.tick()
+torch.cuda.synchronize()
+ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+ev0.record()
+f.solve()
+ev1.record()
+torch.cuda.synchronize()
+W = 3 + 4 * 64
+buf = (ctypes.c_ulonglong * (256 * W))()
+L = lib()
+L.nmpc_debug_stamps_rowpar.argtypes = [ctypes.c_void_p]
+assert L.nmpc_debug_stamps_rowpar(buf) == 0
+st = np.frombuffer(buf, dtype=np.uint64).reshape(256, W).astype(np.int64)[:B]
+it = f.qp_iter.cpu().numpy()
+print("kernel ms", ev0.elapsed_time(ev1), "qp_iter", it.tolist())
+ph = {"A": [], "B": [], "C": [], "D": []}
+for b in range(B):
+    for i in range(int(it[b]) + 1):
+        base = 3 + 4 * i
+        prev = st[b, 2] if i == 0 else st[b, base - 1]
+        ph["A"].append(st[b, base] - prev)
+        ph["B"].append(st[b, base + 1] - st[b, base])
+        if i < it[b]:
+            ph["C"].append(st[b, base + 2] - st[b, base + 1])
+            ph["D"].append(st[b, base + 3] - st[b, base + 2])
+print("P0a cycles", (st[:, 1] - st[:, 0]).tolist(), "P0b", (st[:, 2] - st[:, 1]).tolist())
+for k, v in ph.items():
+    v = np.array(v)
+    print(k, "mean %.0f p50 %.0f max %.0f n %d per stage %.0f" % (v.mean(), np.median(v), v.max(), len(v), v.mean() / (N + 1)))
