@@ -29,7 +29,7 @@ struct nmpc_batch {
     int split_max = 256;         // team-kernel launches of at most this many robots run one block per robot (split)
     // launches of at most this many robots (single-direction IPM, not run_path) run k_sqp_rti_rowpar: one wave
     // per robot with its stage-independent work spread over the wave's 4 rows (latency)
-    int rowpar_max = 1024;
+    int rowpar_max = 256;        // (four waves per robot up to 256 robots; one wave per robot above, A/B only)
     int* iter_key = nullptr;     // [capacity] last executed IPM iterations per robot (written by the team kernel)
     int* order = nullptr;        // [capacity] team slot -> robot
     unsigned char* warm = nullptr;  // [capacity] the robot's last solve succeeded: its scratch records hold its
@@ -136,6 +136,7 @@ hipError_t schedule(nmpc_batch* b, KArgs& a, int mode, hipStream_t s)
     case NMPC_MODEL_OMNI4AMR: a.rowpar = rowpar_ok<Omni4>(b, a, mode); break;
     default: a.rowpar = rowpar_ok<Tric3>(b, a, mode); break;
     }
+    if (a.rowpar) a.rowpar = (a.B <= 256) ? 4 : 1;  // waves per robot
     if (a.rowpar) return hipSuccess;  // one robot per wave: nothing to place
     a.dense = ((a.B + 3) / 4 > b->n_simd) ? 1 : 0;  // 4 teams per wave
     // small batches leave most of the chip idle: one wave per robot, whose spare rows integrate P0's stages

@@ -56,7 +56,7 @@ struct KArgs {
     unsigned char* warm;  // [stride] resident: 1 if the robot's last solve succeeded (its records hold its
                           // multipliers), or nullptr (cold start, nothing written)
     int dense;      // the launch has more waves than the device has SIMDs (selects the team kernel variant)
-    int rowpar;     // launched as k_sqp_rti_rowpar (one wave per robot)
+    int rowpar;     // 0: team kernel; W > 0: k_sqp_rti_rowpar with W waves per robot
     int split;      // one 256-lane block per robot: P0's integrations spread over its 16 rows (4 waves, stage k on
                     // row k mod 16, joined by a block barrier); small batches
 };

@@ -45,7 +45,7 @@ constexpr int kRpIts = 64;
 __device__ unsigned long long g_rp_stamps[256][3 + 4 * kRpIts];
 #define RP_STAMP(slot)                                                                                           \
     do {                                                                                                         \
-        if (lane == 0 && inst < 256 && (slot) < 3 + 4 * kRpIts) g_rp_stamps[inst][(slot)] = __builtin_amdgcn_s_memtime(); \
+        if (tid == 0 && inst < 256 && (slot) < 3 + 4 * kRpIts) g_rp_stamps[inst][(slot)] = __builtin_amdgcn_s_memtime(); \
     } while (0)
 extern "C" int nmpc_debug_stamps_rowpar(unsigned long long* host)
 {
@@ -80,18 +80,23 @@ __device__ __forceinline__ float wave_min_rows(float v)
     return fminf(v, __shfl_xor(v, 32));
 }
 
-template <class M>
-__global__ __launch_bounds__(64, 1) void k_sqp_rti_rowpar(KParams P, KArgs a, int mode)
+// W waves per robot (one per SIMD): the stage-parallel phases run on all 4 W rows; every wave runs the serial
+// phases (identically), and only wave 0's row 0 stores their results (the other lanes store into per-lane dummy
+// records: no two lanes of an instruction write one address)
+template <class M, int W>
+__global__ __launch_bounds__(64 * W, 1) void k_sqp_rti_rowpar(KParams P, KArgs a, int mode)
 {
     using R = RowRec<M>;
     constexpr int NX = M::NX, NU = M::NU, NV = R::NV, NGV = R::NGV, RS = R::RS;
     constexpr bool QM = rec_quad_major<NV>();
-    constexpr int ROWS = 4;
+    constexpr int ROWS = 4 * W;
     const int inst = (int)blockIdx.x;
     if (inst >= a.B) return;
-    const int lane = (int)threadIdx.x;
-    const int q = lane >> 4;  // row: stage-parallel phases take stages q, q + 4, ...
-    const int r = lane & 15;  // slot: variable r of the stage (as a team lane)
+    const int tid = (int)threadIdx.x;
+    const int wave = tid >> 6;
+    const int q = tid >> 4;  // row of the block: stage-parallel phases take stages q, q + ROWS, ...
+    const int r = tid & 15;  // slot: variable r of the stage (as a team lane)
+    const bool wr = tid < 16;  // the lanes that store the serial phases' results
     const int N = P.N;
     const size_t S = (size_t)a.stride;
     const size_t Bn = (size_t)a.B;
@@ -116,8 +121,9 @@ __global__ __launch_bounds__(64, 1) void k_sqp_rti_rowpar(KParams P, KArgs a, in
     float* const rbase = a.scratch + (size_t)inst * (N + 1) * KS;
     float* const tbase = rbase + (lv ? r : 0) * rec_lane<RS, QM>();   // idle slots read slot 0
     float* const tbase_own = rbase + r * rec_lane<RS, QM>();          // every lane's own slot
-    float* const tdummy = rbase + (size_t)N * KS + 15 * rec_lane<RS, QM>();  // nobody reads it
     float* const dzbase = a.scratch + (size_t)a.stride * (N + 1) * KS + (size_t)inst * (N + 1) * 16 + r;
+    // this lane's dummy record (nobody reads it): the target of stores a lane issues without a result to store
+    float* const wdummy = a.scratch + (size_t)a.stride * (N + 1) * 16 * (RS + 1) + ((size_t)(inst & 255) * 256 + tid) * RS;
     const bool warm = P.warm && a.warm && a.warm[inst] && !(a.reset && a.reset[inst]);
     RP_STAMP(0);
 
@@ -126,9 +132,9 @@ __global__ __launch_bounds__(64, 1) void k_sqp_rti_rowpar(KParams P, KArgs a, in
 
     // ---- reset ({name}_acados_reset: zero iterate) ----------------------------------------------------------
     if (a.reset && a.reset[inst]) {
-        for (int e = lane; e < (N + 1) * NX; e += 64) XB(e / NX, e % NX) = 0.0f;
-        for (int e = lane; e < N * NU; e += 64) UBAR(e / NU, e % NU) = 0.0f;
-        __threadfence_block();
+        for (int e = tid; e < (N + 1) * NX; e += 64 * W) XB(e / NX, e % NX) = 0.0f;
+        for (int e = tid; e < N * NU; e += 64 * W) UBAR(e / NU, e % NU) = 0.0f;
+        __syncthreads();
     }
 
     // ---- x0 -----------------------------------------------------------------------------------------------
@@ -163,6 +169,7 @@ __global__ __launch_bounds__(64, 1) void k_sqp_rti_rowpar(KParams P, KArgs a, in
     extern __shared__ float s_row[];
     float* const s_stg = s_row;
     float* const my_traj = s_row + (size_t)(N + 1) * SF * 16;
+    float* const s_red = my_traj + (size_t)(N + 1) * 3;  // [W][8] per-wave partial reductions
     const int len = (mode == kModeRun) ? (a.traj_len ? a.traj_len[inst] : N + 1) : 0;
     {
         struct In {
@@ -249,7 +256,7 @@ __global__ __launch_bounds__(64, 1) void k_sqp_rti_rowpar(KParams P, KArgs a, in
             grow[v] = sv;
         });
     }
-    __syncthreads();  // one wave per block: the stage inputs of every row are in LDS
+    __syncthreads();  // the stage inputs of every row are in LDS
     RP_STAMP(1);
 
     // ---- P0b: the serial pass (every row identically): reference unwrap / pad, gradient, bounds, slacks,
@@ -329,8 +336,8 @@ __global__ __launch_bounds__(64, 1) void k_sqp_rti_rowpar(KParams P, KArgs a, in
             }
 #pragma unroll
             for (int i = 0; i < NGV; i++) rec[R::GV + i] = (k < N && lv) ? cur.g[i] : 0.0f;
-            rec_store<RS, QM>(tbase_own + (size_t)k * KS, rec);  // idle lanes: their own unused slot
-            dzbase[(size_t)k * 16] = 0.0f;
+            rec_store<RS, QM>(wr ? tbase_own + (size_t)k * KS : wdummy, rec);  // idle slots: their own unused one
+            *(wr ? dzbase + (size_t)k * 16 : wdummy) = 0.0f;
             if (k < N) {
                 const float dzd = is_x ? dx : 0.0f;
                 float nx_ = dot_v<NX, NU>(0.0f, dzd, grow);
@@ -344,7 +351,7 @@ __global__ __launch_bounds__(64, 1) void k_sqp_rti_rowpar(KParams P, KArgs a, in
             cur = nxt;
         }
     }
-    __threadfence_block();  // the records before the stage-parallel phase A reads them on other rows
+    __syncthreads();  // the records before the stage-parallel phase A reads them on other rows
     RP_STAMP(2);
 
     double onehot[NV];
@@ -389,6 +396,26 @@ __global__ __launch_bounds__(64, 1) void k_sqp_rti_rowpar(KParams P, KArgs a, in
             load(k_2, ra);
             body(k + dir, rb);
             if (k + dir == k1) break;
+        }
+    };
+
+    // block reductions of per-wave partials (W > 1): every wave combines the W partials in the same order, so every
+    // wave holds identical values and takes identical decisions; the barrier is also the phase boundary
+    auto block_combine = [&](float (&v)[6], const int (&op)[6], int n) {
+        if constexpr (W == 1) {
+            __syncthreads();
+        } else {
+            if ((tid & 63) == 0)
+                for (int i = 0; i < n; i++) s_red[wave * 8 + i] = v[i];
+            __syncthreads();
+            for (int i = 0; i < n; i++) {
+                float acc = s_red[i];
+                for (int w = 1; w < W; w++) {
+                    const float x = s_red[w * 8 + i];
+                    acc = (op[i] == 0) ? acc + x : ((op[i] == 1) ? fmaxf(acc, x) : fminf(acc, x));
+                }
+                v[i] = acc;
+            }
         }
     };
 
@@ -448,17 +475,23 @@ __global__ __launch_bounds__(64, 1) void k_sqp_rti_rowpar(KParams P, KArgs a, in
             rc[R::SIG] = sig;
             rc[R::C0] = c0;
             rc[R::GH] = valid ? gh : 0.0f;
-            float* const pk = (lv && kv) ? tbase + (size_t)k * KS : tdummy;
+            float* const pk = (lv && kv) ? tbase + (size_t)k * KS : wdummy;
             rec_store_range<R::Z, R::LU + 1, RS, QM>(pk, rc);
             rec_store_range<R::SIG, R::GH + 1, RS, QM>(pk, rc);
         }
-        __threadfence_block();
-        sum_c = wave_sum_rows(row_sum16(lv ? sum_c : 0.0f));
-        max_c = wave_max_rows(row_max16(lv ? max_c : 0.0f));
-        lam_max = wave_max_rows(row_max16(lv ? lam_max : 0.0f));
-        res_ineq = wave_max_rows(row_max16(lv ? res_ineq : 0.0f));
-        sc0 = wave_max_rows(row_max16(sc0));
-        nanf_ = wave_max_rows(row_max16(nanf_));
+        {
+            float v[6] = {wave_sum_rows(row_sum16(lv ? sum_c : 0.0f)), wave_max_rows(row_max16(lv ? max_c : 0.0f)),
+                          wave_max_rows(row_max16(lv ? lam_max : 0.0f)), wave_max_rows(row_max16(lv ? res_ineq : 0.0f)),
+                          wave_max_rows(row_max16(sc0)), wave_max_rows(row_max16(nanf_))};
+            const int op[6] = {0, 1, 1, 1, 1, 1};
+            block_combine(v, op, 6);
+            sum_c = v[0];
+            max_c = v[1];
+            lam_max = v[2];
+            res_ineq = v[3];
+            sc0 = v[4];
+            nanf_ = v[5];
+        }
         const float mu = sum_c * inv_m2;
         RP_STAMP(3 + 4 * it);
 
@@ -530,7 +563,7 @@ __global__ __launch_bounds__(64, 1) void k_sqp_rti_rowpar(KParams P, KArgs a, in
 #pragma unroll
                     for (int j = 0; j < NV; j++) Lrow[j] = Lr[j];
                     // LR, LM (every row stores the same values; idle slots store into the dummy record)
-                    rec_store_range<R::LR, R::LM + NU, RS, QM>(lv ? tbase + (size_t)k * KS : tdummy, rc);
+                    rec_store_range<R::LR, R::LM + NU, RS, QM>((wr && lv) ? tbase + (size_t)k * KS : wdummy, rc);
                 }
                 piv = pi_new;
             });
@@ -568,7 +601,7 @@ __global__ __launch_bounds__(64, 1) void k_sqp_rti_rowpar(KParams P, KArgs a, in
             it_done = it;
             break;
         }
-        __threadfence_block();
+        __syncthreads();  // LR / LM of every stage
 
         // phase C (serial, 0 -> N): the direction's input part from the stored factor, its state part from the
         // dynamics; every row the same (identical DZ stores)
@@ -607,11 +640,11 @@ __global__ __launch_bounds__(64, 1) void k_sqp_rti_rowpar(KParams P, KArgs a, in
                     if (r == qq) dz = du_all[qq];
                 dz = is_x ? ((k >= 1) ? dxs : 0.0f) : dz;
                 dz = valid ? dz : 0.0f;
-                dzbase[(size_t)k * 16] = dz;  // every lane its own entry (idle lanes: 0)
+                *(wr ? dzbase + (size_t)k * 16 : wdummy) = dz;  // every slot its own entry (idle slots: 0)
                 if (k < N) dxs = dyn(rc, dz);
             });
         }
-        __threadfence_block();
+        __syncthreads();  // the directions of every stage
         RP_STAMP(5 + 4 * it);
 
         // phase D (stage-parallel): bound directions, fraction-to-boundary step bound, complementarity polynomial
@@ -639,9 +672,15 @@ __global__ __launch_bounds__(64, 1) void k_sqp_rti_rowpar(KParams P, KArgs a, in
             s1 += bnd ? ll * d.dtl + tl * d.dll + lu * d.dtu + tu * d.dlu : 0.0f;
             s2 += bnd ? d.dll * d.dtl + d.dlu * d.dtu : 0.0f;
         }
-        amax = wave_min_rows(row_min16(lv ? amax : 1e30f));
-        s1 = wave_sum_rows(row_sum16(lv ? s1 : 0.0f));
-        s2 = wave_sum_rows(row_sum16(lv ? s2 : 0.0f));
+        {
+            float v[6] = {wave_min_rows(row_min16(lv ? amax : 1e30f)), wave_sum_rows(row_sum16(lv ? s1 : 0.0f)),
+                          wave_sum_rows(row_sum16(lv ? s2 : 0.0f)), 0.0f, 0.0f, 0.0f};
+            const int op[6] = {2, 0, 0, 0, 0, 0};
+            block_combine(v, op, 3);
+            amax = v[0];
+            s1 = v[1];
+            s2 = v[2];
+        }
         alpha = fminf(1.0f, P.tau * amax);
         const float mu_next = fmaxf((sum_c + alpha * s1 + alpha * alpha * s2) * inv_m2, 0.0f);
         const float om = 1.0f - alpha;
@@ -653,7 +692,7 @@ __global__ __launch_bounds__(64, 1) void k_sqp_rti_rowpar(KParams P, KArgs a, in
     if (status == 0) {
         auto entry = [&](int k) -> float* {
             const int kk = k <= N ? k : N;
-            return (q == 0 && is_x) ? &XB(kk, xi) : ((q == 0 && is_u && kk < N) ? &UBAR(kk, r) : tdummy);
+            return (wr && is_x) ? &XB(kk, xi) : ((wr && is_u && kk < N) ? &UBAR(kk, r) : wdummy);
         };
         constexpr int EC = 8;
         for (int k0 = 0; k0 <= N; k0 += EC) {
@@ -674,13 +713,13 @@ __global__ __launch_bounds__(64, 1) void k_sqp_rti_rowpar(KParams P, KArgs a, in
         if (a.xtraj || a.utraj) {
             __threadfence_block();
             for (int k = 0; k <= N; k++) {
-                if (q == 0 && is_x && a.xtraj) a.xtraj[((size_t)k * NX + xi) * Bn + inst] = XB(k, xi);
-                if (q == 0 && is_u && k < N && a.utraj) a.utraj[((size_t)k * NU + r) * Bn + inst] = UBAR(k, r);
+                if (wr && is_x && a.xtraj) a.xtraj[((size_t)k * NX + xi) * Bn + inst] = XB(k, xi);
+                if (wr && is_u && k < N && a.utraj) a.utraj[((size_t)k * NU + r) * Bn + inst] = UBAR(k, r);
             }
         }
     }
     __threadfence_block();
-    if (lane == 0) {
+    if (tid == 0) {
         float u0[NU];
 #pragma unroll
         for (int j = 0; j < NU; j++) {
@@ -725,7 +764,8 @@ __global__ __launch_bounds__(64, 1) void k_sqp_rti_rowpar(KParams P, KArgs a, in
 template <class M>
 size_t rowpar_lds_bytes(int N, int mode)
 {
-    return (size_t)(N + 1) * 16 * (5 + M::NGV) * sizeof(float) + (mode == kModeRun ? (size_t)(N + 1) * 3 * sizeof(float) : 0);
+    // stage inputs, the reference poses (always reserved: the reduction slots follow them), [4][8] reductions
+    return ((size_t)(N + 1) * 16 * (5 + M::NGV) + (size_t)(N + 1) * 3 + 32) * sizeof(float);
 }
 
 template <class M>
@@ -734,7 +774,10 @@ hipError_t launch_sqp_rti_rowpar(const KParams& P, const KArgs& a, int mode, hip
     if (a.B <= 0) return hipSuccess;
     const size_t lds = rowpar_lds_bytes<M>(P.N, mode);
     if (lds > 65536 || P.ipm != 1 || a.segs) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((k_sqp_rti_rowpar<M>), dim3(a.B), dim3(64), lds, stream, P, a, mode);
+    if (a.rowpar >= 4)  // four waves per robot (one per SIMD of its CU)
+        hipLaunchKernelGGL((k_sqp_rti_rowpar<M, 4>), dim3(a.B), dim3(256), lds, stream, P, a, mode);
+    else
+        hipLaunchKernelGGL((k_sqp_rti_rowpar<M, 1>), dim3(a.B), dim3(64), lds, stream, P, a, mode);
     return hipGetLastError();
 }
 

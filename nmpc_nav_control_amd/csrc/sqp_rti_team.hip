@@ -61,8 +61,9 @@ __device__ unsigned long long g_stamps_c1[256][kStampIts];
 template <class M>
 size_t team_scratch_floats(int N, int stride)
 {
-    // the lane records [robot][stage][slot][RS], then the DZ plane [robot][stage][16]
-    return (size_t)stride * (N + 1) * 16 * (TeamRec<M>::RS + (kDzPlane ? 1 : 0)) + 64;
+    // the lane records [robot][stage][slot][RS], the DZ plane [robot][stage][16], then the row-parallel kernel's
+    // per-lane dummy records [256 robots][256 lanes][RS] (sqp_rti_rowpar.hip)
+    return (size_t)stride * (N + 1) * 16 * (TeamRec<M>::RS + 1) + (size_t)256 * 256 * TeamRec<M>::RS + 64;
 }
 
 namespace {
