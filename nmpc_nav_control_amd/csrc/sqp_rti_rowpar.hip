@@ -81,8 +81,8 @@ __device__ __forceinline__ float wave_min_rows(float v)
 }
 
 // W waves per robot (one per SIMD): the stage-parallel phases run on all 4 W rows; every wave runs the serial
-// phases (identically), and only wave 0's row 0 stores their results (the other lanes store into per-lane dummy
-// records: no two lanes of an instruction write one address)
+// phases (identically) and wave 0 stores their results (the other waves store into dummy stage blocks of the same
+// layout: per-lane scattered dummy addresses made the serial phases' stores 1.6x slower, measured)
 template <class M, int W>
 __global__ __launch_bounds__(64 * W, 1) void k_sqp_rti_rowpar(KParams P, KArgs a, int mode)
 {
@@ -122,8 +122,15 @@ __global__ __launch_bounds__(64 * W, 1) void k_sqp_rti_rowpar(KParams P, KArgs a
     float* const tbase = rbase + (lv ? r : 0) * rec_lane<RS, QM>();   // idle slots read slot 0
     float* const tbase_own = rbase + r * rec_lane<RS, QM>();          // every lane's own slot
     float* const dzbase = a.scratch + (size_t)a.stride * (N + 1) * KS + (size_t)inst * (N + 1) * 16 + r;
-    // this lane's dummy record (nobody reads it): the target of stores a lane issues without a result to store
-    float* const wdummy = a.scratch + (size_t)a.stride * (N + 1) * 16 * (RS + 1) + ((size_t)(inst & 255) * 256 + tid) * RS;
+    // Stores of the serial phases: wave 0 stores (its four rows the same values to the same addresses, as one
+    // row would); waves 1.. store into a dummy stage block of their own with the same slot layout (the same
+    // coalescing as the real store; nobody reads it). Idle slots and rows past the last stage of a stage-parallel
+    // phase store into tdummy.
+    float* const dummy = a.scratch + (size_t)a.stride * (N + 1) * 16 * (RS + 1);
+    float* const wblk = dummy + ((size_t)(inst & 255) * 4 + wave) * KS;      // this wave's dummy stage block
+    float* const wdz = dummy + (size_t)256 * 4 * KS + ((size_t)(inst & 255) * 4 + wave) * 16 + r;  // dummy DZ
+    const bool w0 = wave == 0;
+    float* const tdummy = rbase + (size_t)N * KS + 15 * rec_lane<RS, QM>();  // nobody reads it
     const bool warm = P.warm && a.warm && a.warm[inst] && !(a.reset && a.reset[inst]);
     RP_STAMP(0);
 
@@ -336,8 +343,8 @@ __global__ __launch_bounds__(64 * W, 1) void k_sqp_rti_rowpar(KParams P, KArgs a
             }
 #pragma unroll
             for (int i = 0; i < NGV; i++) rec[R::GV + i] = (k < N && lv) ? cur.g[i] : 0.0f;
-            rec_store<RS, QM>(wr ? tbase_own + (size_t)k * KS : wdummy, rec);  // idle slots: their own unused one
-            *(wr ? dzbase + (size_t)k * 16 : wdummy) = 0.0f;
+            rec_store<RS, QM>(w0 ? tbase_own + (size_t)k * KS : wblk + r * rec_lane<RS, QM>(), rec);
+            *(w0 ? dzbase + (size_t)k * 16 : wdz) = 0.0f;
             if (k < N) {
                 const float dzd = is_x ? dx : 0.0f;
                 float nx_ = dot_v<NX, NU>(0.0f, dzd, grow);
@@ -475,7 +482,7 @@ __global__ __launch_bounds__(64 * W, 1) void k_sqp_rti_rowpar(KParams P, KArgs a
             rc[R::SIG] = sig;
             rc[R::C0] = c0;
             rc[R::GH] = valid ? gh : 0.0f;
-            float* const pk = (lv && kv) ? tbase + (size_t)k * KS : wdummy;
+            float* const pk = (lv && kv) ? tbase + (size_t)k * KS : tdummy;
             rec_store_range<R::Z, R::LU + 1, RS, QM>(pk, rc);
             rec_store_range<R::SIG, R::GH + 1, RS, QM>(pk, rc);
         }
@@ -563,7 +570,8 @@ __global__ __launch_bounds__(64 * W, 1) void k_sqp_rti_rowpar(KParams P, KArgs a
 #pragma unroll
                     for (int j = 0; j < NV; j++) Lrow[j] = Lr[j];
                     // LR, LM (every row stores the same values; idle slots store into the dummy record)
-                    rec_store_range<R::LR, R::LM + NU, RS, QM>((wr && lv) ? tbase + (size_t)k * KS : wdummy, rc);
+                    rec_store_range<R::LR, R::LM + NU, RS, QM>(
+                        lv ? (w0 ? tbase + (size_t)k * KS : wblk + r * rec_lane<RS, QM>()) : tdummy, rc);
                 }
                 piv = pi_new;
             });
@@ -640,7 +648,7 @@ __global__ __launch_bounds__(64 * W, 1) void k_sqp_rti_rowpar(KParams P, KArgs a
                     if (r == qq) dz = du_all[qq];
                 dz = is_x ? ((k >= 1) ? dxs : 0.0f) : dz;
                 dz = valid ? dz : 0.0f;
-                *(wr ? dzbase + (size_t)k * 16 : wdummy) = dz;  // every slot its own entry (idle slots: 0)
+                *(w0 ? dzbase + (size_t)k * 16 : wdz) = dz;  // every slot its own entry (idle slots: 0)
                 if (k < N) dxs = dyn(rc, dz);
             });
         }
@@ -692,7 +700,7 @@ __global__ __launch_bounds__(64 * W, 1) void k_sqp_rti_rowpar(KParams P, KArgs a
     if (status == 0) {
         auto entry = [&](int k) -> float* {
             const int kk = k <= N ? k : N;
-            return (wr && is_x) ? &XB(kk, xi) : ((wr && is_u && kk < N) ? &UBAR(kk, r) : wdummy);
+            return (w0 && is_x) ? &XB(kk, xi) : ((w0 && is_u && kk < N) ? &UBAR(kk, r) : tdummy);
         };
         constexpr int EC = 8;
         for (int k0 = 0; k0 <= N; k0 += EC) {

@@ -62,8 +62,8 @@ template <class M>
 size_t team_scratch_floats(int N, int stride)
 {
     // the lane records [robot][stage][slot][RS], the DZ plane [robot][stage][16], then the row-parallel kernel's
-    // per-lane dummy records [256 robots][256 lanes][RS] (sqp_rti_rowpar.hip)
-    return (size_t)stride * (N + 1) * 16 * (TeamRec<M>::RS + 1) + (size_t)256 * 256 * TeamRec<M>::RS + 64;
+    // dummy stage blocks [256 robots][4 waves][16][RS] and dummy DZ rows [256][4][16] (sqp_rti_rowpar.hip)
+    return (size_t)stride * (N + 1) * 16 * (TeamRec<M>::RS + 1) + (size_t)256 * 4 * 16 * (TeamRec<M>::RS + 1) + 64;
 }
 
 namespace {
