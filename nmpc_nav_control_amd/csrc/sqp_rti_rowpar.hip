@@ -177,6 +177,27 @@ __global__ __launch_bounds__(64 * W, 1) void k_sqp_rti_rowpar(KParams P, KArgs a
     float* const s_stg = s_row;
     float* const my_traj = s_row + (size_t)(N + 1) * SF * 16;
     float* const s_red = my_traj + (size_t)(N + 1) * 3;  // [W][8] per-wave partial reductions
+
+    // block reductions of per-wave partials (W > 1): every wave combines the W partials in the same order, so every
+    // wave holds identical values and takes identical decisions; the barrier is also the phase boundary
+    auto block_combine = [&](float (&v)[6], const int (&op)[6], int n) {
+        if constexpr (W == 1) {
+            __syncthreads();
+        } else {
+            if ((tid & 63) == 0)
+                for (int i = 0; i < n; i++) s_red[wave * 8 + i] = v[i];
+            __syncthreads();
+            for (int i = 0; i < n; i++) {
+                float acc = s_red[i];
+                for (int w = 1; w < W; w++) {
+                    const float x = s_red[w * 8 + i];
+                    acc = (op[i] == 0) ? acc + x : ((op[i] == 1) ? fmaxf(acc, x) : fminf(acc, x));
+                }
+                v[i] = acc;
+            }
+        }
+    };
+
     const int len = (mode == kModeRun) ? (a.traj_len ? a.traj_len[inst] : N + 1) : 0;
     {
         struct In {
@@ -266,20 +287,21 @@ __global__ __launch_bounds__(64 * W, 1) void k_sqp_rti_rowpar(KParams P, KArgs a
     __syncthreads();  // the stage inputs of every row are in LDS
     RP_STAMP(1);
 
-    // ---- P0b: the serial pass (every row identically): reference unwrap / pad, gradient, bounds, slacks,
-    // multipliers, the record, and the dynamics-feasible initial iterate dx_{k+1} = A dx_k + b_k --------------
-    float dx = is_x ? x0_lane - XB(0, xi) : 0.0f;
-    float sum_c0 = 0.0f;
-    {
-        float ref_x = 0.0f, ref_y = 0.0f, ref_t = pose_th, prv_x = 0.0f, prv_y = 0.0f, prv_t = 0.0f;
+    // ---- P0b (serial, wave 0): the dynamics-feasible initial iterate dx_{k+1} = A_k dx_k + b_k and, in run mode,
+    // the reference unwrap / padding (NMPCNavControlDiff.cpp:104-118), both recursions over the stages; dx_k and
+    // the stage's reference pose go to LDS for P0c ----------------------------------------------------------------
+    float* const s_dx = s_red + 32;                  // [N+1][16]
+    float* const s_ref = s_dx + (size_t)(N + 1) * 16;  // [N+1][3]
+    if (w0) {
+        float dx = is_x ? x0_lane - XB(0, xi) : 0.0f;
+        float ref_x = 0.0f, ref_y = 0.0f, ref_t = pose_th;
         struct Stg {
-            float v[5], g[NGV], t[3];
+            float b, g[NGV], t[3];
         };
         auto lds_ld = [&](int k, Stg& o) {
             const int kk = k <= N ? k : N;
             const float* const st = s_stg + (size_t)kk * SF * 16 + r;
-#pragma unroll
-            for (int f = 0; f < 5; f++) o.v[f] = st[f * 16];
+            o.b = st[64];
 #pragma unroll
             for (int i = 0; i < NGV; i++) o.g[i] = st[(5 + i) * 16];
 #pragma unroll
@@ -289,7 +311,6 @@ __global__ __launch_bounds__(64 * W, 1) void k_sqp_rti_rowpar(KParams P, KArgs a
         lds_ld(0, cur);
         for (int k = 0; k <= N; k++) {
             lds_ld(k + 1, nxt);
-            float yr = cur.v[1];
             if (mode == kModeRun) {
                 if (k < len) {
                     ref_x = cur.t[0];
@@ -300,51 +321,9 @@ __global__ __launch_bounds__(64 * W, 1) void k_sqp_rti_rowpar(KParams P, KArgs a
                     else if (d < -kPi) th += 2.0f * kPi;
                     ref_t = th;
                 }
-                if (k == N - 1) { prv_x = ref_x; prv_y = ref_y; prv_t = ref_t; }
-                yr = (is_x && xi == 0) ? ref_x : ((is_x && xi == 1) ? ref_y : ((is_x && xi == 2) ? ref_t : 0.0f));
+                if (tid < 3) s_ref[k * 3 + tid] = (tid == 0) ? ref_x : ((tid == 1) ? ref_y : ref_t);
             }
-            const float zbar = cur.v[0];
-            float rec[RS];
-#pragma unroll
-            for (int f = 0; f < RS; f++) rec[f] = 0.0f;
-            const bool vu = is_u && k < N, vx = is_x && k >= 1;
-            const bool valid = vu || vx;
-            if (vu) rec[R::GR] = sc * w_lane * (zbar - yr);
-            if (vx) {
-                float w = sc * w_lane;
-                if (k == N) {
-                    w = we_lane;
-                    if (mode == kModeRun && P.terminal_hack && xi < 3) {  // NMPCNavControlDiff.cpp:127-139
-                        const bool eq = (ref_x == prv_x) && (ref_y == prv_y) && (ref_t == prv_t);
-                        w = (eq ? 100.0f : 1.0f) * w_lane;
-                        we_lane = w;
-                    }
-                }
-                rec[R::GR] = w * (zbar - yr);
-            }
-            const float z = vx ? dx : 0.0f;
-            rec[R::Z] = z;
-            rec[R::TL] = kFar;
-            rec[R::TU] = kFar;
-            rec[R::LB] = -kFar;
-            rec[R::UB] = kFar;
-            if (valid && has_b) {
-                const float lb = lo_b - zbar, ubd = hi_b - zbar;
-                const float tl = fmaxf(z - lb, P.thr0), tu = fmaxf(ubd - z, P.thr0);
-                rec[R::LB] = lb;
-                rec[R::UB] = ubd;
-                rec[R::TL] = tl;
-                rec[R::TU] = tu;
-                const float ll0 = warm ? fmaxf(fminf(cur.v[2], kWarmLambdaCap), P.warm_kappa / tl) : P.mu0 / tl;
-                const float lu0 = warm ? fmaxf(fminf(cur.v[3], kWarmLambdaCap), P.warm_kappa / tu) : P.mu0 / tu;
-                rec[R::LL] = ll0;
-                rec[R::LU] = lu0;
-                sum_c0 += ll0 * tl + lu0 * tu;
-            }
-#pragma unroll
-            for (int i = 0; i < NGV; i++) rec[R::GV + i] = (k < N && lv) ? cur.g[i] : 0.0f;
-            rec_store<RS, QM>(w0 ? tbase_own + (size_t)k * KS : wblk + r * rec_lane<RS, QM>(), rec);
-            *(w0 ? dzbase + (size_t)k * 16 : wdz) = 0.0f;
+            if (tid < 16) s_dx[k * 16 + r] = dx;
             if (k < N) {
                 const float dzd = is_x ? dx : 0.0f;
                 float nx_ = dot_v<NX, NU>(0.0f, dzd, grow);
@@ -353,13 +332,66 @@ __global__ __launch_bounds__(64 * W, 1) void k_sqp_rti_rowpar(KParams P, KArgs a
                     const float sr = row_sum16(lv ? cur.g[i] * dzd : 0.0f);
                     if (xi == i) nx_ = sr;
                 }
-                dx = is_x ? nx_ + cur.v[4] : 0.0f;
+                dx = is_x ? nx_ + cur.b : 0.0f;
             }
             cur = nxt;
         }
     }
-    __syncthreads();  // the records before the stage-parallel phase A reads them on other rows
+    __syncthreads();
     RP_STAMP(2);
+
+    // ---- P0c (stage-parallel): gradient, bounds, slacks, multipliers and the record of stage k on row k mod ROWS
+    if (mode == kModeRun && P.terminal_hack && is_x && xi < 3) {  // NMPCNavControlDiff.cpp:127-139
+        const bool eq = (s_ref[N * 3] == s_ref[(N - 1) * 3]) && (s_ref[N * 3 + 1] == s_ref[(N - 1) * 3 + 1]) &&
+                        (s_ref[N * 3 + 2] == s_ref[(N - 1) * 3 + 2]);
+        we_lane = (eq ? 100.0f : 1.0f) * w_lane;
+    }
+    float sum_c0 = 0.0f;
+    for (int j = 0; j < NR; j++) {
+        const int kr = j * ROWS + q;
+        const bool kv = kr <= N;
+        const int k = kv ? kr : N;
+        const float* const st = s_stg + (size_t)k * SF * 16 + r;
+        const float zbar = st[0];
+        const float yr = (mode == kModeRun) ? ((is_x && xi < 3) ? s_ref[k * 3 + xi] : 0.0f) : st[16];
+        const float dxk = s_dx[k * 16 + r];
+        float rec[RS];
+#pragma unroll
+        for (int f = 0; f < RS; f++) rec[f] = 0.0f;
+        const bool vu = is_u && k < N, vx = is_x && k >= 1;
+        const bool valid = vu || vx;
+        const float w = vx ? ((k == N) ? we_lane : sc * w_lane) : sc * w_lane;
+        rec[R::GR] = valid ? w * (zbar - yr) : 0.0f;
+        const float z = vx ? dxk : 0.0f;
+        rec[R::Z] = z;
+        rec[R::TL] = kFar;
+        rec[R::TU] = kFar;
+        rec[R::LB] = -kFar;
+        rec[R::UB] = kFar;
+        if (valid && has_b) {
+            const float lb = lo_b - zbar, ubd = hi_b - zbar;
+            const float tl = fmaxf(z - lb, P.thr0), tu = fmaxf(ubd - z, P.thr0);
+            rec[R::LB] = lb;
+            rec[R::UB] = ubd;
+            rec[R::TL] = tl;
+            rec[R::TU] = tu;
+            const float ll0 = warm ? fmaxf(fminf(st[32], kWarmLambdaCap), P.warm_kappa / tl) : P.mu0 / tl;
+            const float lu0 = warm ? fmaxf(fminf(st[48], kWarmLambdaCap), P.warm_kappa / tu) : P.mu0 / tu;
+            rec[R::LL] = ll0;
+            rec[R::LU] = lu0;
+            sum_c0 += kv ? ll0 * tl + lu0 * tu : 0.0f;
+        }
+#pragma unroll
+        for (int i = 0; i < NGV; i++) rec[R::GV + i] = (k < N && lv) ? st[(5 + i) * 16] : 0.0f;
+        rec_store<RS, QM>(kv ? tbase_own + (size_t)k * KS : tdummy, rec);  // idle slots: their own unused slot
+        dzbase[(size_t)k * 16] = 0.0f;  // (rows past the end repeat stage N's zero)
+    }
+    {
+        float v[6] = {wave_sum_rows(row_sum16(lv ? sum_c0 : 0.0f)), 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+        const int op[6] = {0, 0, 0, 0, 0, 0};
+        block_combine(v, op, 1);
+        sum_c0 = v[0];
+    }
 
     double onehot[NV];
 #pragma unroll
@@ -369,7 +401,6 @@ __global__ __launch_bounds__(64 * W, 1) void k_sqp_rti_rowpar(KParams P, KArgs a
     for (int i = 0; i < NX; i++) gcol64[i] = (double)gcol[i];
     const int m = N * NU + N * M::NBX;
     const float inv_m2 = 0.5f / (float)m;
-    sum_c0 = row_sum16(lv ? sum_c0 : 0.0f);
 
     auto column = [&](const float (&rc)[RS], float (&Gc)[NX]) {
 #pragma unroll
@@ -403,26 +434,6 @@ __global__ __launch_bounds__(64 * W, 1) void k_sqp_rti_rowpar(KParams P, KArgs a
             load(k_2, ra);
             body(k + dir, rb);
             if (k + dir == k1) break;
-        }
-    };
-
-    // block reductions of per-wave partials (W > 1): every wave combines the W partials in the same order, so every
-    // wave holds identical values and takes identical decisions; the barrier is also the phase boundary
-    auto block_combine = [&](float (&v)[6], const int (&op)[6], int n) {
-        if constexpr (W == 1) {
-            __syncthreads();
-        } else {
-            if ((tid & 63) == 0)
-                for (int i = 0; i < n; i++) s_red[wave * 8 + i] = v[i];
-            __syncthreads();
-            for (int i = 0; i < n; i++) {
-                float acc = s_red[i];
-                for (int w = 1; w < W; w++) {
-                    const float x = s_red[w * 8 + i];
-                    acc = (op[i] == 0) ? acc + x : ((op[i] == 1) ? fmaxf(acc, x) : fminf(acc, x));
-                }
-                v[i] = acc;
-            }
         }
     };
 
@@ -772,8 +783,8 @@ __global__ __launch_bounds__(64 * W, 1) void k_sqp_rti_rowpar(KParams P, KArgs a
 template <class M>
 size_t rowpar_lds_bytes(int N, int mode)
 {
-    // stage inputs, the reference poses (always reserved: the reduction slots follow them), [4][8] reductions
-    return ((size_t)(N + 1) * 16 * (5 + M::NGV) + (size_t)(N + 1) * 3 + 32) * sizeof(float);
+    // stage inputs, reference poses, [4][8] reductions, dx [N+1][16] and unwrapped references [N+1][3] (P0b)
+    return ((size_t)(N + 1) * (16 * (5 + M::NGV) + 3 + 16 + 3) + 32) * sizeof(float);
 }
 
 template <class M>
