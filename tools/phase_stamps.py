@@ -13,7 +13,7 @@ model = sys.argv[1] if len(sys.argv) > 1 else "diff"
 B = int(sys.argv[2]) if len(sys.argv) > 2 else 4096
 N = int(sys.argv[3]) if len(sys.argv) > 3 else 40
 f = Fleet(model, B, N, DEFAULT_SEED + 1, dev)
-for _ in range(30):
+for _ in range(int(os.environ.get("STAMP_WARM", "240"))):  # stationary closed loop (bench default)
     f.tick()
 torch.cuda.synchronize()
 W = 2 + 4 * 64

@@ -2,7 +2,11 @@
 solve kernel's record to profiles/<round>/pmc/pmc_<config>.json (read by bench.py's roofline: traffic and
 issue figures).
 
-usage: python tools/pmc_summary.py gpurun_out/<tag> <config key, e.g. diff_N40_B4096> [--round r02] [--write]
+usage: python tools/pmc_summary.py gpurun_out/<tag> <config key, e.g. diff_N40_B4096> [--round r03] [--last K]
+                                   [--commit <sha>] [--write]
+  --last K   average only the last K dispatches of each kernel (the stationary tail of the bench's closed loop;
+             default: all dispatches)
+  --commit   the commit the GPU run was made from (recorded as source_commit; default: this checkout's HEAD)
 
 Figures per launch of the solve kernel (for a mixed fleet: the sum over its per-model launches of one step):
   l2_fabric_bytes_per_launch = 2 x FETCH_SIZE + WRITE_SIZE (KB -> bytes). MI355X_MICROARCH.md "HBM": on gfx950
@@ -27,11 +31,12 @@ from collections import defaultdict
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def load(prefix):
+def load(prefix, last=None):
     acc = defaultdict(lambda: defaultdict(list))
     for path in glob.glob(prefix + "_pmc*/**/*counter_collection.csv", recursive=True):
         with open(path) as fh:
-            for row in csv.DictReader(fh):
+            rows = sorted(csv.DictReader(fh), key=lambda r: int(r.get("Dispatch_Id") or 0))
+            for row in rows:
                 m = re.search(r"\b(k_\w+)", row["Kernel_Name"])
                 name = m.group(1) if m else row["Kernel_Name"][:60]
                 # one model's kernel template: keep the model in the name (mixed fleets launch three)
@@ -39,6 +44,8 @@ def load(prefix):
                 if t:
                     name = f"k_sqp_rti_team<{t.group(1)}>"
                 acc[name][row["Counter_Name"]].append(float(row["Counter_Value"]))
+    if last:
+        acc = {k: {c: v[-last:] for c, v in d.items()} for k, d in acc.items()}
     return {k: {c: sum(v) / len(v) for c, v in d.items()} for k, d in acc.items()}
 
 
@@ -62,8 +69,10 @@ def issue_est(tot):
 
 def main():
     prefix, key = sys.argv[1], sys.argv[2]
-    rnd = sys.argv[sys.argv.index("--round") + 1] if "--round" in sys.argv else "r02"
-    summ = load(prefix)
+    arg = lambda k, d=None: sys.argv[sys.argv.index(k) + 1] if k in sys.argv else d  # noqa: E731
+    rnd = arg("--round", "r03")
+    last = int(arg("--last", 0)) or None
+    summ = load(prefix, last)
     for k, d in sorted(summ.items()):
         print(k)
         for c, v in sorted(d.items()):
@@ -79,11 +88,13 @@ def main():
     cyc = tot.get("SQ_WAVE_CYCLES", 0.0)
     cyc4 = cyc
     hit, miss = tot.get("TCC_HIT_sum", 0.0), tot.get("TCC_MISS_sum", 0.0)
-    try:
-        commit = subprocess.run(["git", "-C", ROOT, "rev-parse", "--short", "HEAD"], capture_output=True,
-                                text=True).stdout.strip()
-    except OSError:
-        commit = None
+    commit = arg("--commit")
+    if commit is None:
+        try:
+            commit = subprocess.run(["git", "-C", ROOT, "rev-parse", "--short", "HEAD"], capture_output=True,
+                                    text=True).stdout.strip()
+        except OSError:
+            commit = None
     rec = {"kernels": solve, "config": key, "l2_fabric_bytes_per_launch": 2 * fetch * 1024 + write * 1024,
            "fetch_size_kb": fetch, "write_size_kb": write,
            "tcc_hit_rate": hit / (hit + miss) if hit + miss > 0 else None,
@@ -109,6 +120,7 @@ def main():
            "executed_flops_fp32_per_launch": (64 * tot["SQ_INSTS_VALU_FLOPS_FP32"]
                                               if tot.get("SQ_INSTS_VALU_FLOPS_FP32") else None),
            "source": os.path.basename(prefix.rstrip("/")), "source_commit": commit,
+           "dispatches_averaged": f"last {last} per kernel" if last else "all",
            "note": "per launch (mixed: summed over the per-model launches of one step); "
                    "traffic = 2*FETCH_SIZE + WRITE_SIZE (L2<->fabric incl. Infinity-Cache hits)"}
     print(json.dumps(rec, indent=1))
