@@ -200,7 +200,18 @@ int nmpc_fleet_sim_step(nmpc_batch* b, int B, const float* path, float* s, float
  * issues the same targets. Goal robots (path length < 0) get a goal at distance U(goal_r_lo, goal_r_hi) in a
  * uniform direction with a uniform heading; path robots an arc starting within 0.2 m / 0.3 rad of the robot
  * (curvature U(-kappa_max, kappa_max), speed U(speed_lo, speed_hi), length U(len_lo, len_hi)), progress s = 0.
- * The new ttl is ttl_min + ((h >> 8) * (ttl_max - ttl_min + 1) >> 24). */
+ * The new ttl is ttl_min + ((h >> 8) * (ttl_max - ttl_min + 1) >> 24).
+ * `stats` (optional) accumulates the statistics of the solve that preceded this step in the same launch, before the
+ * renewal rewrites `reset` (so `cold_*` count the solves that ran with reset set): */
+typedef struct nmpc_fleet_stats {
+    const int* qp_iter;         /* [B] in: the solve's executed IPM iterations */
+    long long* iters_sum;       /* [B] += qp_iter */
+    int* iters_max;             /* [B] = max(iters_max, qp_iter) */
+    long long* fail_cnt;        /* [B] += (status != 0) */
+    long long* hist;            /* [64] += robots per executed iteration count (clamped to [0, 63]) */
+    long long* cold_cnt;        /* [B] += reset */
+    long long* cold_iters;      /* [B] += reset * qp_iter */
+} nmpc_fleet_stats;
 typedef struct nmpc_fleet_renew {
     unsigned int seed;
     int start;                  /* global index of robot 0 of this call */
@@ -210,7 +221,9 @@ typedef struct nmpc_fleet_renew {
     float pos_tol, ang_tol;     /* final_position_error (m) / final_orientation_error (rad), nmpc_nav_control.yaml:6-7 */
     int* ev;                    /* [B] events so far (in/out) */
     int* ttl;                   /* [B] ticks left (in/out) */
-    unsigned char* reset;       /* [B] out: 1 where this step issued a new goal / path */
+    unsigned char* reset;       /* [B] in: the flags the last solve ran with; out: 1 where this step issued a new
+                                 * goal / path */
+    const nmpc_fleet_stats* stats; /* NULL: no statistics (every pointer of a given one is required, and status) */
 } nmpc_fleet_renew;
 int nmpc_fleet_sim_step_renew(nmpc_batch* b, int B, float* path, float* s, float* pose, float* vel, float* steer,
                               const float* u0, const int* status, float* traj, int* traj_len,

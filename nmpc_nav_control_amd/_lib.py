@@ -33,13 +33,20 @@ class ModelParams(ctypes.Structure):
     ]
 
 
+class FleetStats(ctypes.Structure):
+    """Mirror of nmpc_fleet_stats (include/nmpc_amd/nmpc_batch.h): per-tick solve statistics accumulated by the
+    renewal launch."""
+    _fields_ = [("qp_iter", c_void_p), ("iters_sum", c_void_p), ("iters_max", c_void_p), ("fail_cnt", c_void_p),
+                ("hist", c_void_p), ("cold_cnt", c_void_p), ("cold_iters", c_void_p)]
+
+
 class FleetRenew(ctypes.Structure):
     """Mirror of nmpc_fleet_renew (include/nmpc_amd/nmpc_batch.h): the harness's stationary goal / path renewal."""
     _fields_ = [("seed", ctypes.c_uint), ("start", ctypes.c_int), ("ttl_min", ctypes.c_int), ("ttl_max", ctypes.c_int),
                 ("goal_r_lo", ctypes.c_float), ("goal_r_hi", ctypes.c_float), ("kappa_max", ctypes.c_float),
                 ("speed_lo", ctypes.c_float), ("speed_hi", ctypes.c_float), ("len_lo", ctypes.c_float),
                 ("len_hi", ctypes.c_float), ("pos_tol", ctypes.c_float), ("ang_tol", ctypes.c_float),
-                ("ev", c_void_p), ("ttl", c_void_p), ("reset", c_void_p)]
+                ("ev", c_void_p), ("ttl", c_void_p), ("reset", c_void_p), ("stats", c_void_p)]
 
 
 class CodegenDesc(ctypes.Structure):

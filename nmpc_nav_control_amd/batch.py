@@ -8,7 +8,7 @@ import ctypes
 
 import torch
 
-from ._lib import KERNELS, MODEL_IDS, SCHEDULES, FleetRenew, ModelParams, check, default_params, lib, model_dims
+from ._lib import KERNELS, MODEL_IDS, SCHEDULES, FleetRenew, FleetStats, ModelParams, check, default_params, lib, model_dims
 
 
 def _ptr(t, dtype=None, shape=None, name="argument"):
@@ -27,7 +27,7 @@ def _ptr(t, dtype=None, shape=None, name="argument"):
     return ctypes.c_void_p(t.data_ptr())
 
 
-F32, I32, U8 = torch.float32, torch.int32, (torch.uint8, torch.bool)
+F32, I32, I64, U8 = torch.float32, torch.int32, torch.int64, (torch.uint8, torch.bool)
 
 
 def _stream(stream):
@@ -42,6 +42,8 @@ class BatchSolver:
     ``NMPCNavControl{Diff,Omni4,Tric}::run`` (pre-solve, SQP-RTI, post-solve) with the warm-start
     iterate and carried vel-ref states resident on the device between ticks.
     """
+
+    fused_stats = True  # fleet_sim_step_renew accumulates the solve statistics in its own launch (nmpc_fleet_stats)
 
     def __init__(self, model, N, capacity, params=None, device="cuda", kernel=None):
         self.model = model
@@ -210,19 +212,32 @@ class BatchSolver:
 
 
     def fleet_sim_step_renew(self, path, s, pose, vel, steer, u0, status, traj, traj_len, ev, ttl, reset, seed, start,
-                             renew, stream=None):
+                             renew, stream=None, stats=None):
         """fleet_sim_step (advance) followed by the stationary loop's goal / path renewal (nmpc_fleet_sim_step_renew):
-        ev, ttl int32 [B] in/out, reset uint8 [B] out (the next run's reset mask); renew: scenario.RENEW keys +
-        kappa_max, speed (lo, hi)."""
+        ev, ttl int32 [B] in/out, reset uint8 [B] in (the flags the last solve ran with) / out (the next run's reset
+        mask); renew: scenario.RENEW keys + kappa_max, speed (lo, hi). stats (optional): dict of device tensors the
+        same launch accumulates the last solve's statistics into (nmpc_fleet_stats): qp_iter int32 [B] (in),
+        iters_sum int64 [B], iters_max int32 [B], fail_cnt int64 [B], hist int64 [64], cold_cnt / cold_iters
+        int64 [B]."""
         B = pose.shape[1]
         if not 0 <= B <= self.capacity:
             raise ValueError(f"batch {B} exceeds the capacity {self.capacity}")
+        S = None
+        if stats is not None:
+            S = FleetStats(qp_iter=_ptr(stats["qp_iter"], I32, (B,), "qp_iter"),
+                           iters_sum=_ptr(stats["iters_sum"], I64, (B,), "iters_sum"),
+                           iters_max=_ptr(stats["iters_max"], I32, (B,), "iters_max"),
+                           fail_cnt=_ptr(stats["fail_cnt"], I64, (B,), "fail_cnt"),
+                           hist=_ptr(stats["hist"], I64, (64,), "hist"),
+                           cold_cnt=_ptr(stats["cold_cnt"], I64, (B,), "cold_cnt"),
+                           cold_iters=_ptr(stats["cold_iters"], I64, (B,), "cold_iters"))
         R = FleetRenew(seed=int(seed) & 0xFFFFFFFF, start=int(start), ttl_min=int(renew["ttl_min"]),
                        ttl_max=int(renew["ttl_max"]), goal_r_lo=renew["goal_r_lo"], goal_r_hi=renew["goal_r_hi"],
                        kappa_max=renew["kappa_max"], speed_lo=renew["speed"][0], speed_hi=renew["speed"][1],
                        len_lo=renew["len_lo"], len_hi=renew["len_hi"], pos_tol=renew["pos_tol"],
                        ang_tol=renew["ang_tol"], ev=_ptr(ev, I32, (B,), "ev"), ttl=_ptr(ttl, I32, (B,), "ttl"),
-                       reset=_ptr(reset, U8, (B,), "reset"))
+                       reset=_ptr(reset, U8, (B,), "reset"),
+                       stats=ctypes.cast(ctypes.pointer(S), ctypes.c_void_p) if S is not None else None)
         check(lib().nmpc_fleet_sim_step_renew(
             self._h, B, _ptr(path, F32, (6, B), "path"), _ptr(s, F32, (B,), "s"), _ptr(pose, F32, (3, B), "pose"),
             _ptr(vel, F32, (3, B), "vel"), _ptr(steer, F32, (B,), "steer"), _ptr(u0, F32, (self.nu, B), "u0"),

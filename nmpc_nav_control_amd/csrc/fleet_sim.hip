@@ -65,10 +65,30 @@ __device__ inline float fleet_u(const nmpc_fleet_renew& R, unsigned int gi, int 
 template <class M>
 __global__ void k_fleet_sim(KParams P, int B, int stride, float* path, float* s, float* pose, float* vel,
                             float* steer, const float* u0, const int* status, const float* carried, float* traj,
-                            int* traj_len, int advance, nmpc_fleet_renew R)
+                            int* traj_len, int advance, nmpc_fleet_renew R, nmpc_fleet_stats S)
 {
     constexpr int NX = M::NX, NU = M::NU;
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (S.qp_iter) {
+        // the statistics of the solve this step follows (bench harness; replaces a dozen small launches per tick).
+        // `reset` still holds the flags that solve ran with. The histogram goes through a block-local LDS copy.
+        __shared__ unsigned int hist[64];
+        if (threadIdx.x < 64) hist[threadIdx.x] = 0u;
+        __syncthreads();
+        if (i < B) {
+            const int it = S.qp_iter[i];
+            const long long cold = R.reset[i] ? 1 : 0;
+            S.iters_sum[i] += it;
+            S.iters_max[i] = max(S.iters_max[i], it);
+            S.fail_cnt[i] += status[i] != 0 ? 1 : 0;
+            S.cold_cnt[i] += cold;
+            S.cold_iters[i] += cold * it;
+            atomicAdd(&hist[min(max(it, 0), 63)], 1u);
+        }
+        __syncthreads();
+        if (threadIdx.x < 64 && hist[threadIdx.x])
+            atomicAdd((unsigned long long*)&S.hist[threadIdx.x], (unsigned long long)hist[threadIdx.x]);
+    }
     if (i >= B) return;
     const size_t Bn = (size_t)B;
     float ps[3] = {pose[i], pose[Bn + i], pose[2 * Bn + i]};
@@ -197,9 +217,12 @@ hipError_t launch_fleet_sim(const KParams& P, int B, int stride, float* path, fl
     if (B <= 0) return hipSuccess;
     const int block = 256;
     nmpc_fleet_renew R{};
+    nmpc_fleet_stats S{};
     if (renew) R = *renew;
+    if (renew && renew->stats) S = *renew->stats;
+    R.stats = nullptr;  // host memory: the kernel gets S by value
     hipLaunchKernelGGL(k_fleet_sim<M>, dim3((B + block - 1) / block), dim3(block), 0, stream, P, B, stride, path, s,
-                       pose, vel, steer, u0, status, carried, traj, traj_len, advance, R);
+                       pose, vel, steer, u0, status, carried, traj, traj_len, advance, R, S);
     return hipGetLastError();
 }
 

@@ -627,6 +627,10 @@ int nmpc_fleet_sim_step_renew(nmpc_batch* b, int B, float* path, float* s, float
 {
     if (!renew || !renew->ev || !renew->ttl || !renew->reset) return set_err(NMPC_ERR_ARG, "renew: NULL argument");
     if (renew->ttl_min < 1 || renew->ttl_max < renew->ttl_min) return set_err(NMPC_ERR_ARG, "renew: ttl range");
+    if (const nmpc_fleet_stats* st = renew->stats)
+        if (!st->qp_iter || !st->iters_sum || !st->iters_max || !st->fail_cnt || !st->hist || !st->cold_cnt ||
+            !st->cold_iters || !status)
+            return set_err(NMPC_ERR_ARG, "renew: stats needs every pointer and status");
     return fleet_sim(b, B, path, s, pose, vel, steer, u0, status, traj, traj_len, 1, renew, stream);
 }
 

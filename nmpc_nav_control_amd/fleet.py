@@ -70,11 +70,14 @@ class Fleet:
                         reset=self.reset if self.renew else None, cmd=self.cmd, u0=self.u0, status=self.status,
                         qp_iter=self.qp_iter, stream=self.stream)
 
-    def advance(self):
+    def advance(self, stats=None):
+        """The plant / reference step after a solve; stats (renewal only): FleetNode's device statistics of this
+        fleet, accumulated by the same launch (nmpc_fleet_stats)."""
         if self.renew:
+            kw = {"stats": stats} if stats is not None else {}
             self.solver.fleet_sim_step_renew(self.path, self.s, self.pose, self.vel, self.steer, self.u0, self.status,
                                              self.traj, self.tlen, self.ev, self.ttl, self.reset, self.seed,
-                                             self.start, self.renew, stream=self.stream)
+                                             self.start, self.renew, stream=self.stream, **kw)
         else:
             self.solver.fleet_sim_step(self.path, self.s, self.pose, self.vel, self.steer, self.u0, self.status,
                                        self.traj, self.tlen, advance=True, stream=self.stream)
@@ -165,6 +168,16 @@ class FleetNode:
         self._ones = torch.ones(max([f.B for f in self.fleets] + [1]), dtype=torch.int64, device=self.dev)
         self.cold_cnt = torch.zeros(self.B, dtype=torch.int64, device=self.dev)
         self.cold_iters = torch.zeros(self.B, dtype=torch.int64, device=self.dev)
+        # the statistics of a renewing fleet on the device solver go into its plant / renewal launch (one launch per
+        # tick instead of a dozen small torch ops on the fleet's stream); accumulate_one is the general form
+        self.fused = []
+        for j, f in enumerate(self.fleets):
+            sl = slice(self.offs[j], self.offs[j + 1])
+            ok = (cuda and f.renew is not None and getattr(f.solver, "fused_stats", False)
+                  and os.environ.get("NMPC_FLEET_FUSED_STATS", "1") != "0")
+            self.fused.append(dict(qp_iter=f.qp_iter, iters_sum=self.iters_sum[sl], iters_max=self.iters_max[sl],
+                                   fail_cnt=self.fail_cnt[sl], hist=self.iter_hist[j], cold_cnt=self.cold_cnt[sl],
+                                   cold_iters=self.cold_iters[sl]) if ok else None)
 
     def tick_all(self):
         """One control tick of every robot of this rank (joined: with the fleet-wide tick boundary)."""
@@ -279,10 +292,11 @@ class FleetNode:
                 f.solve()
                 if timer is not None:
                     timer.end(j, f.stream)
-                self.accumulate_one(j)
+                if self.fused[j] is None:
+                    self.accumulate_one(j)
                 if self.gather is not None:
                     self._stage(j, f, slot)
-                f.advance()
+                f.advance(self.fused[j])
             if self.gather is not None:
                 self._collect(slot)
             self.tick_no += 1
@@ -300,8 +314,9 @@ class FleetNode:
             f.solve()
             if timer is not None:
                 timer.end(j, f.stream if f.stream is not None else main)
-            self.accumulate_one(j)
-            f.advance()
+            if self.fused[j] is None:
+                self.accumulate_one(j)
+            f.advance(self.fused[j])
             if self.multi:
                 done = torch.cuda.Event()
                 done.record(f.stream)

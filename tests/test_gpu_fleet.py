@@ -304,3 +304,27 @@ def test_decoupled_gather_on_device(built):
                          for f in node.fleets], dim=1)
         assert torch.equal(node.gathered, exp)
     assert int(node.fail_cnt.sum()) == 0
+
+
+def test_fused_statistics_equal_torch_ops(built):
+    """The device statistics FleetNode accumulates inside the plant / renewal launch (nmpc_fleet_stats) equal the
+    general torch form (accumulate_one) on the same closed loop: per-robot iteration sums and maxima, failures, the
+    iteration histogram and the post-renewal (cold) counts, bit for bit. Short ttls make renewals frequent."""
+    ren = dict(ttl_min=2, ttl_max=9)
+    models = [("diff", 700), ("omni4", 300)]
+    a = FleetNode(models, 40, SEED + 4, DEV, renew=ren)
+    b = FleetNode(models, 40, SEED + 4, DEV, renew=ren)
+    assert all(x is not None for x in a.fused)
+    b.fused = [None] * len(b.fleets)
+    for _ in range(15):
+        a.step()
+        b.step()
+    a.join()
+    b.join()
+    torch.cuda.synchronize()
+    for name in ("iters_sum", "iters_max", "fail_cnt", "cold_cnt", "cold_iters"):
+        assert torch.equal(getattr(a, name), getattr(b, name)), name
+    for ha, hb in zip(a.iter_hist, b.iter_hist):
+        assert torch.equal(ha, hb)
+    assert int(a.cold_cnt.sum()) > 0 and int(torch.stack(a.iter_hist).sum()) == 15 * a.B
+    assert a.iter_stats() == b.iter_stats()
