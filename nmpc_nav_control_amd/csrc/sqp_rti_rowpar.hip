@@ -1,5 +1,6 @@
-// sqp_rti_rowpar.hip -- batched SQP-RTI step for small batches: one wavefront per robot, the stage-independent
-// work spread over the wave's four DPP rows, only the recursions over the horizon serial.
+// sqp_rti_rowpar.hip -- batched SQP-RTI step for small batches: one block of W wavefronts per robot (W = 4 up to
+// 256 robots: one wave per SIMD of the robot's CU), the stage-independent work spread over the block's 4 W DPP rows,
+// only the recursions over the horizon serial.
 //
 // The same single-direction IPM as k_sqp_rti_team (sqp_rti_team.hip, SD rule; DESIGN.md "Algorithm and
 // precision"), the same records, warm start and stopping rule, reorganised for latency. In the team kernel one
@@ -8,13 +9,14 @@
 // (NMPCNavControlROS.cpp:713 -> NMPCNavControlDiff.cpp:142). Most of that work does not depend on the
 // neighbouring stage: applying the step, the slacks / multipliers, the residuals, the barrier weights and the
 // rhs terms before the Riccati step (phase A), and the bound directions, the step bound and the complementarity
-// polynomial after the forward recursion (phase D). Here row q of the wave (lanes 16q .. 16q+15, lane 16q + v
-// owns variable v as in a team) runs those phases for stages q, q+4, ...; the Riccati factorisation (phase B:
-// fp64 P G, G'P G, input-block Cholesky, rhs) and the forward recursion of the directions (phase C) are the only
-// stage-serial passes, and every row computes them identically (same records, same DPP broadcasts inside its
-// row), so no row waits on another and stores of the serial phases are identical from all rows. P0 likewise:
-// the RK4 linearisation of stage k on row k mod 4, then the serial initial-iterate pass from LDS.
-// One robot per wave also makes every loop exit wave-uniform (no lockstep teams).
+// polynomial after the forward recursion (phase D). Here row q of the block (lanes 16q .. 16q+15 of its wave
+// q / 4; lane 16q + v owns variable v as in a team) runs those phases for stages q, q + 4 W, ..., and block
+// reductions (LDS) combine the rows; the Riccati factorisation (phase B: fp64 P G, G'P G, input-block Cholesky,
+// rhs) and the forward recursion of the directions (phase C) are the only stage-serial passes, and every wave
+// computes them identically on its row 0 (same records, same DPP broadcasts inside the row), so no wave waits on
+// another; wave 0 stores them, the other waves store to a per-wave dummy block. P0 likewise: the RK4
+// linearisation of stage k on row k mod 4 W, then the serial initial-iterate pass from LDS.
+// One robot per block also makes every loop exit block-uniform (no lockstep teams).
 #include "nmpc_kernels.hpp"
 #include "team_common.hpp"
 
