@@ -1,8 +1,8 @@
 #!/bin/bash
 # Copy the judged summaries of tools/profile_r03.sh (part A, tag A) and tools/profile_r03b.sh (part B, tag B) runs from
 # gpurun_out/ into profiles/r03/, stamping the commit both runs were made from.
-# usage: bash tools/collect_r03.sh <tag A> <tag B> <commit>
-A=gpurun_out/$1; B=gpurun_out/$2; C=$3
+# usage: bash tools/collect_r03.sh <tag A> <tag B> <commit of A> [commit of B, default: of A]
+A=gpurun_out/$1; B=gpurun_out/$2; C=$3; CB=${4:-$3}
 P=profiles/r03
 set -e
 mkdir -p $P/configs $P/pmc $P/stamps $P/windows
@@ -22,9 +22,11 @@ d = defaultdict(list)
 for f in glob.glob(sys.argv[1] + "/**/*marker_api_trace.csv", recursive=True):
     for r in csv.DictReader(open(f)):
         d[r.get("Function") or r.get("Operation") or "?"].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
-out = {k: {"count": len(v), "mean_us": sum(v) / len(v), "min_us": min(v)} for k, v in sorted(d.items())}
+out = {k: {"count": len(v), "median_us": sorted(v)[len(v) // 2], "mean_us": sum(v) / len(v), "min_us": min(v)}
+       for k, v in sorted(d.items())}
 print(json.dumps({"source": "rocprofv3 --marker-trace --kernel-trace of build/capsule_latency 300 (tools/profile_r03.sh)",
-                  "source_commit": sys.argv[2], "ranges": out}, indent=1))
+                  "source_commit": sys.argv[2], "ranges": out,
+                  "note": "the first call's capsule.engine range includes the device and engine set-up (mean skewed)"}, indent=1))
 PY
 python3 - "$A/prof/run_kernel_trace.csv" "$C" > $P/bench_metric_kernel_trace_timed.json <<'PY'
 import csv, json, sys
@@ -43,7 +45,7 @@ for c in metric:diff_N40_B4096 diff1024:diff_N40_B1024 omni4:omni4_N40_B4096 tri
   t=${c%%:*}; k=${c#*:}
   for d in $B ${B}2 ${B}c; do
     if ls -d $d/${t}_pmc1 >/dev/null 2>&1; then
-      python3 tools/pmc_summary.py $d/$t "$k" --round r03 --last 10 --commit $C --write > /dev/null; break
+      python3 tools/pmc_summary.py $d/$t "$k" --round r03 --last 10 --commit $CB --write > /dev/null; break
     fi
   done
 done
