@@ -62,20 +62,34 @@ __device__ inline float fleet_u(const nmpc_fleet_renew& R, unsigned int gi, int 
     return (float)(fleet_hash(R.seed, gi, 16u * (unsigned int)e + (unsigned int)j) >> 8) * (1.0f / 16777216.0f);
 }
 
+// 16 lanes per robot (kLanes robots per 256-thread block): lane 0 runs the robot's scalar work (statistics, plant
+// step, renewal, nearest-point projection) and leaves the path parameters in LDS; then the robot's 16 lanes evaluate
+// its N+1 reference poses (pose k on lane k mod 16). One lane per robot with a serial pose loop took 17.6 us per
+// tick for 4096 robots on 16 CUs (profiles/r03/bench_metric_kernel_stats.csv).
+constexpr int kFleetLanes = 16;
+constexpr int kFleetBlock = 256;
+
 template <class M>
-__global__ void k_fleet_sim(KParams P, int B, int stride, float* path, float* s, float* pose, float* vel,
-                            float* steer, const float* u0, const int* status, const float* carried, float* traj,
-                            int* traj_len, int advance, nmpc_fleet_renew R, nmpc_fleet_stats S)
+__global__ __launch_bounds__(kFleetBlock) void k_fleet_sim(KParams P, int B, int stride, float* path, float* s,
+                                                          float* pose, float* vel, float* steer, const float* u0,
+                                                          const int* status, const float* carried, float* traj,
+                                                          int* traj_len, int advance, nmpc_fleet_renew R,
+                                                          nmpc_fleet_stats S)
 {
     constexpr int NX = M::NX, NU = M::NU;
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    constexpr int RPB = kFleetBlock / kFleetLanes;  // robots per block
+    const int lane = threadIdx.x % kFleetLanes, slot = threadIdx.x / kFleetLanes;
+    const int i = blockIdx.x * RPB + slot;
+    const bool lead = lane == 0 && i < B;
+    const size_t Bn = (size_t)B;
+    __shared__ float sh_sc[RPB], sh_len[RPB];
     if (S.qp_iter) {
         // the statistics of the solve this step follows (bench harness; replaces a dozen small launches per tick).
         // `reset` still holds the flags that solve ran with. The histogram goes through a block-local LDS copy.
         __shared__ unsigned int hist[64];
         if (threadIdx.x < 64) hist[threadIdx.x] = 0u;
         __syncthreads();
-        if (i < B) {
+        if (lead) {
             const int it = S.qp_iter[i];
             const long long cold = R.reset[i] ? 1 : 0;
             S.iters_sum[i] += it;
@@ -89,122 +103,131 @@ __global__ void k_fleet_sim(KParams P, int B, int stride, float* path, float* s,
         if (threadIdx.x < 64 && hist[threadIdx.x])
             atomicAdd((unsigned long long*)&S.hist[threadIdx.x], (unsigned long long)hist[threadIdx.x]);
     }
-    if (i >= B) return;
-    const size_t Bn = (size_t)B;
-    float ps[3] = {pose[i], pose[Bn + i], pose[2 * Bn + i]};
-    if (advance && (!status || status[i] == 0)) {
-        float v3[3] = {vel[i], vel[Bn + i], vel[2 * Bn + i]};
-        float x[NX], u[NU], xn[NX];
-        x[0] = ps[0];
-        x[1] = ps[1];
-        x[2] = ps[2];
-        M::direct_kin(v3, steer ? steer[i] : 0.0f, P, x + 3);
+    if (lead) {
+        float ps[3] = {pose[i], pose[Bn + i], pose[2 * Bn + i]};
+        if (advance && (!status || status[i] == 0)) {
+            float v3[3] = {vel[i], vel[Bn + i], vel[2 * Bn + i]};
+            float x[NX], u[NU], xn[NX];
+            x[0] = ps[0];
+            x[1] = ps[1];
+            x[2] = ps[2];
+            M::direct_kin(v3, steer ? steer[i] : 0.0f, P, x + 3);
 #pragma unroll
-        for (int j = 0; j < NU; j++) u[j] = u0[(size_t)j * Bn + i];
-        // ref states at the solve's x0 = carried (already advanced by the post-solve) - u0 * dt_ctrl
+            for (int j = 0; j < NU; j++) u[j] = u0[(size_t)j * Bn + i];
+            // ref states at the solve's x0 = carried (already advanced by the post-solve) - u0 * dt_ctrl
 #pragma unroll
-        for (int j = 0; j < M::NBX; j++) x[M::idxbx(j)] = carried[(size_t)j * stride + i] - u[j] * P.dt_ctrl;
-        rk4<M>(x, u, P, P.dt_ctrl, xn);
-        ps[0] = xn[0];
-        ps[1] = xn[1];
-        ps[2] = xn[2];
-        float nv[3];
-        if (M::ID == kDiff) {
-            nv[0] = 0.5f * (xn[3] + xn[4]);
-            nv[1] = 0.0f;
-            nv[2] = (xn[4] - xn[3]) / P.p[0];
-        } else if (M::ID == kOmni4) {
-            nv[0] = 0.25f * (xn[3] - xn[4] + xn[5] - xn[6]);
-            nv[1] = 0.25f * (-xn[3] - xn[4] + xn[5] + xn[6]);
-            nv[2] = -(xn[3] + xn[4] + xn[5] + xn[6]) / (2.0f * P.p[0]);
-        } else {
-            nv[0] = xn[3];
-            nv[1] = 0.0f;
-            nv[2] = 0.0f;
-            if (steer) steer[i] = xn[4];
-        }
-#pragma unroll
-        for (int j = 0; j < 3; j++) {
-            pose[(size_t)j * Bn + i] = ps[j];
-            vel[(size_t)j * Bn + i] = nv[j];
-        }
-    }
-    if (R.ev && advance) {
-        // the fleet manager: arrival (the end-of-trajectory test of processGoToPose / processFollowPath,
-        // NMPCNavControlROS.cpp:637-643 / :682-693; |heading error| where the reference compares the signed
-        // normAngRad) or the ttl of the current goal / path ends -> a new one, and reset_mpc on the next solve
-        float end[3];
-        if (path[5 * Bn + i] < 0.0f) {
-            end[0] = path[i];
-            end[1] = path[Bn + i];
-            end[2] = path[2 * Bn + i];
-        } else {
-            arc_pose(path, Bn, i, path[5 * Bn + i], end);
-        }
-        const float dx = ps[0] - end[0], dy = ps[1] - end[1];
-        const bool arrived = (dx * dx + dy * dy <= R.pos_tol * R.pos_tol) && fabsf(wrap_pi(ps[2] - end[2])) <= R.ang_tol;
-        const int ttl = R.ttl[i] - 1;
-        if (arrived || ttl <= 0) {
-            const int e = R.ev[i] + 1;
-            const unsigned int gi = (unsigned int)(R.start + i);
-            const float ua = fleet_u(R, gi, e, 0), ub = fleet_u(R, gi, e, 1), uc = fleet_u(R, gi, e, 2);
-            float sa, ca;
-            __sincosf(2.0f * kPi * ua, &sa, &ca);
-            if (path[5 * Bn + i] < 0.0f) {
-                const float rr = R.goal_r_lo + (R.goal_r_hi - R.goal_r_lo) * ub;
-                path[i] = ps[0] + rr * ca;
-                path[Bn + i] = ps[1] + rr * sa;
-                path[2 * Bn + i] = kPi * (2.0f * uc - 1.0f);
+            for (int j = 0; j < M::NBX; j++) x[M::idxbx(j)] = carried[(size_t)j * stride + i] - u[j] * P.dt_ctrl;
+            rk4<M>(x, u, P, P.dt_ctrl, xn);
+            ps[0] = xn[0];
+            ps[1] = xn[1];
+            ps[2] = xn[2];
+            float nv[3];
+            if (M::ID == kDiff) {
+                nv[0] = 0.5f * (xn[3] + xn[4]);
+                nv[1] = 0.0f;
+                nv[2] = (xn[4] - xn[3]) / P.p[0];
+            } else if (M::ID == kOmni4) {
+                nv[0] = 0.25f * (xn[3] - xn[4] + xn[5] - xn[6]);
+                nv[1] = 0.25f * (-xn[3] - xn[4] + xn[5] + xn[6]);
+                nv[2] = -(xn[3] + xn[4] + xn[5] + xn[6]) / (2.0f * P.p[0]);
             } else {
-                const float rr = 0.2f * ub;
-                path[i] = ps[0] + rr * ca;
-                path[Bn + i] = ps[1] + rr * sa;
-                path[2 * Bn + i] = ps[2] + 0.3f * (2.0f * uc - 1.0f);
-                path[3 * Bn + i] = R.kappa_max * (2.0f * fleet_u(R, gi, e, 3) - 1.0f);
-                path[4 * Bn + i] = R.speed_lo + (R.speed_hi - R.speed_lo) * fleet_u(R, gi, e, 4);
-                path[5 * Bn + i] = R.len_lo + (R.len_hi - R.len_lo) * fleet_u(R, gi, e, 5);
-                s[i] = 0.0f;
+                nv[0] = xn[3];
+                nv[1] = 0.0f;
+                nv[2] = 0.0f;
+                if (steer) steer[i] = xn[4];
             }
-            const unsigned long long span = (unsigned long long)(R.ttl_max - R.ttl_min + 1);
-            R.ttl[i] = R.ttl_min + (int)((unsigned long long)(fleet_hash(R.seed, gi, 16u * (unsigned int)e + 15u) >> 8) * span >> 24);
-            R.ev[i] = e;
-            R.reset[i] = 1;
-        } else {
-            R.ttl[i] = ttl;
-            R.reset[i] = 0;
+#pragma unroll
+            for (int j = 0; j < 3; j++) {
+                pose[(size_t)j * Bn + i] = ps[j];
+                vel[(size_t)j * Bn + i] = nv[j];
+            }
         }
+        if (R.ev && advance) {
+            // the fleet manager: arrival (the end-of-trajectory test of processGoToPose / processFollowPath,
+            // NMPCNavControlROS.cpp:637-643 / :682-693; |heading error| where the reference compares the signed
+            // normAngRad) or the ttl of the current goal / path ends -> a new one, and reset_mpc on the next solve
+            float end[3];
+            if (path[5 * Bn + i] < 0.0f) {
+                end[0] = path[i];
+                end[1] = path[Bn + i];
+                end[2] = path[2 * Bn + i];
+            } else {
+                arc_pose(path, Bn, i, path[5 * Bn + i], end);
+            }
+            const float dx = ps[0] - end[0], dy = ps[1] - end[1];
+            const bool arrived = (dx * dx + dy * dy <= R.pos_tol * R.pos_tol) && fabsf(wrap_pi(ps[2] - end[2])) <= R.ang_tol;
+            const int ttl = R.ttl[i] - 1;
+            if (arrived || ttl <= 0) {
+                const int e = R.ev[i] + 1;
+                const unsigned int gi = (unsigned int)(R.start + i);
+                const float ua = fleet_u(R, gi, e, 0), ub = fleet_u(R, gi, e, 1), uc = fleet_u(R, gi, e, 2);
+                float sa, ca;
+                __sincosf(2.0f * kPi * ua, &sa, &ca);
+                if (path[5 * Bn + i] < 0.0f) {
+                    const float rr = R.goal_r_lo + (R.goal_r_hi - R.goal_r_lo) * ub;
+                    path[i] = ps[0] + rr * ca;
+                    path[Bn + i] = ps[1] + rr * sa;
+                    path[2 * Bn + i] = kPi * (2.0f * uc - 1.0f);
+                } else {
+                    const float rr = 0.2f * ub;
+                    path[i] = ps[0] + rr * ca;
+                    path[Bn + i] = ps[1] + rr * sa;
+                    path[2 * Bn + i] = ps[2] + 0.3f * (2.0f * uc - 1.0f);
+                    path[3 * Bn + i] = R.kappa_max * (2.0f * fleet_u(R, gi, e, 3) - 1.0f);
+                    path[4 * Bn + i] = R.speed_lo + (R.speed_hi - R.speed_lo) * fleet_u(R, gi, e, 4);
+                    path[5 * Bn + i] = R.len_lo + (R.len_hi - R.len_lo) * fleet_u(R, gi, e, 5);
+                    s[i] = 0.0f;
+                }
+                const unsigned long long span = (unsigned long long)(R.ttl_max - R.ttl_min + 1);
+                R.ttl[i] = R.ttl_min + (int)((unsigned long long)(fleet_hash(R.seed, gi, 16u * (unsigned int)e + 15u) >> 8) * span >> 24);
+                R.ev[i] = e;
+                R.reset[i] = 1;
+            } else {
+                R.ttl[i] = ttl;
+                R.reset[i] = 0;
+            }
+        }
+        const float len = path[5 * Bn + i];
+        float sc = 0.0f;
+        if (len < 0.0f) {
+            // go-to-pose: the goal pose alone
+            traj[i] = path[i];
+            traj[Bn + i] = path[Bn + i];
+            traj[2 * Bn + i] = path[2 * Bn + i];
+            if (traj_len) traj_len[i] = 1;
+        } else {
+            // nearest point: a few projection steps from the previous progress (monotone, clamped to the path)
+            sc = s[i];
+            for (int itn = 0; itn < 3; itn++) {
+                float q[3];
+                arc_pose(path, Bn, i, sc, q);
+                float sn, cs;
+                __sincosf(q[2], &sn, &cs);
+                sc += (ps[0] - q[0]) * cs + (ps[1] - q[1]) * sn;
+                sc = fminf(fmaxf(sc, 0.0f), len);
+            }
+            sc = fmaxf(sc, s[i]);
+            s[i] = sc;
+            if (traj_len) traj_len[i] = P.N + 1;
+        }
+        sh_sc[slot] = sc;
+        sh_len[slot] = len;
     }
-    const int N = P.N;
-    const float len = path[5 * Bn + i];
-    if (len < 0.0f) {
-        // go-to-pose: the goal pose alone
-        traj[i] = path[i];
-        traj[Bn + i] = path[Bn + i];
-        traj[2 * Bn + i] = path[2 * Bn + i];
-        if (traj_len) traj_len[i] = 1;
-        return;
-    }
-    // nearest point: a few projection steps from the previous progress (monotone, clamped to the path)
-    float sc = s[i];
-    for (int itn = 0; itn < 3; itn++) {
-        float q[3];
-        arc_pose(path, Bn, i, sc, q);
-        float sn, cs;
-        __sincosf(q[2], &sn, &cs);
-        sc += (ps[0] - q[0]) * cs + (ps[1] - q[1]) * sn;
-        sc = fminf(fmaxf(sc, 0.0f), len);
-    }
-    sc = fmaxf(sc, s[i]);
-    s[i] = sc;
+    __syncthreads();
+    if (i >= B) return;
+    const float len = sh_len[slot];
+    if (len < 0.0f) return;
+    // the robot's N+1 reference poses on its 16 lanes (path[] of this robot was last written by its lead lane,
+    // before the barrier)
+    const float sc = sh_sc[slot];
     const float spacing = fabsf(path[4 * Bn + i]) * P.dt_ctrl;
-    for (int k = 0; k <= N; k++) {
+    for (int k = lane; k <= P.N; k += kFleetLanes) {
         float q[3];
         arc_pose(path, Bn, i, fminf(sc + (k + 1) * spacing, len), q);
         traj[((size_t)k * 3 + 0) * Bn + i] = q[0];
         traj[((size_t)k * 3 + 1) * Bn + i] = q[1];
         traj[((size_t)k * 3 + 2) * Bn + i] = q[2];
     }
-    if (traj_len) traj_len[i] = N + 1;
 }
 
 }  // namespace
@@ -215,13 +238,13 @@ hipError_t launch_fleet_sim(const KParams& P, int B, int stride, float* path, fl
                             int* traj_len, int advance, const nmpc_fleet_renew* renew, hipStream_t stream)
 {
     if (B <= 0) return hipSuccess;
-    const int block = 256;
+    constexpr int rpb = kFleetBlock / kFleetLanes;
     nmpc_fleet_renew R{};
     nmpc_fleet_stats S{};
     if (renew) R = *renew;
     if (renew && renew->stats) S = *renew->stats;
     R.stats = nullptr;  // host memory: the kernel gets S by value
-    hipLaunchKernelGGL(k_fleet_sim<M>, dim3((B + block - 1) / block), dim3(block), 0, stream, P, B, stride, path, s,
+    hipLaunchKernelGGL(k_fleet_sim<M>, dim3((B + rpb - 1) / rpb), dim3(kFleetBlock), 0, stream, P, B, stride, path, s,
                        pose, vel, steer, u0, status, carried, traj, traj_len, advance, R, S);
     return hipGetLastError();
 }
