@@ -30,9 +30,10 @@ __host__ __device__ inline unsigned int fleet_hash(unsigned int seed, unsigned i
 
 namespace {
 
-__device__ inline void arc_pose(const float* path, size_t Bn, int i, float s, float* out)
+// pose at arc length s of the arc path pp = {x0, y0, th0, kappa, ...}
+__device__ inline void arc_pose(const float* pp, float s, float* out)
 {
-    const float x0 = path[i], y0 = path[Bn + i], th0 = path[2 * Bn + i], kap = path[3 * Bn + i];
+    const float x0 = pp[0], y0 = pp[1], th0 = pp[2], kap = pp[3];
     const float th = th0 + kap * s;
     float s1, c1;
     __sincosf(th, &s1, &c1);
@@ -82,41 +83,52 @@ __global__ __launch_bounds__(kFleetBlock) void k_fleet_sim(KParams P, int B, int
     const int i = blockIdx.x * RPB + slot;
     const bool lead = lane == 0 && i < B;
     const size_t Bn = (size_t)B;
-    __shared__ float sh_sc[RPB], sh_len[RPB];
-    if (S.qp_iter) {
-        // the statistics of the solve this step follows (bench harness; replaces a dozen small launches per tick).
-        // `reset` still holds the flags that solve ran with. The histogram goes through a block-local LDS copy.
-        __shared__ unsigned int hist[64];
-        if (threadIdx.x < 64) hist[threadIdx.x] = 0u;
-        __syncthreads();
-        if (lead) {
+    __shared__ float sh_path[RPB][6], sh_sc[RPB];
+    __shared__ unsigned int hist[64];  // block-local histogram of the statistics (S.qp_iter)
+    if (threadIdx.x < 64) hist[threadIdx.x] = 0u;
+    __syncthreads();
+    if (lead) {
+        // the lead lane loads everything first: as far as the compiler knows every array may alias every other, so
+        // a load placed after a store waits for it (one memory round trip each)
+        const bool renew = R.ev && advance;
+        const int st_i = status ? status[i] : 0;
+        const unsigned char rs_i = (S.qp_iter || renew) ? R.reset[i] : 0;
+        float ps[3] = {pose[i], pose[Bn + i], pose[2 * Bn + i]};
+        float v3[3] = {vel[i], vel[Bn + i], vel[2 * Bn + i]};
+        const float st0 = steer ? steer[i] : 0.0f;
+        float u[NU], cr[M::NBX], pp[6];
+#pragma unroll
+        for (int j = 0; j < NU; j++) u[j] = advance ? u0[(size_t)j * Bn + i] : 0.0f;
+#pragma unroll
+        for (int j = 0; j < M::NBX; j++) cr[j] = advance ? carried[(size_t)j * stride + i] : 0.0f;
+#pragma unroll
+        for (int j = 0; j < 6; j++) pp[j] = path[(size_t)j * Bn + i];
+        float s_i = s[i];
+        const int ev_i = renew ? R.ev[i] : 0, ttl_i = renew ? R.ttl[i] : 0;
+        if (S.qp_iter) {
+            // the statistics of the solve this step follows (bench harness; replaces a dozen small launches per
+            // tick); `reset` still holds the flags that solve ran with
             const int it = S.qp_iter[i];
-            const long long cold = R.reset[i] ? 1 : 0;
-            S.iters_sum[i] += it;
-            S.iters_max[i] = max(S.iters_max[i], it);
-            S.fail_cnt[i] += status[i] != 0 ? 1 : 0;
-            S.cold_cnt[i] += cold;
-            S.cold_iters[i] += cold * it;
+            const long long cold = rs_i ? 1 : 0;
+            const long long isum = S.iters_sum[i], fcnt = S.fail_cnt[i], ccnt = S.cold_cnt[i];
+            const long long citer = S.cold_iters[i];
+            const int imax = S.iters_max[i];
+            S.iters_sum[i] = isum + it;
+            S.iters_max[i] = max(imax, it);
+            S.fail_cnt[i] = fcnt + (st_i != 0 ? 1 : 0);
+            S.cold_cnt[i] = ccnt + cold;
+            S.cold_iters[i] = citer + cold * it;
             atomicAdd(&hist[min(max(it, 0), 63)], 1u);
         }
-        __syncthreads();
-        if (threadIdx.x < 64 && hist[threadIdx.x])
-            atomicAdd((unsigned long long*)&S.hist[threadIdx.x], (unsigned long long)hist[threadIdx.x]);
-    }
-    if (lead) {
-        float ps[3] = {pose[i], pose[Bn + i], pose[2 * Bn + i]};
-        if (advance && (!status || status[i] == 0)) {
-            float v3[3] = {vel[i], vel[Bn + i], vel[2 * Bn + i]};
-            float x[NX], u[NU], xn[NX];
+        if (advance && st_i == 0) {
+            float x[NX], xn[NX];
             x[0] = ps[0];
             x[1] = ps[1];
             x[2] = ps[2];
-            M::direct_kin(v3, steer ? steer[i] : 0.0f, P, x + 3);
-#pragma unroll
-            for (int j = 0; j < NU; j++) u[j] = u0[(size_t)j * Bn + i];
+            M::direct_kin(v3, st0, P, x + 3);
             // ref states at the solve's x0 = carried (already advanced by the post-solve) - u0 * dt_ctrl
 #pragma unroll
-            for (int j = 0; j < M::NBX; j++) x[M::idxbx(j)] = carried[(size_t)j * stride + i] - u[j] * P.dt_ctrl;
+            for (int j = 0; j < M::NBX; j++) x[M::idxbx(j)] = cr[j] - u[j] * P.dt_ctrl;
             rk4<M>(x, u, P, P.dt_ctrl, xn);
             ps[0] = xn[0];
             ps[1] = xn[1];
@@ -142,42 +154,44 @@ __global__ __launch_bounds__(kFleetBlock) void k_fleet_sim(KParams P, int B, int
                 vel[(size_t)j * Bn + i] = nv[j];
             }
         }
-        if (R.ev && advance) {
+        if (renew) {
             // the fleet manager: arrival (the end-of-trajectory test of processGoToPose / processFollowPath,
             // NMPCNavControlROS.cpp:637-643 / :682-693; |heading error| where the reference compares the signed
             // normAngRad) or the ttl of the current goal / path ends -> a new one, and reset_mpc on the next solve
             float end[3];
-            if (path[5 * Bn + i] < 0.0f) {
-                end[0] = path[i];
-                end[1] = path[Bn + i];
-                end[2] = path[2 * Bn + i];
+            if (pp[5] < 0.0f) {
+                end[0] = pp[0];
+                end[1] = pp[1];
+                end[2] = pp[2];
             } else {
-                arc_pose(path, Bn, i, path[5 * Bn + i], end);
+                arc_pose(pp, pp[5], end);
             }
             const float dx = ps[0] - end[0], dy = ps[1] - end[1];
             const bool arrived = (dx * dx + dy * dy <= R.pos_tol * R.pos_tol) && fabsf(wrap_pi(ps[2] - end[2])) <= R.ang_tol;
-            const int ttl = R.ttl[i] - 1;
+            const int ttl = ttl_i - 1;
             if (arrived || ttl <= 0) {
-                const int e = R.ev[i] + 1;
+                const int e = ev_i + 1;
                 const unsigned int gi = (unsigned int)(R.start + i);
                 const float ua = fleet_u(R, gi, e, 0), ub = fleet_u(R, gi, e, 1), uc = fleet_u(R, gi, e, 2);
                 float sa, ca;
                 __sincosf(2.0f * kPi * ua, &sa, &ca);
-                if (path[5 * Bn + i] < 0.0f) {
+                if (pp[5] < 0.0f) {
                     const float rr = R.goal_r_lo + (R.goal_r_hi - R.goal_r_lo) * ub;
-                    path[i] = ps[0] + rr * ca;
-                    path[Bn + i] = ps[1] + rr * sa;
-                    path[2 * Bn + i] = kPi * (2.0f * uc - 1.0f);
+                    pp[0] = ps[0] + rr * ca;
+                    pp[1] = ps[1] + rr * sa;
+                    pp[2] = kPi * (2.0f * uc - 1.0f);
                 } else {
                     const float rr = 0.2f * ub;
-                    path[i] = ps[0] + rr * ca;
-                    path[Bn + i] = ps[1] + rr * sa;
-                    path[2 * Bn + i] = ps[2] + 0.3f * (2.0f * uc - 1.0f);
-                    path[3 * Bn + i] = R.kappa_max * (2.0f * fleet_u(R, gi, e, 3) - 1.0f);
-                    path[4 * Bn + i] = R.speed_lo + (R.speed_hi - R.speed_lo) * fleet_u(R, gi, e, 4);
-                    path[5 * Bn + i] = R.len_lo + (R.len_hi - R.len_lo) * fleet_u(R, gi, e, 5);
-                    s[i] = 0.0f;
+                    pp[0] = ps[0] + rr * ca;
+                    pp[1] = ps[1] + rr * sa;
+                    pp[2] = ps[2] + 0.3f * (2.0f * uc - 1.0f);
+                    pp[3] = R.kappa_max * (2.0f * fleet_u(R, gi, e, 3) - 1.0f);
+                    pp[4] = R.speed_lo + (R.speed_hi - R.speed_lo) * fleet_u(R, gi, e, 4);
+                    pp[5] = R.len_lo + (R.len_hi - R.len_lo) * fleet_u(R, gi, e, 5);
+                    s_i = 0.0f;
                 }
+#pragma unroll
+                for (int j = 0; j < 6; j++) path[(size_t)j * Bn + i] = pp[j];
                 const unsigned long long span = (unsigned long long)(R.ttl_max - R.ttl_min + 1);
                 R.ttl[i] = R.ttl_min + (int)((unsigned long long)(fleet_hash(R.seed, gi, 16u * (unsigned int)e + 15u) >> 8) * span >> 24);
                 R.ev[i] = e;
@@ -187,43 +201,46 @@ __global__ __launch_bounds__(kFleetBlock) void k_fleet_sim(KParams P, int B, int
                 R.reset[i] = 0;
             }
         }
-        const float len = path[5 * Bn + i];
+        const float len = pp[5];
         float sc = 0.0f;
         if (len < 0.0f) {
             // go-to-pose: the goal pose alone
-            traj[i] = path[i];
-            traj[Bn + i] = path[Bn + i];
-            traj[2 * Bn + i] = path[2 * Bn + i];
+            traj[i] = pp[0];
+            traj[Bn + i] = pp[1];
+            traj[2 * Bn + i] = pp[2];
             if (traj_len) traj_len[i] = 1;
         } else {
             // nearest point: a few projection steps from the previous progress (monotone, clamped to the path)
-            sc = s[i];
+            sc = s_i;
             for (int itn = 0; itn < 3; itn++) {
                 float q[3];
-                arc_pose(path, Bn, i, sc, q);
+                arc_pose(pp, sc, q);
                 float sn, cs;
                 __sincosf(q[2], &sn, &cs);
                 sc += (ps[0] - q[0]) * cs + (ps[1] - q[1]) * sn;
                 sc = fminf(fmaxf(sc, 0.0f), len);
             }
-            sc = fmaxf(sc, s[i]);
+            sc = fmaxf(sc, s_i);
             s[i] = sc;
             if (traj_len) traj_len[i] = P.N + 1;
         }
+#pragma unroll
+        for (int j = 0; j < 6; j++) sh_path[slot][j] = pp[j];
         sh_sc[slot] = sc;
-        sh_len[slot] = len;
     }
     __syncthreads();
+    if (S.qp_iter && threadIdx.x < 64 && hist[threadIdx.x])
+        atomicAdd((unsigned long long*)&S.hist[threadIdx.x], (unsigned long long)hist[threadIdx.x]);
     if (i >= B) return;
-    const float len = sh_len[slot];
+    const float* pp = sh_path[slot];
+    const float len = pp[5];
     if (len < 0.0f) return;
-    // the robot's N+1 reference poses on its 16 lanes (path[] of this robot was last written by its lead lane,
-    // before the barrier)
+    // the robot's N+1 reference poses on its 16 lanes
     const float sc = sh_sc[slot];
-    const float spacing = fabsf(path[4 * Bn + i]) * P.dt_ctrl;
+    const float spacing = fabsf(pp[4]) * P.dt_ctrl;
     for (int k = lane; k <= P.N; k += kFleetLanes) {
         float q[3];
-        arc_pose(path, Bn, i, fminf(sc + (k + 1) * spacing, len), q);
+        arc_pose(pp, fminf(sc + (k + 1) * spacing, len), q);
         traj[((size_t)k * 3 + 0) * Bn + i] = q[0];
         traj[((size_t)k * 3 + 1) * Bn + i] = q[1];
         traj[((size_t)k * 3 + 2) * Bn + i] = q[2];
