@@ -88,9 +88,13 @@ constexpr int kStampItsC = 0;
 // SD: one direction per IPM iteration (P1 builds the rhs with the centring target sigma mu, one forward sweep
 // computes the direction, the step and the complementarity polynomial that predicts the next mu) instead of
 // Mehrotra's predictor-corrector (P1 + F0 + C1 + F1 sweeps)
-template <class M, bool MS, bool SD>
-__global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int mode)
+// MODE (kModeSolve / kModeRun) is a template parameter: as a runtime argument its branches inside P0's stage loop
+// (reference unwrap, yref or pose-reference loads) made the compiler's waits at their joins drain the whole memory
+// counter, the stage's record stores and the prefetched rows included
+template <class M, bool MS, bool SD, int MODE>
+__global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a)
 {
+    constexpr int mode = MODE;
     using R = TeamRec<M, SD>;
     constexpr int NX = M::NX, NU = M::NU, NV = R::NV, NGV = R::NGV, RS = R::RS;
     constexpr bool QM = rec_quad_major<NV>();
@@ -333,9 +337,11 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
     float dx = is_x ? x0_lane - XB(0, xi) : 0.0f;  // this lane's state delta at the current stage
     float sum_c0 = 0.0f;  // complementarity of the initial point (its mean sets the first SD target)
     // warm start: the previous multipliers (LL, LU) of the stage, prefetched one stage ahead
+    // (an unconditional load and a select: a load under the team's warm flag is masked per team, and the
+    // compiler's waits for every later load of the loop then drain the whole memory counter)
     auto load_l = [&](int k) -> float2 {
-        return warm ? *reinterpret_cast<const float2*>(tbase + (size_t)(k <= N ? k : N) * KS + rec_off<RS, QM>(R::LL))
-                    : make_float2(0.0f, 0.0f);
+        const float2 v = *reinterpret_cast<const float2*>(tbase + (size_t)(k <= N ? k : N) * KS + rec_off<RS, QM>(R::LL));
+        return warm ? v : make_float2(0.0f, 0.0f);
     };
     // One stage of the serial pass: reference (run mode: unwrap + pad), cost gradient, bounds / slacks /
     // multipliers, the stage record, and the dynamics-feasible initial state of the next stage. Inputs: this
@@ -347,15 +353,14 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
         // entries >= 3 of yref are left at zero
         float yr = yr_in;
         if (mode == kModeRun) {
-            if (k < len) {
-                ref_x = trk[0];
-                ref_y = trk[1];
-                float th = trk[2];
-                const float d = th - ref_t;
-                if (d > kPi) th -= 2.0f * kPi;
-                else if (d < -kPi) th += 2.0f * kPi;
-                ref_t = th;
-            }
+            // branch-free (selects): a divergent branch here (len is per team) made the compiler's waits at its
+            // join drain the whole memory counter, the stage's record stores included
+            const bool in = k < len;
+            const float th = trk[2], d = th - ref_t;
+            const float thu = (d > kPi) ? th - 2.0f * kPi : ((d < -kPi) ? th + 2.0f * kPi : th);
+            ref_x = in ? trk[0] : ref_x;
+            ref_y = in ? trk[1] : ref_y;
+            ref_t = in ? thu : ref_t;
             if (k == N - 1) { prv_x = ref_x; prv_y = ref_y; prv_t = ref_t; }
             yr = (is_x && xi == 0) ? ref_x : ((is_x && xi == 1) ? ref_y : ((is_x && xi == 2) ? ref_t : 0.0f));
         }
@@ -413,7 +418,12 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a, int
         // diff (7 idle lanes, +78 % P0 store bytes) 1.043 -> 1.065 ms, so 9-slot teams keep the masked store
         // (profiles/r02/ab/uncond_stores.txt)
         if constexpr (NV > 12) rec_store<RS, QM>(tbase_own + (size_t)k * KS, rec);
+#ifdef P0_MASKED_STORE
         else if (lv) rec_store<RS, QM>(tbase + (size_t)k * KS, rec);
+#else
+        // 9-slot teams: the idle lanes all store into the team's dummy record (one record's bytes, not seven)
+        else rec_store<RS, QM>(lv ? tbase + (size_t)k * KS : tdummy, rec);
+#endif
         if constexpr (kDzPlane) dzbase[(size_t)k * 16] = 0.0f;  // P1 of iteration 0 applies a zero step
         // dynamics-feasible initial states: dx_{k+1} = A dx_k + b_k (inputs start at du = 0, dx_0 = x0 - xbar_0);
         // row i of [B A] dz: NGV row sums over the columns + the constant rows held in grow
@@ -1072,15 +1082,15 @@ hipError_t launch_sqp_rti_team(const KParams& P, const KArgs& a, int mode, hipSt
     const size_t lds = as.split ? split_lds
                                 : ((mode == kModeRun && a.segs) ? (sizeof(double) + 3 * sizeof(float)) * 16 * (size_t)(P.N + 1) : 0);
     if (lds > 65536) return hipErrorInvalidValue;
+    auto go = [&](auto kern) { hipLaunchKernelGGL(kern, dim3(grid), dim3(block), lds, stream, P, as); };
+    const bool run = mode == kModeRun;
     if (P.ipm == 1) {
-        if (a.dense)
-            hipLaunchKernelGGL((k_sqp_rti_team<M, true, true>), dim3(grid), dim3(block), lds, stream, P, as, mode);
-        else
-            hipLaunchKernelGGL((k_sqp_rti_team<M, false, true>), dim3(grid), dim3(block), lds, stream, P, as, mode);
+        if (a.dense) run ? go(k_sqp_rti_team<M, true, true, kModeRun>) : go(k_sqp_rti_team<M, true, true, kModeSolve>);
+        else run ? go(k_sqp_rti_team<M, false, true, kModeRun>) : go(k_sqp_rti_team<M, false, true, kModeSolve>);
     } else if (a.dense) {
-        hipLaunchKernelGGL((k_sqp_rti_team<M, true, false>), dim3(grid), dim3(block), lds, stream, P, as, mode);
+        run ? go(k_sqp_rti_team<M, true, false, kModeRun>) : go(k_sqp_rti_team<M, true, false, kModeSolve>);
     } else {
-        hipLaunchKernelGGL((k_sqp_rti_team<M, false, false>), dim3(grid), dim3(block), lds, stream, P, as, mode);
+        run ? go(k_sqp_rti_team<M, false, false, kModeRun>) : go(k_sqp_rti_team<M, false, false, kModeSolve>);
     }
     return hipGetLastError();
 }

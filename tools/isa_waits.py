@@ -1,6 +1,6 @@
 """Memory-counter waits in the gfx950 ISA of the solve kernel, per loop (a development check for the sweep loops).
 
-usage: python tools/isa_waits.py [--kernel Diff2ELb0ELb1] [--flags "-DFOO"] [--all]
+usage: python tools/isa_waits.py [--kernel Diff2ELb0ELb1ELi1] [--flags "-DFOO"] [--all]
 Compiles csrc/sqp_rti_team.hip to device assembly with the product flags (+ --flags), takes one kernel
 instantiation and prints, for every loop, its header label, depth, instruction count, the number of fp64 DPP
 FMAs (the P1 factorisation loop is the one with ~120) and every s_waitcnt vmcnt in it with its line."""
@@ -51,7 +51,7 @@ def loops(lines):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--kernel", default="Diff2ELb0ELb1")
+    ap.add_argument("--kernel", default="Diff2ELb0ELb1ELi1")  # diff, not dense, single-direction, run mode
     ap.add_argument("--flags", default="")
     ap.add_argument("--all", action="store_true", help="every loop, not only those with vmcnt waits")
     ap.add_argument("--asm", default="/tmp/isa_waits.s")
