@@ -889,10 +889,14 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a)
                 const bool vu = is_u && k < N;
                 const bool vx = is_x && k >= 1;
                 const bool valid = vu || vx;
+                // NU = 2: computed at every stage and zeroed at k = N (a select): under `if (k < N)` the compiler
+                // sank the first stage's LR / LM load into the branch and waited for it (and every prefetch) at once
+                // (same-box: metric +0.4 %, tric +1.1 %; omni4's longer substitution lost 0.6 %, so NU = 4 keeps
+                // the branch; profiles/r03/ab/f1_uncond.txt)
                 float du_all[NU];
 #pragma unroll
                 for (int q = 0; q < NU; q++) du_all[q] = 0.0f;
-                if (k < N) {
+                if (NU == 2 || k < N) {
                     float w[NU];
                     sfor<0, NU>([&](auto qc) {
                         constexpr int q = decltype(qc)::value;
@@ -908,7 +912,7 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a)
                         du_all[q] = sq * frcp(bc<q>(rc[R::LM + q]));
                     });
 #pragma unroll
-                    for (int q = 0; q < NU; q++) du_all[q] = -du_all[q];
+                    for (int q = 0; q < NU; q++) du_all[q] = (k < N) ? -du_all[q] : 0.0f;
                 }
                 float dz = 0.0f;
 #pragma unroll
