@@ -947,9 +947,12 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a)
                         s2 += bnd ? d.dll * d.dtl + d.dlu * d.dtu : 0.0f;
                     }
                 }
-                if (ld && valid) {
-                    if (corr && kDzPlane) dzbase[(size_t)k * 16] = dz;
-                    else tbase[(size_t)k * KS + (!corr ? rec_off<RS, QM>(R::DZA) : rec_off<RS, QM>(R::DZ))] = dz;
+                {  // unconditional (lanes without a direction write the dummy record): a masked store here left
+                   // the compiler's wait after the sweep a full drain
+                    const bool st = ld && valid;
+                    if (corr && kDzPlane) *(st ? dzbase + (size_t)k * 16 : tdummy) = dz;
+                    else *(st ? tbase + (size_t)k * KS + (!corr ? rec_off<RS, QM>(R::DZA) : rec_off<RS, QM>(R::DZ))
+                              : tdummy) = dz;
                 }
                 if (k < N) dxs = dyn(rc, valid ? dz : 0.0f);
             });
