@@ -88,13 +88,18 @@ constexpr int kStampItsC = 0;
 // SD: one direction per IPM iteration (P1 builds the rhs with the centring target sigma mu, one forward sweep
 // computes the direction, the step and the complementarity polynomial that predicts the next mu) instead of
 // Mehrotra's predictor-corrector (P1 + F0 + C1 + F1 sweeps)
-// MODE (kModeSolve / kModeRun) is a template parameter: as a runtime argument its branches inside P0's stage loop
-// (reference unwrap, yref or pose-reference loads) made the compiler's waits at their joins drain the whole memory
-// counter, the stage's record stores and the prefetched rows included
+// zeros: the source of a cold robot's warm-start multiplier loads (load_l in P0)
+__device__ float g_zero4[4];
+
+// MODE is a template parameter: kModeSolve, kModeRun, or kModeRunPath (run mode with the in-kernel path march,
+// a.segs set). As runtime arguments their branches inside P0's stage loop (reference unwrap, yref or pose-reference
+// loads, and a pose load from either LDS or global memory, i.e. a flat load) made the compiler's waits drain the
+// whole memory counter, the stage's record stores and the prefetched rows included
+constexpr int kModeRunPath = 2;
 template <class M, bool MS, bool SD, int MODE>
 __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a)
 {
-    constexpr int mode = MODE;
+    constexpr int mode = MODE == kModeRunPath ? kModeRun : MODE;
     using R = TeamRec<M, SD>;
     constexpr int NX = M::NX, NU = M::NU, NV = R::NV, NGV = R::NGV, RS = R::RS;
     constexpr bool QM = rec_quad_major<NV>();
@@ -166,7 +171,7 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a)
     // LDS: path mode and split run launches: [teams][N+1] path parameters, then [teams][N+1][3] float poses
     // (split: one team); split launches then the serial P0 pass's stage inputs
     extern __shared__ double s_path[];
-    const bool path = (mode == kModeRun) && a.segs;
+    constexpr bool path = MODE == kModeRunPath;  // (the launcher picks it exactly when a.segs is set)
     const bool traj_lds = path || (a.split && mode == kModeRun);
     const int nslot = a.split ? 1 : 16;
     const int tslot = a.split ? 0 : (int)(threadIdx.x >> 4);
@@ -337,11 +342,12 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a)
     float dx = is_x ? x0_lane - XB(0, xi) : 0.0f;  // this lane's state delta at the current stage
     float sum_c0 = 0.0f;  // complementarity of the initial point (its mean sets the first SD target)
     // warm start: the previous multipliers (LL, LU) of the stage, prefetched one stage ahead
-    // (an unconditional load and a select: a load under the team's warm flag is masked per team, and the
-    // compiler's waits for every later load of the loop then drain the whole memory counter)
+    // (the flag selects the address, not the value: a cold team reads a zero pair. A load whose value is only
+    // used under the team's warm flag is issued under that lane mask, and the compiler's waits for every later load
+    // of the loop then drain the whole memory counter)
     auto load_l = [&](int k) -> float2 {
-        const float2 v = *reinterpret_cast<const float2*>(tbase + (size_t)(k <= N ? k : N) * KS + rec_off<RS, QM>(R::LL));
-        return warm ? v : make_float2(0.0f, 0.0f);
+        const float* const src = warm ? tbase + (size_t)(k <= N ? k : N) * KS + rec_off<RS, QM>(R::LL) : g_zero4;
+        return *reinterpret_cast<const float2*>(src);
     };
     // One stage of the serial pass: reference (run mode: unwrap + pad), cost gradient, bounds / slacks /
     // multipliers, the stage record, and the dynamics-feasible initial state of the next stage. Inputs: this
@@ -470,39 +476,71 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a)
             cur = nxt;
         }
     } else {
-        float2 lprev = load_l(0);
-        for (int k = 0; k <= N; k++) {
-            const float2 lp = lprev;
-            lprev = load_l(k + 1);
-            float xb2[NX], ub2[NU], tr2[3];
-            load_row(k + 2, xb2, ub2, tr2);  // two stages ahead (clamped)
-            float yr = 0.0f;
-            if (mode != kModeRun) {
+        // three row buffers used in turn (the loop unrolled by 3, compile-time buffer indices): buffer i holds stage
+        // k + i while the loop is at stage k and is refilled with stage k + 3 after its body. A rotation by copies
+        // (xb = xb1; xb1 = xb2) copied registers whose loads were still in flight, and each copy waited for every
+        // memory operation issued before it (a full drain per stage)
+        struct Row {
+            float xb[NX], ub[NU], tr[3], yr;
+            float2 lp;
+        };
+        auto load_p0 = [&](int k, Row& o) {
+            load_row(k, o.xb, o.ub, o.tr);
+            o.lp = load_l(k);
+            o.yr = 0.0f;
+            if (mode != kModeRun) {  // (unconditional load of a valid entry, then a select)
+                const int kk = k <= N ? k : N;
                 const int j = is_u ? NX + r : xi;
-                yr = (lv && j < a.ny_in) ? a.yref[((size_t)k * a.ny_in + j) * Bn + inst] : 0.0f;
+                const bool use = lv && j < a.ny_in;
+                const float v = a.yref[((size_t)kk * a.ny_in + (use ? j : 0)) * Bn + inst];
+                o.yr = use ? v : 0.0f;
             }
-            float xn[NX], g[NX];
+        };
+        Row rw[3];
 #pragma unroll
-            for (int i = 0; i < NX; i++) { xn[i] = 0.0f; g[i] = 0.0f; }
-            if (k < N) rk4_column<M>(xb, ub, P, lv ? r : NU, xn, g);
-            float zbar = 0.0f;
+        for (int j = 0; j < NX; j++) { rw[0].xb[j] = xb[j]; rw[1].xb[j] = xb1[j]; }
 #pragma unroll
-            for (int j = 0; j < NU; j++)
-                if (r == j) zbar = ub[j];
+        for (int j = 0; j < NU; j++) { rw[0].ub[j] = ub[j]; rw[1].ub[j] = ub1[j]; }
 #pragma unroll
-            for (int j = 0; j < NX; j++)
-                if (is_x && xi == j) zbar = xb[j];
-            float bk = 0.0f;
+        for (int j = 0; j < 3; j++) { rw[0].tr[j] = tr[j]; rw[1].tr[j] = tr1[j]; }
+        rw[0].lp = load_l(0);
+        rw[1].lp = load_l(1);
+        rw[0].yr = rw[1].yr = 0.0f;
+        if (mode != kModeRun) {
+            Row t0, t1;
+            load_p0(0, t0);
+            load_p0(1, t1);
+            rw[0].yr = t0.yr;
+            rw[1].yr = t1.yr;
+        }
+        for (int k0 = 0;; k0 += 3) {
+            bool stop = false;
+            sfor<0, 3>([&](auto ic) {
+                constexpr int i = decltype(ic)::value;
+                if (stop) return;
+                const int k = k0 + i;
+                load_p0(k + 2, rw[(i + 2) % 3]);  // two stages ahead (clamped)
+                const Row& c = rw[i];
+                const Row& n1 = rw[(i + 1) % 3];
+                float xn[NX], g[NX];
 #pragma unroll
-            for (int i = 0; i < NX; i++)
-                if (xi == i) bk = xn[i] - xb1[i];
-            p0_body(k, zbar, yr, tr, lp, g, bk);
+                for (int q = 0; q < NX; q++) { xn[q] = 0.0f; g[q] = 0.0f; }
+                if (k < N) rk4_column<M>(c.xb, c.ub, P, lv ? r : NU, xn, g);
+                float zbar = 0.0f;
 #pragma unroll
-            for (int j = 0; j < NX; j++) { xb[j] = xb1[j]; xb1[j] = xb2[j]; }
+                for (int j = 0; j < NU; j++)
+                    if (r == j) zbar = c.ub[j];
 #pragma unroll
-            for (int j = 0; j < NU; j++) { ub[j] = ub1[j]; ub1[j] = ub2[j]; }
+                for (int j = 0; j < NX; j++)
+                    if (is_x && xi == j) zbar = c.xb[j];
+                float bk = 0.0f;
 #pragma unroll
-            for (int j = 0; j < 3; j++) { tr[j] = tr1[j]; tr1[j] = tr2[j]; }
+                for (int q = 0; q < NX; q++)
+                    if (xi == q) bk = xn[q] - n1.xb[q];
+                p0_body(k, zbar, c.yr, c.tr, c.lp, g, bk);
+                if (k == N) stop = true;
+            });
+            if (stop) break;
         }
     }
     // e_r: places the diagonal D of M = D + G'PG with one multiply per entry instead of two selects (same-box
@@ -1090,14 +1128,23 @@ hipError_t launch_sqp_rti_team(const KParams& P, const KArgs& a, int mode, hipSt
                                 : ((mode == kModeRun && a.segs) ? (sizeof(double) + 3 * sizeof(float)) * 16 * (size_t)(P.N + 1) : 0);
     if (lds > 65536) return hipErrorInvalidValue;
     auto go = [&](auto kern) { hipLaunchKernelGGL(kern, dim3(grid), dim3(block), lds, stream, P, as); };
-    const bool run = mode == kModeRun;
+    // compile-time mode (the kernel's MODE parameter)
+    const int km = mode != kModeRun ? kModeSolve : (a.segs ? kModeRunPath : kModeRun);
+    auto pick = [&](auto msc, auto sdc) {
+        constexpr bool ms = decltype(msc)::value, sd = decltype(sdc)::value;
+        if (km == kModeRunPath) go(k_sqp_rti_team<M, ms, sd, kModeRunPath>);
+        else if (km == kModeRun) go(k_sqp_rti_team<M, ms, sd, kModeRun>);
+        else go(k_sqp_rti_team<M, ms, sd, kModeSolve>);
+    };
+    using T = std::true_type;
+    using F = std::false_type;
     if (P.ipm == 1) {
-        if (a.dense) run ? go(k_sqp_rti_team<M, true, true, kModeRun>) : go(k_sqp_rti_team<M, true, true, kModeSolve>);
-        else run ? go(k_sqp_rti_team<M, false, true, kModeRun>) : go(k_sqp_rti_team<M, false, true, kModeSolve>);
+        if (a.dense) pick(T{}, T{});
+        else pick(F{}, T{});
     } else if (a.dense) {
-        run ? go(k_sqp_rti_team<M, true, false, kModeRun>) : go(k_sqp_rti_team<M, true, false, kModeSolve>);
+        pick(T{}, F{});
     } else {
-        run ? go(k_sqp_rti_team<M, false, false, kModeRun>) : go(k_sqp_rti_team<M, false, false, kModeSolve>);
+        pick(F{}, F{});
     }
     return hipGetLastError();
 }

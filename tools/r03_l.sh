@@ -4,4 +4,4 @@
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out/r03l
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 240 --timeout-method thread > gpurun_out/r03l/tests.log 2>&1 || exit $?
-timeout -k 10 1000 python tools/ab_env.py r03l/dz "metric diff1024 omni4 tric" base=NMPC_AMD_LIB=@ROOT/nmpc_nav_control_amd/lib/base/libnmpc_amd.so --reps=2
+timeout -k 10 1000 python tools/ab_env.py r03l/p0b "metric diff1024 omni4 tric" base=NMPC_AMD_LIB=@ROOT/nmpc_nav_control_amd/lib/base/libnmpc_amd.so --reps=2
