@@ -4,7 +4,6 @@
 
 #include <hip/hip_runtime.h>
 
-#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -36,14 +35,6 @@ struct nmpc_batch {
     unsigned char* warm = nullptr;  // [capacity] the robot's last solve succeeded: its scratch records hold its
                                     // multipliers (IPM warm start)
     int* sorted = nullptr;       // [capacity] sort scratch
-    // tail hand-off of unsplit team launches (single-direction rule): robots still iterating at the top of IPM
-    // iteration hand_cap (0 = never) finish in the row-parallel tail launch of hand_grid_max blocks (DESIGN.md
-    // section 4, "Tail hand-off")
-    int hand_cap = 0;
-    int hand_grid_max = 512;
-    int* hand_count = nullptr;   // [2]
-    int* hand_list = nullptr;    // [capacity]
-    float* hand_state = nullptr; // [capacity][kHandStride]
 };
 
 namespace {
@@ -121,35 +112,12 @@ size_t scratch_floats(int model, int N, int stride)
     }
 }
 
-// the team launch, then (hand-off armed) the tail launch over the robots it handed off
 template <class M>
-hipError_t launch_team_tail(nmpc_batch* b, KArgs& a, int mode, hipStream_t s)
-{
-    const bool hand = b->hand_cap > 0 && b->hand_cap < b->kp.iter_max && b->kp.ipm == NMPC_IPM_SINGLE &&
-                      rowpar_lds_bytes<M>(b->prm.N, mode) <= 65536;
-    if (hand) {
-        a.hand_cap = b->hand_cap;
-        a.hand_count = b->hand_count;
-        a.hand_list = b->hand_list;
-        a.hand_state = b->hand_state;
-    }
-    hipError_t e = launch_sqp_rti_team<M>(b->kp, a, mode, s);
-    if (e != hipSuccess || !hand) return e;
-    KArgs t = a;
-    t.hand_grid = a.B < b->hand_grid_max ? a.B : b->hand_grid_max;
-    e = launch_sqp_rti_rowpar<M>(b->kp, t, mode, s);
-    if (e != hipSuccess) (void)hipMemsetAsync(b->hand_count, 0, 2 * sizeof(int), s);  // keep the list empty
-    return e;
-}
-
-template <class M>
-hipError_t launch_m(nmpc_batch* b, KArgs& a, int mode, hipStream_t s)
+hipError_t launch_m(nmpc_batch* b, const KArgs& a, int mode, hipStream_t s)
 {
     if (a.rowpar) return launch_sqp_rti_rowpar<M>(b->kp, a, mode, s);
-    if (!a.split) return launch_team_tail<M>(b, a, mode, s);
     return launch_sqp_rti_team<M>(b->kp, a, mode, s);
 }
-
 
 template <class M>
 bool rowpar_ok(const nmpc_batch* b, const KArgs& a, int mode)
@@ -363,8 +331,6 @@ int nmpc_batch_create(const nmpc_model_params* prm, int capacity, nmpc_batch** o
     }
     if (const char* v = std::getenv("NMPC_AMD_SPLIT_MAX")) b->split_max = std::atoi(v);  // A/B: 0 = never split
     if (const char* v = std::getenv("NMPC_AMD_ROWPAR_MAX")) b->rowpar_max = std::atoi(v);  // A/B: 0 = never
-    if (const char* v = std::getenv("NMPC_AMD_HAND_CAP")) b->hand_cap = std::atoi(v);      // A/B: 0 = never
-    if (const char* v = std::getenv("NMPC_AMD_HAND_GRID")) b->hand_grid_max = std::max(1, std::atoi(v));
     const int N = prm->N;
     const size_t S = (size_t)capacity;
     hipError_t e;
@@ -378,10 +344,6 @@ int nmpc_batch_create(const nmpc_model_params* prm, int capacity, nmpc_batch** o
         (e = hipMalloc(&b->sorted, sizeof(int) * S)) != hipSuccess ||
         (e = hipMemset(b->iter_key, 0, sizeof(int) * S)) != hipSuccess ||
         (e = hipMalloc(&b->warm, S)) != hipSuccess || (e = hipMemset(b->warm, 0, S)) != hipSuccess ||
-        (e = hipMalloc(&b->hand_count, 2 * sizeof(int))) != hipSuccess ||
-        (e = hipMemset(b->hand_count, 0, 2 * sizeof(int))) != hipSuccess ||
-        (e = hipMalloc(&b->hand_list, sizeof(int) * S)) != hipSuccess ||
-        (e = hipMalloc(&b->hand_state, sizeof(float) * kHandStride * S)) != hipSuccess ||
         (e = hipMalloc(&b->xbar, sizeof(float) * (N + 1) * b->nx * S)) != hipSuccess ||
         (e = hipMalloc(&b->ubar, sizeof(float) * N * b->nu * S)) != hipSuccess ||
         (e = hipMalloc(&b->carried, sizeof(float) * b->nbx * S)) != hipSuccess ||
@@ -410,9 +372,6 @@ int nmpc_batch_destroy(nmpc_batch* b)
     (void)hipFree(b->order);
     (void)hipFree(b->sorted);
     (void)hipFree(b->warm);
-    (void)hipFree(b->hand_count);
-    (void)hipFree(b->hand_list);
-    (void)hipFree(b->hand_state);
     delete b;
     return NMPC_OK;
 }

@@ -59,15 +59,7 @@ struct KArgs {
     int rowpar;     // 0: team kernel; W > 0: k_sqp_rti_rowpar with W waves per robot
     int split;      // one 256-lane block per robot: P0's integrations spread over its 16 rows (4 waves, stage k on
                     // row k mod 16, joined by a block barrier); small batches
-    // tail hand-off (team kernel, single-direction rule): a team still iterating at the top of IPM iteration
-    // hand_cap (> 0) stops there, appends its robot to hand_list and leaves its IPM scalars in hand_state; the
-    // row-parallel tail launch (hand_grid blocks of four waves) finishes those robots' solves
-    int hand_cap, hand_grid;
-    int* hand_count;   // [2] device: list length, finished tail blocks (both zero between launches)
-    int* hand_list;    // [stride] robots handed off by the last team launch
-    float* hand_state; // [stride][kHandStride]
 };
-constexpr int kHandStride = 32;
 
 template <class M>
 size_t team_scratch_floats(int N, int stride);

@@ -85,16 +85,14 @@ __device__ __forceinline__ float wave_min_rows(float v)
 // W waves per robot (one per SIMD): the stage-parallel phases run on all 4 W rows; every wave runs the serial
 // phases (identically) and wave 0 stores their results (the other waves store into dummy stage blocks of the same
 // layout: per-lane scattered dummy addresses made the serial phases' stores 1.6x slower, measured)
-// RESUME: continue the IPM of a robot the team kernel handed off (KArgs::hand_cap): its records, the DZ plane and
-// the iterate are as the team kernel left them at the top of IPM iteration hand_cap, and the scalars of that point
-// (step, targets, previous mu, terminal weights) are in its hand_state row; P0 is not repeated
-template <class M, int W, bool RESUME>
-__device__ __forceinline__ void rowpar_robot(const KParams& P, const KArgs& a, int mode, int inst)
+template <class M, int W>
+__global__ __launch_bounds__(64 * W, 1) void k_sqp_rti_rowpar(KParams P, KArgs a, int mode)
 {
     using R = RowRec<M>;
     constexpr int NX = M::NX, NU = M::NU, NV = R::NV, NGV = R::NGV, RS = R::RS;
     constexpr bool QM = rec_quad_major<NV>();
     constexpr int ROWS = 4 * W;
+    const int inst = (int)blockIdx.x;
     if (inst >= a.B) return;
     const int tid = (int)threadIdx.x;
     const int wave = tid >> 6;
@@ -142,7 +140,7 @@ __device__ __forceinline__ void rowpar_robot(const KParams& P, const KArgs& a, i
 #define UBAR(k, j) a.ubar[((size_t)(k) * NU + (j)) * S + inst]
 
     // ---- reset ({name}_acados_reset: zero iterate) ----------------------------------------------------------
-    if (!RESUME && a.reset && a.reset[inst]) {
+    if (a.reset && a.reset[inst]) {
         for (int e = tid; e < (N + 1) * NX; e += 64 * W) XB(e / NX, e % NX) = 0.0f;
         for (int e = tid; e < N * NU; e += 64 * W) UBAR(e / NU, e % NU) = 0.0f;
         __syncthreads();
@@ -172,10 +170,6 @@ __device__ __forceinline__ void rowpar_robot(const KParams& P, const KArgs& a, i
         if (xi == j) x0_lane = x0[j];
     float we_lane = 0.0f;
     if (is_x) we_lane = (mode != kModeRun && a.We) ? a.We[(size_t)xi * Bn + inst] : P.We[xi];
-    // the hand-off row: [0, 16) the team lanes' terminal weights (the diff terminal hack applied), then the step,
-    // the direction's target, the next target, the previous mu and the iteration count
-    const float* const hs = RESUME ? a.hand_state + (size_t)inst * kHandStride : nullptr;
-    if constexpr (RESUME) we_lane = hs[r];
 
     // ---- P0a: RK4 linearisation of stage k on row k mod 4 -> LDS [k][field][lane] -----------------------------
     // fields: zbar, yref entry, warm multipliers (2), defect b_k, the NGV varying Jacobian rows; run mode also the
@@ -206,8 +200,8 @@ __device__ __forceinline__ void rowpar_robot(const KParams& P, const KArgs& a, i
         }
     };
 
-    const int len = (mode == kModeRun && !RESUME) ? (a.traj_len ? a.traj_len[inst] : N + 1) : 0;
-    if constexpr (!RESUME) {
+    const int len = (mode == kModeRun) ? (a.traj_len ? a.traj_len[inst] : N + 1) : 0;
+    {
         struct In {
             float x[NX], u[NU], y, xnext, tq;
             float2 l;
@@ -300,7 +294,7 @@ __device__ __forceinline__ void rowpar_robot(const KParams& P, const KArgs& a, i
     // the stage's reference pose go to LDS for P0c ----------------------------------------------------------------
     float* const s_dx = s_red + 32;                  // [N+1][16]
     float* const s_ref = s_dx + (size_t)(N + 1) * 16;  // [N+1][3]
-    if (!RESUME && w0) {
+    if (w0) {
         float dx = is_x ? x0_lane - XB(0, xi) : 0.0f;
         float ref_x = 0.0f, ref_y = 0.0f, ref_t = pose_th;
         struct Stg {
@@ -349,13 +343,13 @@ __device__ __forceinline__ void rowpar_robot(const KParams& P, const KArgs& a, i
     RP_STAMP(2);
 
     // ---- P0c (stage-parallel): gradient, bounds, slacks, multipliers and the record of stage k on row k mod ROWS
-    if (!RESUME && mode == kModeRun && P.terminal_hack && is_x && xi < 3) {  // NMPCNavControlDiff.cpp:127-139
+    if (mode == kModeRun && P.terminal_hack && is_x && xi < 3) {  // NMPCNavControlDiff.cpp:127-139
         const bool eq = (s_ref[N * 3] == s_ref[(N - 1) * 3]) && (s_ref[N * 3 + 1] == s_ref[(N - 1) * 3 + 1]) &&
                         (s_ref[N * 3 + 2] == s_ref[(N - 1) * 3 + 2]);
         we_lane = (eq ? 100.0f : 1.0f) * w_lane;
     }
     float sum_c0 = 0.0f;
-    for (int j = 0; j < (RESUME ? 0 : NR); j++) {
+    for (int j = 0; j < NR; j++) {
         const int kr = j * ROWS + q;
         const bool kv = kr <= N;
         const int k = kv ? kr : N;
@@ -394,7 +388,7 @@ __device__ __forceinline__ void rowpar_robot(const KParams& P, const KArgs& a, i
         rec_store<RS, QM>(kv ? tbase_own + (size_t)k * KS : tdummy, rec);  // idle slots: their own unused slot
         dzbase[(size_t)k * 16] = 0.0f;  // (rows past the end repeat stage N's zero)
     }
-    if constexpr (!RESUME) {
+    {
         float v[6] = {wave_sum_rows(row_sum16(lv ? sum_c0 : 0.0f)), 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
         const int op[6] = {0, 0, 0, 0, 0, 0};
         block_combine(v, op, 1);
@@ -450,15 +444,7 @@ __device__ __forceinline__ void rowpar_robot(const KParams& P, const KArgs& a, i
     float exit_res[3] = {0.0f, 0.0f, 0.0f};
     float alpha = 0.0f, sigma_mu = 0.0f, mu_prev = 3.0e38f;
     float tg_rhs = P.sd_hi * sum_c0 * inv_m2;
-    int it0 = 0;
-    if constexpr (RESUME) {
-        alpha = hs[16];
-        sigma_mu = hs[17];
-        tg_rhs = hs[18];
-        mu_prev = hs[19];
-        it0 = __float_as_int(hs[20]);
-    }
-    for (int it = it0;; it++) {
+    for (int it = 0;; it++) {
         // phase A (stage-parallel): apply the previous step, residuals, barrier weight, rhs terms
         const float a_upd = (it > 0) ? alpha : 0.0f;
         float res_ineq = 0.0f, sum_c = 0.0f, max_c = 0.0f, lam_max = 0.0f, sc0 = 1.0f, nanf_ = 0.0f;
@@ -794,32 +780,6 @@ __device__ __forceinline__ void rowpar_robot(const KParams& P, const KArgs& a, i
 #undef UBAR
 }
 
-template <class M, int W>
-__global__ __launch_bounds__(64 * W, 1) void k_sqp_rti_rowpar(KParams P, KArgs a, int mode)
-{
-    rowpar_robot<M, W, false>(P, a, mode, (int)blockIdx.x);
-}
-
-// The robots the team kernel handed off (hand_list[0 .. hand_count[0])), one block of W waves each; a grid smaller
-// than the list loops over it. The last block to finish clears the list for the next launch (every block has read
-// the count by then).
-template <class M, int W>
-__global__ __launch_bounds__(64 * W, 1) void k_sqp_rti_rowpar_tail(KParams P, KArgs a, int mode)
-{
-    const int n = a.hand_count[0];
-    for (int j = (int)blockIdx.x; j < n; j += (int)gridDim.x) {
-        rowpar_robot<M, W, true>(P, a, mode, a.hand_list[j]);
-        __syncthreads();  // the block's LDS reductions of one robot before the next robot's
-    }
-    if (threadIdx.x == 0) {
-        __threadfence();
-        if (atomicAdd(a.hand_count + 1, 1) == (int)gridDim.x - 1) {
-            atomicExch(a.hand_count, 0);
-            atomicExch(a.hand_count + 1, 0);
-        }
-    }
-}
-
 }  // namespace
 
 template <class M>
@@ -834,11 +794,8 @@ hipError_t launch_sqp_rti_rowpar(const KParams& P, const KArgs& a, int mode, hip
 {
     if (a.B <= 0) return hipSuccess;
     const size_t lds = rowpar_lds_bytes<M>(P.N, mode);
-    if (lds > 65536 || P.ipm != 1 || (a.segs && a.hand_grid <= 0)) return hipErrorInvalidValue;
-    if (a.hand_grid > 0) {  // the team kernel's hand-offs: four waves per robot
-        if (!a.hand_count || !a.hand_list || !a.hand_state) return hipErrorInvalidValue;
-        hipLaunchKernelGGL((k_sqp_rti_rowpar_tail<M, 4>), dim3(a.hand_grid), dim3(256), lds, stream, P, a, mode);
-    } else if (a.rowpar >= 4)  // four waves per robot (one per SIMD of its CU)
+    if (lds > 65536 || P.ipm != 1 || a.segs) return hipErrorInvalidValue;
+    if (a.rowpar >= 4)  // four waves per robot (one per SIMD of its CU)
         hipLaunchKernelGGL((k_sqp_rti_rowpar<M, 4>), dim3(a.B), dim3(256), lds, stream, P, a, mode);
     else
         hipLaunchKernelGGL((k_sqp_rti_rowpar<M, 1>), dim3(a.B), dim3(64), lds, stream, P, a, mode);

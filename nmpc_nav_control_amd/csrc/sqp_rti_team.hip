@@ -648,21 +648,6 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a)
     // previous step) and the initial point's mu (P0; mu0 for a cold start, where every pair has t lambda = mu0)
     float tg_rhs = P.sd_hi * sum_c0 * inv_m2;
     for (int it = 0;; it++) {
-        if (SD && a.hand_cap > 0 && it == a.hand_cap) {
-            // tail hand-off: the lockstep wave would run its slowest team's remaining iterations serially; a team
-            // still iterating here leaves them to the row-parallel tail launch (its records, the DZ plane and the
-            // iterate are complete at this point; the scalars go to its hand_state row) and every team stops
-            if (!done) {
-                float* const hs = a.hand_state + (size_t)inst * kHandStride;
-                hs[r] = we_lane;
-                hs[16 + r] = (r == 0) ? alpha : ((r == 1) ? sigma_mu : ((r == 2) ? tg_rhs : ((r == 3) ? mu_prev
-                             : __int_as_float(it))));
-                if (r == 0) a.hand_list[atomicAdd(a.hand_count, 1)] = inst;
-                status = kStatusHanded;
-                done = true;
-            }
-            break;
-        }
         // P1 (backward): apply the previous step, residuals, adjoint, fp64 classic Riccati factorisation,
         // predictor rhs
         double Lrow[NV];  // lane NU+i: row i of P_{k+1} (the state block of the previous stage's M after its pivots)
@@ -1077,7 +1062,7 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a)
         }
     }
     __threadfence_block();
-    if (r == 0 && status != kStatusHanded) {
+    if (r == 0) {
         float u0[NU];
 #pragma unroll
         for (int j = 0; j < NU; j++) {

@@ -71,7 +71,6 @@ constexpr float kCompMaxRatio = 30.0f;
 // infeasible as the failure test does; tools/infeas_study.py); the oracle uses the same two constants
 constexpr float kInfeasLambda = 1e5f;
 constexpr float kInfeasRes = 1e-3f;
-constexpr int kStatusHanded = -1;  // internal: the robot's IPM continues in the tail launch (KArgs::hand_cap)
 constexpr float kWarmLambdaCap = 1e3f;  // largest warm-started bound multiplier
 constexpr float kFar = 1e30f;  // sentinel bound / slack of unbounded slots (z + kFar - kFar == 0 in fp32)
 
