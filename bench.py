@@ -238,6 +238,9 @@ def main():
     ap.add_argument("--cpu-ticks", type=int, default=8)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--gather", action="store_true", help="all-gather u0+status to rank 0 every tick (RCCL)")
+    ap.add_argument("--dist", action="store_true",
+                    help="initialise the RCCL process group at world size 1 too (exercises the barrier, the MAX "
+                         "all-reduce of the timed region and the command all-gather on a one-GPU box)")
     ap.add_argument("--groups", type=int, default=None,
                     help="stream groups per model (default: the config's); each is a Fleet on its own HIP stream")
     ap.add_argument("--joined", action="store_true",
@@ -249,7 +252,7 @@ def main():
     rank, world, local_rank = world_info()
     dev = torch.device("cuda", local_rank)
     torch.cuda.set_device(dev)
-    if world > 1:
+    if world > 1 or args.dist:
         dist.init_process_group("nccl", device_id=dev)
 
     cfg = CONFIGS[args.config]
@@ -318,7 +321,7 @@ def main():
             "failed_solves": int(node.fail_cnt.sum().item()), "roofline": roof, "cpu_baseline": cpu,
         }
         print(json.dumps(result), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.barrier()
         dist.destroy_process_group()
     return result

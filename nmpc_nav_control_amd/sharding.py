@@ -95,7 +95,7 @@ class CommandGather:
     def collect(self, slot):
         """All-gather staging slot `slot` (on the current stream) -> [rows][total]."""
         src, bufs = self.stage_bufs[slot], self.recv[slot]
-        if dist.is_initialized() and dist.get_world_size() > 1:
+        if dist.is_initialized():  # (world size 1 too: bench.py --dist runs the RCCL call on one GPU)
             dist.all_gather(bufs, src)
         else:
             bufs[0].copy_(src)
