@@ -249,6 +249,12 @@ def main():
                     help="every robot keeps its first goal / path (the round-2 workload, which parks and drifts)")
     args = ap.parse_args()
 
+    # stdout carries exactly one JSON line: native libraries that print to fd 1 (RCCL's version banner at process
+    # group start-up) are sent to stderr, the JSON line goes to the original stdout
+    sys.stdout.flush()
+    json_out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
+
     rank, world, local_rank = world_info()
     dev = torch.device("cuda", local_rank)
     torch.cuda.set_device(dev)
@@ -320,7 +326,7 @@ def main():
             "qp_iter": {k: (round(v, 3) if isinstance(v, float) else v) for k, v in its.items()},
             "failed_solves": int(node.fail_cnt.sum().item()), "roofline": roof, "cpu_baseline": cpu,
         }
-        print(json.dumps(result), flush=True)
+        print(json.dumps(result), file=json_out, flush=True)
     if dist.is_initialized():
         dist.barrier()
         dist.destroy_process_group()
