@@ -170,3 +170,59 @@ def test_params_struct_layout_and_ipm_options(built):
         setattr(bad, field, val)
         assert L.nmpc_batch_create(ctypes.byref(bad), 8, ctypes.byref(h)) != 0, field
         assert b"qp_" in L.nmpc_last_error()
+
+
+def test_null_handle_is_an_argument_error_everywhere(built):
+    """Every batched entry point checks its handle before touching the device: NULL -> NMPC_ERR_ARG and a message
+    (the reference's wrappers map any non-zero status to their exception path, NMPCNavControl.cpp:14-23)."""
+    import ctypes
+    L = _lib.lib()
+    vp = ctypes.c_void_p
+    calls = {
+        "nmpc_batch_set_params": lambda: L.nmpc_batch_set_params(None, _lib.default_params("diff", 20)),
+        "nmpc_batch_get_params": lambda: L.nmpc_batch_get_params(None, _lib.ModelParams()),
+        "nmpc_batch_init_iterate": lambda: L.nmpc_batch_init_iterate(None, 1, 0, None),
+        "nmpc_batch_solve": lambda: L.nmpc_batch_solve(None, 1, *([None] * 2), 9, *([None] * 11)),
+        "nmpc_batch_solve_iterate": lambda: L.nmpc_batch_solve_iterate(None, 1, None, None, 9, *([None] * 4), 1,
+                                                                        *([None] * 4)),
+        "nmpc_batch_run": lambda: L.nmpc_batch_run(None, 1, *([None] * 12)),
+        "nmpc_batch_set_kernel": lambda: L.nmpc_batch_set_kernel(None, 0),
+        "nmpc_batch_set_schedule": lambda: L.nmpc_batch_set_schedule(None, 0),
+        "nmpc_batch_state": lambda: L.nmpc_batch_state(None, None, None, None, None),
+        "nmpc_batch_forget_warm": lambda: L.nmpc_batch_forget_warm(None, 1, None, None),
+        "nmpc_batch_warm_state": lambda: L.nmpc_batch_warm_state(None, None, None, None),
+        "nmpc_fleet_sim_step": lambda: L.nmpc_fleet_sim_step(None, 1, *([None] * 9), 0, None),
+    }
+    for name, call in calls.items():
+        assert call() == -1, name  # NMPC_ERR_ARG
+        assert L.nmpc_last_error(), name
+    assert L.nmpc_batch_destroy(vp()) == 0  # destroying NULL is a no-op, like free()
+
+
+@pytest.mark.parametrize("field,val,code", [("N", 0, -1), ("N", 5000, -1), ("dt", 0.0, -1), ("dt_ctrl", -1.0, -1),
+                                            ("qp_iter_max", 0, -1), ("qp_warm_iter_max", -1, -1)])
+def test_params_validation_at_create(built, field, val, code):
+    """nmpc_batch_create validates the parameter block before any device allocation (runs without a GPU)."""
+    import ctypes
+    L = _lib.lib()
+    bad = _lib.default_params("diff", 20)
+    setattr(bad, field, val)
+    h = ctypes.c_void_p()
+    assert L.nmpc_batch_create(ctypes.byref(bad), 8, ctypes.byref(h)) == code, field
+    assert not h.value and L.nmpc_last_error()
+
+
+def test_bounds_weights_and_capacity_validation(built):
+    """Empty bound boxes and non-positive model parameters are argument errors; a zero input weight R is the one
+    unsupported OCP (the input-block Cholesky needs R dt > 0, as the reference's yaml always gives); capacity < 1."""
+    import ctypes
+    L = _lib.lib()
+    h = ctypes.c_void_p()
+    for mutate, code in ((lambda p: p.lbx.__setitem__(0, p.ubx[0]), -1), (lambda p: p.lbu.__setitem__(1, 2.0), -1),
+                         (lambda p: p.p.__setitem__(0, 0.0), -1), (lambda p: p.W.__setitem__(7, 0.0), -3)):
+        prm = _lib.default_params("diff", 20)
+        mutate(prm)
+        assert L.nmpc_batch_create(ctypes.byref(prm), 8, ctypes.byref(h)) == code
+        assert not h.value
+    assert L.nmpc_batch_create(ctypes.byref(_lib.default_params("diff", 20)), 0, ctypes.byref(h)) == -1
+    assert b"capacity" in L.nmpc_last_error()
