@@ -98,9 +98,6 @@ KParams to_kparams(const nmpc_model_params& p, int nx, int nu, int nbx, int nbu)
     k.warm_kappa = (float)p.qp_warm_kappa;
     if (const char* v = std::getenv("NMPC_AMD_WARM")) k.warm = std::atoi(v) != 0;
     if (const char* v = std::getenv("NMPC_AMD_WARM_KAPPA")) k.warm_kappa = std::strtof(v, nullptr);
-    if (const char* v = std::getenv("NMPC_AMD_THR0")) k.thr0 = std::strtof(v, nullptr);
-    k.thr0_warm = k.thr0;
-    if (const char* v = std::getenv("NMPC_AMD_THR0_WARM")) k.thr0_warm = std::strtof(v, nullptr);
     k.warm_iter_max = p.qp_warm_iter_max > 0 ? p.qp_warm_iter_max : p.qp_iter_max;
     if (const char* v = std::getenv("NMPC_AMD_WARM_ITER_MAX")) k.warm_iter_max = std::atoi(v);
     return k;

@@ -31,7 +31,6 @@ struct KParams {
     // warm start of the bound multipliers from the robot's previous solve (KArgs::warm flags)
     int warm;
     float warm_kappa;
-    float thr0_warm;    // initial slack floor of warm-started robots (thr0 for cold ones)
     int warm_iter_max;  // a solve that needed more IPM iterations starts the next one cold
 };
 

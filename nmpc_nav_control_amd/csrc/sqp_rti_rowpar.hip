@@ -372,8 +372,7 @@ __global__ __launch_bounds__(64 * W, 1) void k_sqp_rti_rowpar(KParams P, KArgs a
         rec[R::UB] = kFar;
         if (valid && has_b) {
             const float lb = lo_b - zbar, ubd = hi_b - zbar;
-            const float th0 = warm ? P.thr0_warm : P.thr0;
-            const float tl = fmaxf(z - lb, th0), tu = fmaxf(ubd - z, th0);
+            const float tl = fmaxf(z - lb, P.thr0), tu = fmaxf(ubd - z, P.thr0);
             rec[R::LB] = lb;
             rec[R::UB] = ubd;
             rec[R::TL] = tl;
