@@ -27,7 +27,7 @@ sys.path.insert(0, ROOT)
 
 from nmpc_nav_control_amd.fleet import FleetNode  # noqa: E402
 from nmpc_nav_control_amd.scenario import DEFAULT_SEED  # noqa: E402
-from nmpc_nav_control_amd.sharding import TimedRegion, world_info  # noqa: E402
+from nmpc_nav_control_amd.sharding import TimedRegion, mixed_counts, world_info  # noqa: E402
 
 # BASELINE.json configs (index -> seed offset 20250824 + idx)
 CONFIGS = {
@@ -149,9 +149,35 @@ def roofline(fleets, node, kernel_ms, steps, step_s=None):
                        "the launches of %d decoupled streams overlapping" % len(fleets)) if node.decoupled else
                       "HIP events on the launch stream(s), timed region",
             "compulsory_bytes_per_launch": cbytes, "achieved_compulsory_GBs": round(cbytes / t_k / 1e9, 2),
+            "hbm": hbm_block(pmc, src, traffic, cbytes, t_k),
             "note": "VALU-bound, latency-limited: <=15x15 per-robot blocks, no GEMM-shaped work (no MFMA); "
                     "traffic = 2*FETCH_SIZE + WRITE_SIZE (L2<->fabric incl. Infinity-Cache hits) per step (the sum "
                     "over the step's launches: one per model and stream group)"}
+
+
+def hbm_block(pmc, src, traffic, cbytes, t_k):
+    """North-star HBM reporting: the memory-side bytes of the step's solve launches from the PMC record
+    (2 x FETCH_SIZE + WRITE_SIZE, the gfx950 correction of MI355X_MICROARCH.md "HBM"), their rate over the launch
+    time and its fraction of the 8 TB/s HBM peak, beside the compulsory bytes and their fraction. The
+    counters sit at the L2's memory side, so Infinity-Cache (MALL) hits are included: an upper bound on DRAM bytes.
+    ea_*req_dram: the share of those requests gfx950 tags as destined for DRAM (TCC_EA0_*REQ_DRAM), whose
+    meaning tools/ubench_mall.hip calibrates (profiles/<round>/pmc/mall_calibration.json)."""
+    out = {"peak_GBs": HBM_PEAK_GBS, "compulsory_bytes_per_step": cbytes,
+           "compulsory_GBs": round(cbytes / t_k / 1e9, 3), "compulsory_frac": round(cbytes / t_k / 1e9 / HBM_PEAK_GBS, 6)}
+    if traffic is not None:
+        gbs = traffic / t_k / 1e9
+        out.update({"pmc_bytes_per_step": traffic, "pmc_GBs": round(gbs, 1), "pmc_frac": round(gbs / HBM_PEAK_GBS, 4),
+                    "pmc_over_compulsory": round(traffic / cbytes, 1) if cbytes else None, "pmc_source": src,
+                    "includes_mall_hits": True})
+    if pmc and pmc.get("ea_rdreq"):
+        rd, rdd = pmc["ea_rdreq"], pmc.get("ea_rdreq_dram")
+        wr, wrd = pmc.get("ea_wrreq"), pmc.get("ea_wrreq_dram")
+        out["dram_destined_share"] = {"read": round(rdd / rd, 4) if rdd is not None else None,
+                                      "write": round(wrd / wr, 4) if wr and wrd is not None else None}
+        cal, csrc = _profile_json("pmc/mall_calibration.json")
+        if cal:
+            out["dram_counter_calibration"] = {"source": csrc, "verdict": cal.get("verdict")}
+    return out
 
 
 def _scaled(v, g):
@@ -224,9 +250,40 @@ class LaunchTimer:
         return [max(s[0].elapsed_time(b) for b in e) for s, e in self.ev]
 
 
+def _free_port():
+    import socket
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def launch_ranks(n, argv):
+    """`--gpus N` (N > 1) without torchrun's environment: start the N rank processes here, one per GPU, with
+    torch.distributed.run as a child process (RCCL rendezvous on 127.0.0.1), and return its exit code. This
+    process makes no HIP call before or after (it only parses arguments), so no GPU state is shared or inherited;
+    rank 0 prints the one JSON line to the inherited stdout."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__), *argv]
+    env = dict(os.environ, NMPC_BENCH_LAUNCHER="bench.py --gpus %d" % n)
+    sys.stdout.flush()
+    return subprocess.run(cmd, env=env).returncode
+
+
+def _factory(spec):
+    """--test-solver MODULE:ATTR -> the solver class FleetNode builds its fleets with (default: BatchSolver)."""
+    if not spec:
+        return None
+    import importlib
+    mod, attr = spec.split(":")
+    return getattr(importlib.import_module(mod), attr)
+
+
 def main():
     ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="ranks (one per GPU). Under torchrun it must equal WORLD_SIZE; without torchrun's "
+                         "environment and N > 1, bench.py starts the N ranks itself")
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", default="metric", choices=sorted(CONFIGS))
@@ -247,7 +304,16 @@ def main():
                     help="fleet-wide tick boundary across streams (default: decoupled streams unless --gather)")
     ap.add_argument("--no-renew", action="store_true",
                     help="every robot keeps its first goal / path (the round-2 workload, which parks and drifts)")
+    ap.add_argument("--batch-per-gpu", type=int, default=None,
+                    help="robots per rank (default: the config's; mixed splits them over the three models)")
+    # test hooks of the launch path (tests/test_bench_launch.py): CPU ranks over gloo with a CPU solver class
+    ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"], help=argparse.SUPPRESS)
+    ap.add_argument("--test-solver", default=None, help=argparse.SUPPRESS)
     args = ap.parse_args()
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return launch_ranks(args.gpus, sys.argv[1:])
 
     # stdout carries exactly one JSON line: native libraries that print to fd 1 (RCCL's version banner at process
     # group start-up) are sent to stderr, the JSON line goes to the original stdout
@@ -256,39 +322,57 @@ def main():
     os.dup2(2, 1)
 
     rank, world, local_rank = world_info()
-    dev = torch.device("cuda", local_rank)
-    torch.cuda.set_device(dev)
+    cpu = args.device == "cpu"
+    dev = torch.device("cpu") if cpu else torch.device("cuda", local_rank)
+    if not cpu:
+        torch.cuda.set_device(dev)
     if world > 1 or args.dist:
-        dist.init_process_group("nccl", device_id=dev)
+        dist.init_process_group("gloo" if cpu else "nccl", **({} if cpu else {"device_id": dev}))
+    ranks = dist.get_world_size() if dist.is_initialized() else 1
+    backend = dist.get_backend() if dist.is_initialized() else None
+    if ranks != args.gpus or ranks != world:
+        print(f"bench.py: --gpus {args.gpus} but the process group has {ranks} rank(s) (WORLD_SIZE {world})",
+              file=sys.stderr)
+        if dist.is_initialized():
+            dist.destroy_process_group()
+        return 3
 
     cfg = CONFIGS[args.config]
+    models = cfg["models"]
+    if args.batch_per_gpu is not None:
+        models = (mixed_counts(args.batch_per_gpu, [m for m, _ in models]) if len(models) > 1
+                  else [(models[0][0], args.batch_per_gpu)])
     gather = args.gather or (args.config == "mixed" and world > 1)
     # weak scaling: the global fleet holds B x world robots of each model; this rank owns the contiguous
     # shard [rank*B, (rank+1)*B) of it (sharding.shard_range), no collective on the solve path
     groups = cfg.get("groups", 1) if args.groups is None else args.groups
-    node = FleetNode(cfg["models"], cfg["N"], DEFAULT_SEED + cfg["idx"], dev, rank=rank, world=world, gather=gather,
-                     groups=groups, decoupled=False if args.joined else None, renew=not args.no_renew)
+    node = FleetNode(models, cfg["N"], DEFAULT_SEED + cfg["idx"], dev, rank=rank, world=world, gather=gather,
+                     groups=groups, decoupled=False if args.joined else None, renew=not args.no_renew,
+                     solver_factory=_factory(args.test_solver))
     fleets = node.fleets
-    torch.cuda.synchronize()
+    if not cpu:
+        torch.cuda.synchronize()
 
     # warmup runs every op of the timed loop (the first use of a torch kernel loads its code object)
     for _ in range(args.closed_loop_warmup + args.warmup):
         node.step()
     node.reset_stats()
-    torch.cuda.synchronize()
+    if not cpu:
+        torch.cuda.synchronize()
 
     # per-launch timing of the solve kernels with HIP events on their launch streams (FleetNode.step calls the
     # timer around every solve launch). One stream: the solve's duration. Joined streams: from one start event
     # on the main stream to each stream's end-of-solve event (the region = the latest). Decoupled streams: each
     # launch from its own stream's start event.
-    timer = LaunchTimer(len(fleets), args.steps)
+    timer = None if cpu else LaunchTimer(len(fleets), args.steps)
     with TimedRegion(dev) as region:
         for k in range(args.steps):
-            timer.k = k
+            if timer is not None:
+                timer.k = k
             node.step(timer)
     elapsed = region.elapsed
 
-    kernel_ms = timer.kernel_ms(node.decoupled)
+    kernel_ms = timer.kernel_ms(node.decoupled) if timer is not None else None
     its = node.iter_stats()
     B_rank = node.B
     k_mean = float(node.iters_sum.sum().item()) / (B_rank * args.steps)
@@ -297,22 +381,23 @@ def main():
 
     result = None
     if rank == 0:
-        roof = roofline(fleets, node, kernel_ms, args.steps, step_s=elapsed / args.steps)
-        cpu = None
+        roof = roofline(fleets, node, kernel_ms, args.steps, step_s=elapsed / args.steps) if not cpu else None
+        cpu_base = None
         u0_err = None
-        if not args.no_cpu_baseline and world == 1:
+        if not args.no_cpu_baseline and world == 1 and not cpu:
             nthreads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
             cpu_rate, u0_err, nf, ns, rate_1 = cpu_baseline(fleets, args.cpu_sample, args.cpu_ticks, nthreads)
-            cpu = {"value": round(cpu_rate, 1), "unit": "SQP-RTI iterations/sec", "cores": nthreads, "kind": "port",
-                   "sample": f"{ns} instance-iterations: {'all' if args.cpu_sample <= 0 else args.cpu_sample} robots of each model x "
-                             f"{args.cpu_ticks} closed-loop ticks after the timed region, fp64 oracle/nmpc_oracle.c, "
-                             f"OpenMP {nthreads} threads, identical inputs", "failed": nf,
-                   "value_1core": round(rate_1, 1),
-                   "note": "a reported baseline, not a target: timed after the timed region on the GPU box's shared "
-                           "host cores, so it varies from run to run"}
+            cpu_base = {"value": round(cpu_rate, 1), "unit": "SQP-RTI iterations/sec", "cores": nthreads,
+                        "kind": "port",
+                        "sample": f"{ns} instance-iterations: {'all' if args.cpu_sample <= 0 else args.cpu_sample} robots of each model x "
+                                  f"{args.cpu_ticks} closed-loop ticks after the timed region, fp64 oracle/nmpc_oracle.c, "
+                                  f"OpenMP {nthreads} threads, identical inputs", "failed": nf,
+                        "value_1core": round(rate_1, 1),
+                        "note": "a reported baseline, not a target: timed after the timed region on the GPU box's shared "
+                                "host cores, so it varies from run to run"}
         result = {
             "metric": "SQP-RTI iterations/sec (whole node), diff N=40 batch=4096; u0 max-abs err",
-            "value": round(value, 1), "unit": "SQP-RTI iterations/sec", "n_gpus": world, "steps": args.steps,
+            "value": round(value, 1), "unit": "SQP-RTI iterations/sec", "n_gpus": ranks, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "fp32+fp64",
             "data": ("synthetic seeded closed-loop fleet (SURVEY 8d), random-arc paths + goal poses" +
@@ -320,18 +405,21 @@ def main():
                                                "2-6 s ttl (NMPCNavControlROS.cpp:304-327)")),
             "config": {"workload": cfg["desc"], "config": args.config, "N": cfg["N"],
                        "batch_per_gpu": B_rank, "global_batch": B_rank * world,
-                       "models": [m for m, _ in cfg["models"]], "parallelism": f"instance-sharded x{world}",
+                       "models": [m for m, _ in models], "parallelism": f"instance-sharded x{world}",
+                       "ranks": ranks, "backend": backend,
+                       "launcher": os.environ.get("NMPC_BENCH_LAUNCHER",
+                                                  "torchrun" if "WORLD_SIZE" in os.environ else "single process"),
                        "closed_loop_warmup_ticks": args.closed_loop_warmup, "rccl_gather": gather},
             "u0_max_abs_err": u0_err, "qp_iter_mean": round(k_mean, 3), "qp_iter_max": int(node.iters_max.max().item()),
             "qp_iter": {k: (round(v, 3) if isinstance(v, float) else v) for k, v in its.items()},
-            "failed_solves": int(node.fail_cnt.sum().item()), "roofline": roof, "cpu_baseline": cpu,
+            "failed_solves": int(node.fail_cnt.sum().item()), "roofline": roof, "cpu_baseline": cpu_base,
         }
         print(json.dumps(result), file=json_out, flush=True)
     if dist.is_initialized():
         dist.barrier()
         dist.destroy_process_group()
-    return result
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -49,6 +49,12 @@ void ocp_nlp_out_set(ocp_nlp_config* config, ocp_nlp_dims* dims, ocp_nlp_out* ou
 /* fields: "time_tot" (double, seconds), "time_lin", "time_qp_sol" (double), "sqp_iter", "qp_iter",
  *         "status" (int). */
 void ocp_nlp_get(ocp_nlp_solver* solver, const char* field, void* return_value_);
+/* Solver options (acados: ocp_nlp_solver_opts_set(config, capsule->nlp_opts, field, value)). Fields:
+ *   "qp_warm_start" (int): 0 = HPIPM's cold start every solve (the reference's generated default,
+ *                   scripts/diff/generate_c_code.py:68-74); 1 or 2 = warm-started bound
+ *                   multipliers from the capsule's previous solve (this library's default for capsules);
+ *   "qp_iter_max"   (int >= 1): IPM iteration cap (50). Unknown fields are logged and ignored. */
+void ocp_nlp_solver_opts_set(ocp_nlp_config* config, void* opts_, const char* field, void* value);
 /* Dimension query: "x", "u", "y_ref" per stage (int). */
 int ocp_nlp_dims_get_from_attr(ocp_nlp_config* config, ocp_nlp_dims* dims, ocp_nlp_out* out, int stage,
                                const char* field);

@@ -69,6 +69,12 @@ typedef struct nmpc_model_params {
      * A robot whose QP was hard last tick starts its next IPM cold: warm-started multipliers speed up the easy
      * majority but lengthen exactly the hard QPs that set the launch time (DESIGN.md "Algorithm and precision"). */
     int qp_warm_iter_max;
+    /* Early infeasibility exit (status 4): the IPM stops once its largest bound multiplier exceeds
+     * qp_infeas_lambda * max(1, w_max / 10) (w_max: the largest stage or terminal weight of the robot, terminal
+     * hack included) while the bound residual stays above 1e-3. HPIPM has no such test (a hard QP runs to
+     * qp_iter_max, which acados' RTI accepts), so 0 switches it off; the batched default is 1e5, the capsule ABI
+     * default 0 (acados semantics). */
+    double qp_infeas_lambda;
 } nmpc_model_params;
 
 enum { NMPC_IPM_MEHROTRA = 0, NMPC_IPM_SINGLE = 1 };
@@ -181,6 +187,12 @@ int nmpc_batch_forget_warm(nmpc_batch* b, int B, const unsigned char* mask, void
  * nmpc_batch_state this is everything a solve reads from the handle, e.g. to checkpoint a fleet or to replay a
  * tick bit for bit. */
 int nmpc_batch_warm_state(nmpc_batch* b, unsigned char** warm, float** scratch, size_t* scratch_bytes);
+
+/* The warm-start rule the solve kernels apply (the parameters after the NMPC_AMD_WARM / NMPC_AMD_WARM_ITER_MAX
+ * overrides): a robot's flag is set after a solve iff warm && status == 0 && iterations < iter_max &&
+ * iterations <= warm_iter_max. Hosts that mirror the device flags (the capsule shim) use this, not their copy of
+ * the parameters. Each output may be NULL. */
+int nmpc_batch_warm_rule(const nmpc_batch* b, int* warm, int* warm_iter_max, int* iter_max);
 
 /* Bench / test harness: closed-loop plant step and path-reference regeneration for B robots
  * (see DESIGN.md "Synthetic closed loop"). All device pointers, [field][B]:

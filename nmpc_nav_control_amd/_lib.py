@@ -30,6 +30,7 @@ class ModelParams(ctypes.Structure):
         ("qp_mu0", ctypes.c_double), ("qp_thr0", ctypes.c_double), ("qp_tau", ctypes.c_double),
         ("qp_ipm", ctypes.c_int), ("qp_sigma_lo", ctypes.c_double), ("qp_sigma_hi", ctypes.c_double),
         ("qp_warm_start", ctypes.c_int), ("qp_warm_kappa", ctypes.c_double), ("qp_warm_iter_max", ctypes.c_int),
+        ("qp_infeas_lambda", ctypes.c_double),
     ]
 
 
@@ -74,7 +75,7 @@ class SolverCapsule(ctypes.Structure):
 BATCH_SYMBOLS = [
     "nmpc_model_dims", "nmpc_model_params_default", "nmpc_model_params_set_limits", "nmpc_batch_create",
     "nmpc_batch_destroy", "nmpc_batch_set_params", "nmpc_batch_get_params", "nmpc_batch_init_iterate",
-    "nmpc_batch_solve", "nmpc_batch_solve_iterate", "nmpc_batch_run", "nmpc_batch_run_path", "nmpc_batch_state", "nmpc_batch_warm_state", "nmpc_batch_forget_warm", "nmpc_batch_set_kernel", "nmpc_batch_set_schedule",
+    "nmpc_batch_solve", "nmpc_batch_solve_iterate", "nmpc_batch_run", "nmpc_batch_run_path", "nmpc_batch_state", "nmpc_batch_warm_state", "nmpc_batch_warm_rule", "nmpc_batch_forget_warm", "nmpc_batch_set_kernel", "nmpc_batch_set_schedule",
     "nmpc_fleet_sim_step", "nmpc_fleet_sim_step_renew", "nmpc_fleet_hash",
     "nmpc_last_error", "nmpc_version", "nmpc_path_discretize", "nmpc_codegen_default", "nmpc_capsule_new",
     "nmpc_capsule_delete", "nmpc_capsule_create", "nmpc_capsule_reset", "nmpc_capsule_update_params",
@@ -83,7 +84,7 @@ BATCH_SYMBOLS = [
 KERNELS = {"team": 0}
 SCHEDULES = {"off": 0, "auto": 1, "sorted": 2, "interleaved": 3, "spread": 4}
 NLP_SYMBOLS = ["ocp_nlp_constraints_model_set", "ocp_nlp_cost_model_set", "ocp_nlp_out_get", "ocp_nlp_out_set",
-               "ocp_nlp_get", "ocp_nlp_dims_get_from_attr"]
+               "ocp_nlp_get", "ocp_nlp_solver_opts_set", "ocp_nlp_dims_get_from_attr"]
 CAPSULE_SUFFIXES = ["create_capsule", "free_capsule", "create", "create_with_discretization", "reset",
                     "update_params", "solve", "batch_solve", "free", "print_stats", "get_nlp_in", "get_nlp_out",
                     "get_nlp_solver", "get_nlp_config", "get_nlp_opts", "get_nlp_dims"]
@@ -125,6 +126,7 @@ def lib():
     L.nmpc_batch_state.argtypes = [vp, ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.POINTER(vp), c_int_p]
     L.nmpc_batch_forget_warm.argtypes = [vp, i, vp, vp]
     L.nmpc_batch_warm_state.argtypes = [vp, ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.POINTER(ctypes.c_size_t)]
+    L.nmpc_batch_warm_rule.argtypes = [vp, c_int_p, c_int_p, c_int_p]
     L.nmpc_fleet_sim_step.argtypes = [vp, i, vp, vp, vp, vp, vp, vp, vp, vp, vp, i, vp]
     L.nmpc_fleet_sim_step_renew.argtypes = [vp, i, vp, vp, vp, vp, vp, vp, vp, vp, vp, ctypes.POINTER(FleetRenew), vp]
     L.nmpc_fleet_hash.argtypes = [ctypes.c_uint, ctypes.c_uint, ctypes.c_uint]
@@ -141,6 +143,7 @@ def lib():
     L.ocp_nlp_out_get.argtypes = [vp, vp, vp, i, ctypes.c_char_p, vp]
     L.ocp_nlp_out_set.argtypes = [vp, vp, vp, i, ctypes.c_char_p, vp]
     L.ocp_nlp_get.argtypes = [vp, ctypes.c_char_p, vp]
+    L.ocp_nlp_solver_opts_set.argtypes = [vp, vp, ctypes.c_char_p, vp]
     _lib = L
     return L
 

@@ -162,6 +162,12 @@ class NMPCNavControl:
         self._L.ocp_nlp_out_set(self._cfg, self._dims, self._out, stage, field.encode(),
                                 a.ctypes.data_as(ctypes.c_void_p))
 
+    def solver_opts_set(self, field, value):
+        """ocp_nlp_solver_opts_set(config, capsule->nlp_opts, field, &value) for the int fields "qp_warm_start"
+        (0: HPIPM's cold start every solve, the reference's generated default) and "qp_iter_max"."""
+        v = ctypes.c_int(int(value))
+        self._L.ocp_nlp_solver_opts_set(self._cfg, self._capsule.contents.nlp_opts, field.encode(), ctypes.byref(v))
+
     def qp_iter(self):
         """IPM iterations of the last solve (ocp_nlp_get "qp_iter")."""
         n = ctypes.c_int()

@@ -143,6 +143,9 @@ void codegen_defaults(nmpc_capsule_impl* c, const nmpc_codegen_desc& d)
     // a capsule is one robot whose latency is its own IPM count, so its warm start floors the multipliers for the
     // mean count (kappa 0.01; the batch default for diff, 0.2, is tuned for the slowest robot of a fleet)
     c->prm.qp_warm_kappa = 0.01;
+    // HPIPM has no infeasibility exit: a hard QP runs to qp_iter_max and acados' RTI accepts the result
+    // (SURVEY Appendix B.6), so the drop-in never turns a stiff but feasible QP into the wrapper's exception
+    c->prm.qp_infeas_lambda = 0.0;
     c->prm.dt = d.tf / d.N;    // uniform time steps tf / N_codegen (ocp.solver_options.tf, N_horizon)
     std::memcpy(c->prm.p, d.p, sizeof(d.p));
     std::memcpy(c->prm.lbx, d.lbx, sizeof(d.lbx));
@@ -441,6 +444,8 @@ void solve_group(std::vector<nmpc_capsule_impl*>& cs, std::vector<Packed>& ps, c
                      std::chrono::duration<double>(ta - t0).count() * 1e3,
                      std::chrono::duration<double>(tb - ta).count() * 1e3,
                      std::chrono::duration<double>(t1 - tb).count() * 1e3, tq * 1e3);
+    int rule_warm = 0, rule_wmax = 0, rule_imax = 0;
+    nmpc_batch_warm_rule(e.batch, &rule_warm, &rule_wmax, &rule_imax);
     std::vector<double*> xbs(n), ubs(n);  // failed solves keep their iterate (nullptr: skipped)
     for (int q = 0; q < n; q++) {
         nmpc_capsule_impl* c = cs[idx[q]];
@@ -455,10 +460,9 @@ void solve_group(std::vector<nmpc_capsule_impl*>& cs, std::vector<Packed>& ps, c
         c->time_tot = tt;
         c->time_qp = tq;
         c->time_lin = 0.0;
-        // the kernel's epilogue rule: warm = qp_warm_start && status == 0 && the IPM converged before its cap
-        const nmpc_model_params& pp = ps[idx[0]].prm;
-        const bool conv = hst[q] == 0 && hit[q] < pp.qp_iter_max &&
-                          hit[q] <= (pp.qp_warm_iter_max > 0 ? pp.qp_warm_iter_max : pp.qp_iter_max);
+        // the kernel's epilogue rule, with the engine's effective parameters (env overrides included), so that
+        // dev_warm mirrors the device flags exactly: warm && status == 0 && converged before the cap
+        const bool conv = rule_warm && hst[q] == 0 && hit[q] < rule_imax && hit[q] <= rule_wmax;
         c->warm_ok = conv;
         e.owner[q] = c->uid;
         e.dev_warm[q] = conv ? 1 : 0;
@@ -620,6 +624,22 @@ void ocp_nlp_get(ocp_nlp_solver* solver, const char* field, void* return_value_)
     else log_err("ocp_nlp_get", std::string("unsupported field ") + field);
 }
 
+void ocp_nlp_solver_opts_set(ocp_nlp_config* config, void* opts_, const char* field, void* value)
+{
+    (void)opts_;
+    nmpc_capsule_impl* c = config ? impl_of(config->impl) : nullptr;
+    if (!c || !field || !value) return;
+    const int v = *static_cast<const int*>(value);
+    if (!std::strcmp(field, "qp_warm_start")) {
+        c->prm.qp_warm_start = v ? 1 : 0;
+        if (!v) c->warm_ok = false;
+    } else if (!std::strcmp(field, "qp_iter_max") && v >= 1) {
+        c->prm.qp_iter_max = v;
+    } else {
+        log_err("ocp_nlp_solver_opts_set", std::string("unsupported field ") + field);
+    }
+}
+
 int ocp_nlp_dims_get_from_attr(ocp_nlp_config* config, ocp_nlp_dims* dims, ocp_nlp_out* out, int stage,
                                const char* field)
 {
@@ -687,7 +707,7 @@ nmpc_solver_capsule* nmpc_capsule_new(int model)
     cap->nlp_in = &c->in;
     cap->nlp_out = &c->out;
     cap->nlp_solver = &c->solver;
-    cap->nlp_opts = nullptr;
+    cap->nlp_opts = c;  // opaque: ocp_nlp_solver_opts_set finds the capsule through its config
     return cap;
 }
 

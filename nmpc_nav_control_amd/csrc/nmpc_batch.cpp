@@ -100,6 +100,9 @@ KParams to_kparams(const nmpc_model_params& p, int nx, int nu, int nbx, int nbu)
     if (const char* v = std::getenv("NMPC_AMD_WARM_KAPPA")) k.warm_kappa = std::strtof(v, nullptr);
     k.warm_iter_max = p.qp_warm_iter_max > 0 ? p.qp_warm_iter_max : p.qp_iter_max;
     if (const char* v = std::getenv("NMPC_AMD_WARM_ITER_MAX")) k.warm_iter_max = std::atoi(v);
+    k.infeas_lam = p.qp_infeas_lambda > 0.0 ? (float)p.qp_infeas_lambda : INFINITY;
+    k.wmax = 0.0f;
+    for (int i = 0; i < nx + nu; i++) k.wmax = std::fmax(k.wmax, (float)p.W[i]);
     return k;
 }
 
@@ -196,6 +199,7 @@ int check_params(const nmpc_model_params* prm)
     if (prm->qp_warm_start != 0 && prm->qp_warm_start != 1) return set_err(NMPC_ERR_ARG, "qp_warm_start must be 0 or 1");
     if (prm->qp_warm_start && !(prm->qp_warm_kappa > 0.0)) return set_err(NMPC_ERR_ARG, "qp_warm_kappa must be > 0");
     if (prm->qp_warm_iter_max < 0) return set_err(NMPC_ERR_ARG, "qp_warm_iter_max must be >= 0");
+    if (!(prm->qp_infeas_lambda >= 0.0)) return set_err(NMPC_ERR_ARG, "qp_infeas_lambda must be >= 0 (0: off)");
     if (prm->qp_ipm == NMPC_IPM_SINGLE &&
         !(prm->qp_sigma_lo > 0.0 && prm->qp_sigma_lo <= prm->qp_sigma_hi && prm->qp_sigma_hi <= 1.0))
         return set_err(NMPC_ERR_ARG, "qp_sigma_lo / qp_sigma_hi need 0 < lo <= hi <= 1");
@@ -289,6 +293,9 @@ int nmpc_model_params_default(int model, int N, nmpc_model_params* prm)
     // metric 3.00 -> 3.73 M it/s (cold 3.75, <= 10: 3.74, <= 16: 3.19), diff1024 0.87 -> 1.02 M. omni4 and tric
     // (kappa 0.01) lose with the rule (omni4 2.88 -> 2.47, tric 3.06 -> 2.82, mixed 4.52 -> 3.96 M): always warm
     prm->qp_warm_iter_max = (model == NMPC_MODEL_DIFF2AMR) ? 12 : 0;
+    // early status-4 exit for infeasible QPs (a carried vel-ref far outside its bound): multipliers > 1e5 x the
+    // weight scale with an open bound residual (tools/infeas_study.py: feasible bench QPs stay below 88)
+    prm->qp_infeas_lambda = 1e5;
     return NMPC_OK;
 }
 
@@ -420,6 +427,7 @@ int nmpc_batch_solve(nmpc_batch* b, int B, const float* x0, const float* yref, i
     std::memset(&a, 0, sizeof(a));
     a.B = B;
     a.stride = b->capacity;
+    a.sstride = b->capacity;
     a.xbar = b->xbar;
     a.ubar = b->ubar;
     a.carried = b->carried;
@@ -454,6 +462,7 @@ int nmpc_batch_solve_iterate(nmpc_batch* b, int B, const float* x0, const float*
     std::memset(&a, 0, sizeof(a));
     a.B = B;
     a.stride = ld;
+    a.sstride = b->capacity;  // the scratch planes follow the allocation, not the caller's ld
     a.xbar = xbar;
     a.ubar = ubar;
     a.carried = b->carried;  // run mode only
@@ -482,6 +491,7 @@ int nmpc_batch_run(nmpc_batch* b, int B, const float* pose, const float* vel, co
     std::memset(&a, 0, sizeof(a));
     a.B = B;
     a.stride = b->capacity;
+    a.sstride = b->capacity;
     a.xbar = b->xbar;
     a.ubar = b->ubar;
     a.carried = b->carried;
@@ -519,6 +529,7 @@ int nmpc_batch_run_path(nmpc_batch* b, int B, const float* pose, const float* ve
     std::memset(&a, 0, sizeof(a));
     a.B = B;
     a.stride = b->capacity;
+    a.sstride = b->capacity;
     a.xbar = b->xbar;
     a.ubar = b->ubar;
     a.carried = b->carried;
@@ -574,6 +585,15 @@ int nmpc_batch_forget_warm(nmpc_batch* b, int B, const unsigned char* mask, void
     if (B == 0) return NMPC_OK;
     hipLaunchKernelGGL(k_forget_warm, dim3((B + 255) / 256), dim3(256), 0, (hipStream_t)stream, b->warm, mask, B);
     return hip_err(hipGetLastError(), "forget_warm launch");
+}
+
+int nmpc_batch_warm_rule(const nmpc_batch* b, int* warm, int* warm_iter_max, int* iter_max)
+{
+    if (!b) return set_err(NMPC_ERR_ARG, "batch is NULL");
+    if (warm) *warm = b->kp.warm ? 1 : 0;
+    if (warm_iter_max) *warm_iter_max = b->kp.warm_iter_max;
+    if (iter_max) *iter_max = b->kp.iter_max;
+    return NMPC_OK;
 }
 
 int nmpc_batch_warm_state(nmpc_batch* b, unsigned char** warm, float** scratch, size_t* scratch_bytes)

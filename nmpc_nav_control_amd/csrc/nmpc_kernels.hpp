@@ -17,7 +17,8 @@ enum KernelMode { kModeSolve = 0, kModeRun = 1 };
 // Device pointers of one batched launch. Public inputs/outputs are [field][B] (instance-minor);
 // the device-resident state (iterate, carried refs, scratch) is [field][stride], stride = capacity.
 struct KArgs {
-    int B, stride;
+    int B, stride;   // stride: leading dimension of xbar / ubar / carried (the capacity, or the caller's ld)
+    int sstride;     // the handle's capacity: row count of the scratch planes (DZ plane, dummy blocks), whatever stride is
     float* xbar;     // [(N+1)*NX][stride]   SQP iterate, warm start of the next tick
     float* ubar;     // [N*NU][stride]
     float* carried;  // [NBX][stride]        ref states carried between ticks (run mode)

@@ -32,6 +32,9 @@ struct KParams {
     int warm;
     float warm_kappa;
     int warm_iter_max;  // a solve that needed more IPM iterations starts the next one cold
+    // infeasibility exit: multiplier threshold qp_infeas_lambda (+inf: off), scaled in the kernel by
+    // max(1, max(wmax, the robot's terminal weights) / 10); wmax = the largest stage weight
+    float infeas_lam, wmax;
 };
 
 enum ModelId { kDiff = 0, kOmni4 = 1, kTric = 2 };

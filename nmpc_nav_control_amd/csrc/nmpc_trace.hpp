@@ -4,13 +4,20 @@
 // launches and waits per call; without a tool attached a push / pop is a call into an idle library.
 #pragma once
 
+// Built with NMPC_ROCTX (the Makefile sets it when rocprofiler-sdk's roctx is installed); otherwise a no-op.
+#ifdef NMPC_ROCTX
 #include <rocprofiler-sdk-roctx/roctx.h>
+#endif
 
 namespace nmpc {
 
 struct TraceRange {
+#ifdef NMPC_ROCTX
     explicit TraceRange(const char* name) { roctxRangePushA(name); }
     ~TraceRange() { roctxRangePop(); }
+#else
+    explicit TraceRange(const char*) {}
+#endif
     TraceRange(const TraceRange&) = delete;
     TraceRange& operator=(const TraceRange&) = delete;
 };

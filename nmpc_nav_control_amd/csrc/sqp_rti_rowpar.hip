@@ -123,12 +123,12 @@ __global__ __launch_bounds__(64 * W, 1) void k_sqp_rti_rowpar(KParams P, KArgs a
     float* const rbase = a.scratch + (size_t)inst * (N + 1) * KS;
     float* const tbase = rbase + (lv ? r : 0) * rec_lane<RS, QM>();   // idle slots read slot 0
     float* const tbase_own = rbase + r * rec_lane<RS, QM>();          // every lane's own slot
-    float* const dzbase = a.scratch + (size_t)a.stride * (N + 1) * KS + (size_t)inst * (N + 1) * 16 + r;
+    float* const dzbase = a.scratch + (size_t)a.sstride * (N + 1) * KS + (size_t)inst * (N + 1) * 16 + r;
     // Stores of the serial phases: wave 0 stores (its four rows the same values to the same addresses, as one
     // row would); waves 1.. store into a dummy stage block of their own with the same slot layout (the same
     // coalescing as the real store; nobody reads it). Idle slots and rows past the last stage of a stage-parallel
     // phase store into tdummy.
-    float* const dummy = a.scratch + (size_t)a.stride * (N + 1) * 16 * (RS + 1);
+    float* const dummy = a.scratch + (size_t)a.sstride * (N + 1) * 16 * (RS + 1);
     float* const wblk = dummy + ((size_t)(inst & 255) * 4 + wave) * KS;      // this wave's dummy stage block
     float* const wdz = dummy + (size_t)256 * 4 * KS + ((size_t)(inst & 255) * 4 + wave) * 16 + r;  // dummy DZ
     const bool w0 = wave == 0;
@@ -348,6 +348,7 @@ __global__ __launch_bounds__(64 * W, 1) void k_sqp_rti_rowpar(KParams P, KArgs a
                         (s_ref[N * 3 + 2] == s_ref[(N - 1) * 3 + 2]);
         we_lane = (eq ? 100.0f : 1.0f) * w_lane;
     }
+    const float lam_thr = P.infeas_lam * fmaxf(1.0f, fmaxf(P.wmax, row_max16(is_x ? we_lane : 0.0f)) * 0.1f);
     float sum_c0 = 0.0f;
     for (int j = 0; j < NR; j++) {
         const int kr = j * ROWS + q;
@@ -605,7 +606,7 @@ __global__ __launch_bounds__(64 * W, 1) void k_sqp_rti_rowpar(KParams P, KArgs a
         } else if (failf > 0.0f) {
             status = (mu <= kBreakdownMuT && res_ineq <= P.tol_ineq * 10.0f) ? 0 : 4;
             stop = true;
-        } else if (lam_max > kInfeasLambda && res_ineq > kInfeasRes) {
+        } else if (lam_max > lam_thr && res_ineq > kInfeasRes) {
             status = 4;
             stop = true;
         } else {

@@ -144,7 +144,7 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a)
     // stores that lanes without work issue unconditionally
     float* const tdummy = a.scratch + (size_t)inst * (N + 1) * 16 * RS + (size_t)N * 16 * RS + 15 * rec_lane<RS, QM>();
     // this lane's DZ in the dense plane after the records: dzbase + k * 16 (every lane its own float)
-    float* const dzbase = a.scratch + (size_t)a.stride * (N + 1) * 16 * RS + (size_t)inst * (N + 1) * 16 + r;
+    float* const dzbase = a.scratch + (size_t)a.sstride * (N + 1) * 16 * RS + (size_t)inst * (N + 1) * 16 + r;
     // IPM warm start: the bound multipliers of the robot's previous successful solve are still in its records
     const bool warm = P.warm && a.warm && a.warm[inst] && !(a.reset && a.reset[inst]);
     constexpr int KS = 16 * RS;
@@ -553,6 +553,8 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a)
     for (int i = 0; i < NX; i++) gcol64[i] = (double)gcol[i];
 
     STAMP(1);
+    // infeasibility threshold of this robot: qp_infeas_lambda scaled by its largest weight (terminal hack included)
+    const float lam_thr = P.infeas_lam * fmaxf(1.0f, fmaxf(P.wmax, row_max16(is_x ? we_lane : 0.0f)) * 0.1f);
     const int m = N * NU + N * M::NBX;
     const float inv_m2 = 0.5f / (float)m;
     sum_c0 = row_sum16(lv ? sum_c0 : 0.0f);
@@ -833,7 +835,7 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a)
             } else if (failf > 0.0f) {
                 status = (mu <= kBreakdownMuT && res_ineq <= P.tol_ineq * 10.0f) ? 0 : 4;
                 stop = true;
-            } else if (lam_max > kInfeasLambda && res_ineq > kInfeasRes) {
+            } else if (lam_max > lam_thr && res_ineq > kInfeasRes) {
                 status = 4;  // primal infeasible: stop now instead of holding the wave for qp_iter_max iterations
                 stop = true;
             } else {

@@ -69,7 +69,7 @@ constexpr float kCompMaxRatio = 30.0f;
 // diverge while the bound residual cannot close. A feasible QP of this OCP keeps them at the size of its cost
 // weights (max 88 over 768 bench-loop QPs with renewals, against > 1e5 by IPM iteration 13-20 for QPs made
 // infeasible as the failure test does; tools/infeas_study.py); the oracle uses the same two constants
-constexpr float kInfeasLambda = 1e5f;
+// (the multiplier threshold is nmpc_model_params.qp_infeas_lambda, 1e5 by default, scaled by the largest weight)
 constexpr float kInfeasRes = 1e-3f;
 constexpr float kWarmLambdaCap = 1e3f;  // largest warm-started bound multiplier
 constexpr float kFar = 1e30f;  // sentinel bound / slack of unbounded slots (z + kFar - kFar == 0 in fp32)

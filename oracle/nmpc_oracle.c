@@ -79,6 +79,7 @@ void oc_params_default(int model, int N, oc_params* prm)
     prm->mu0 = 1.0;
     prm->thr0 = 0.5;
     prm->tau = 0.995;
+    prm->infeas_lambda = OC_INFEAS_LAMBDA;
 }
 
 /* ------------------------------------------------------------------------------------------------ */
@@ -411,6 +412,11 @@ int oc_qp_ipm(const oc_params* prm, const oc_qp* qp, oc_qp_sol* sol, oc_stats* s
         m += c;
     }
     const double m2 = 2.0 * m;
+    /* infeasibility threshold: infeas_lambda scaled by the largest stage / terminal weight (0: no such exit) */
+    double wmax = 0.0;
+    for (int i = 0; i < prm->ny; i++) wmax = fmax(wmax, prm->W[i]);
+    for (int i = 0; i < nx; i++) wmax = fmax(wmax, qp->Hx[N * nx + i]);
+    const double lam_thr = prm->infeas_lambda > 0.0 ? prm->infeas_lambda * fmax(1.0, 0.1 * wmax) : INFINITY;
 
     double* buf = (double*)calloc((size_t)(N + 1) * (4 * nx + 4 * nu + 4 * NB) + (size_t)N * (nu * nx + nu * nu + nu),
                                   sizeof(double));
@@ -501,7 +507,7 @@ int oc_qp_ipm(const oc_params* prm, const oc_qp* qp, oc_qp_sol* sol, oc_stats* s
          * QP of this OCP keeps them at the size of its cost weights: max 88 over 768 bench-loop QPs against > 1e5
          * by iteration 13-20 of the infeasible ones, tools/infeas_study.py) -> QP failure, the status the
          * wrapper turns into an exception (NMPCNavControl.cpp:14-23) */
-        if (lam_max > OC_INFEAS_LAMBDA && res_ineq > OC_INFEAS_RES) { status = 4; break; }
+        if (lam_max > lam_thr && res_ineq > OC_INFEAS_RES) { status = 4; break; }
         if (it >= prm->iter_max) { status = 0; break; } /* max-iter tolerated in RTI */
 
         /* Newton solves sharing one factorisation: pass 0 predictor (affine, target 0); pass 1 Mehrotra

@@ -56,6 +56,9 @@ typedef struct oc_params {
     int iter_max;
     double tol_stat, tol_ineq, tol_comp;
     double mu0, thr0, tau;
+    /* infeasibility exit: multiplier threshold infeas_lambda * max(1, w_max / 10) (w_max: the largest stage or
+     * terminal weight of the QP); 0 = off (HPIPM: run to iter_max). Default OC_INFEAS_LAMBDA, as the device. */
+    double infeas_lambda;
 } oc_params;
 
 typedef struct oc_stats {

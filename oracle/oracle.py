@@ -33,6 +33,7 @@ class OcParams(ctypes.Structure):
         ("iter_max", ctypes.c_int),
         ("tol_stat", ctypes.c_double), ("tol_ineq", ctypes.c_double), ("tol_comp", ctypes.c_double),
         ("mu0", ctypes.c_double), ("thr0", ctypes.c_double), ("tau", ctypes.c_double),
+        ("infeas_lambda", ctypes.c_double),
     ]
 
 

@@ -184,3 +184,50 @@ def test_unsupported_ocp_data_rejected_and_recovered(built):
     ctl._cset(0, "ubx", x0 + 0.1)  # x0 must stay an equality
     with pytest.raises(RuntimeError):
         ctl._solve()
+
+
+def test_capsule_cold_start_option_matches_oracle(built):
+    """ocp_nlp_solver_opts_set(.., "qp_warm_start", 0): every solve starts the IPM cold, as HPIPM does in the
+    reference's generated solver (scripts/diff/generate_c_code.py:68-74). Same QP solutions as the oracle; the
+    cold capsule needs at least as many IPM iterations as the warm one over the same closed loop."""
+    iters = {}
+    for warm in (1, 0):
+        ctl, Cmd = make("diff")
+        ctl.solver_opts_set("qp_warm_start", warm)
+        o = Oracle("diff", N)
+        xb, ub = o.iterate_create()
+        carried = np.zeros(o.nbx)
+        pose, vel = np.array([0.05, -0.02, 2.9]), np.array([0.1, 0.0, 0.05])
+        its = []
+        for tick in range(10):
+            refs = path(tick, N + 1)
+            ok, _ = ctl.run(Pose(*pose), Vel(*vel), refs, Cmd())
+            assert ok
+            its.append(ctl.qp_iter())
+            traj = np.array([[p.x, p.y, p.theta] for p in refs])
+            x0, yref, We = o.prepare(pose, vel, 0.0, traj, carried)
+            s, st, xb, ub = o.sqp_rti(xb, ub, x0, yref, We)
+            assert s == 0
+            _, carried = o.post(x0, ub[0])
+            np.testing.assert_allclose(ctl.u0, ub[0], atol=TOL)
+            xn, v3, _ = plant("diff", o, x0, ub[0])
+            pose, vel = xn[:3], np.array(v3)
+        iters[warm] = its
+    assert sum(iters[0][1:]) >= sum(iters[1][1:]), iters
+
+
+def test_capsule_infeasible_qp_runs_to_iter_max(built):
+    """The capsule ABI keeps acados' semantics for a hard QP: no early infeasibility exit (qp_infeas_lambda 0),
+    the IPM runs to qp_iter_max and the solve reports status 0 (acados' RTI accepts HPIPM's max-iter exit), while
+    the batched default exits with status 4 (tests/test_gpu_fleet.py). A carried vel-ref of 50 m/s against the
+    1 m/s bound cannot be brought inside it within one step."""
+    ctl, Cmd = make("diff")
+    ctl.solver_opts_set("qp_iter_max", 30)
+    x0 = np.array([0.0, 0.0, 0.2, 0.0, 0.0, 50.0, 0.0])
+    ctl._cset(0, "lbx", x0)
+    ctl._cset(0, "ubx", x0)
+    ctl.yref[:, :3] = [0.5, 0.2, 0.3]
+    for k in range(N + 1):
+        ctl._wset(k, "yref", ctl.yref[k] if k < N else ctl.yref[k][:ctl.nx])
+    ctl._solve()
+    assert ctl.status == 0 and ctl.qp_iter() == 30, (ctl.status, ctl.qp_iter())

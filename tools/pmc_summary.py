@@ -67,7 +67,38 @@ def issue_est(tot):
     return cycles / (4.0 * tot["SQ_WAVE_CYCLES"])
 
 
+def mall(prefix):
+    """--mall <prefix>: tools/mall_calibration.sh's two runs of tools/ubench_mall -> requests per KiB read and the
+    verdict on TCC_EA0_RDREQ_DRAM (the last launch of each run; its JSON line is in the run's log)."""
+    res = {}
+    for mib in (64, 2048):
+        d = load(f"{prefix}_{mib}", None)
+        k = next((n for n in d if "k_stream" in n), None)
+        line = next((ln for ln in open(f"{prefix}_{mib}.log") if ln.startswith("{")), None)
+        bench = json.loads(line) if line else {}
+        c = d.get(k, {}) if k else {}
+        b = bench.get("bytes_read_per_launch")
+        kib = b / 1024 if b else None
+        res[f"table_{mib}MiB"] = {
+            "bytes_read_per_launch": b, "GBs": bench.get("GBs"),
+            "rdreq_per_kib": c.get("TCC_EA0_RDREQ_sum", 0) / kib if kib else None,
+            "rdreq_dram_per_kib": c.get("TCC_EA0_RDREQ_DRAM_sum", 0) / kib if kib else None,
+            "rdreq_32b_per_kib": c.get("TCC_EA0_RDREQ_32B_sum", 0) / kib if kib else None,
+            "dram_share": (c.get("TCC_EA0_RDREQ_DRAM_sum", 0) / c["TCC_EA0_RDREQ_sum"]) if c.get("TCC_EA0_RDREQ_sum") else None}
+    lo, hi = res["table_64MiB"], res["table_2048MiB"]
+    if lo["dram_share"] is not None and hi["dram_share"] is not None:
+        sep = lo["dram_share"] < 0.5 * hi["dram_share"]
+        res["verdict"] = ("TCC_EA0_RDREQ_DRAM excludes Infinity-Cache hits: the resident table's re-reads are not "
+                          "DRAM-destined" if sep else
+                          "TCC_EA0_RDREQ_DRAM counts Infinity-Cache hits as DRAM-destined (same share for a resident "
+                          "and a non-resident table): the L2 memory-side counters bound DRAM bytes from above only")
+    res["source"] = "tools/mall_calibration.sh (tools/ubench_mall.hip: 64 MiB x 16 reps resident, 2 GiB x 2 reps not)"
+    print(json.dumps(res, indent=1))
+
+
 def main():
+    if sys.argv[1] == "--mall":
+        return mall(sys.argv[2])
     prefix, key = sys.argv[1], sys.argv[2]
     arg = lambda k, d=None: sys.argv[sys.argv.index(k) + 1] if k in sys.argv else d  # noqa: E731
     rnd = arg("--round", "r03")
@@ -119,6 +150,10 @@ def main():
                                               if tot.get("SQ_INSTS_VALU_FLOPS_FP64") else None),
            "executed_flops_fp32_per_launch": (64 * tot["SQ_INSTS_VALU_FLOPS_FP32"]
                                               if tot.get("SQ_INSTS_VALU_FLOPS_FP32") else None),
+           # pass 5: L2 memory-side requests and the share destined for DRAM (TCC_EA0_*REQ_DRAM); whether that
+           # share excludes Infinity-Cache hits is what tools/ubench_mall.hip calibrates (profiles/<round>/pmc/)
+           "ea_rdreq": tot.get("TCC_EA0_RDREQ_sum"), "ea_rdreq_dram": tot.get("TCC_EA0_RDREQ_DRAM_sum"),
+           "ea_wrreq": tot.get("TCC_EA0_WRREQ_sum"), "ea_wrreq_dram": tot.get("TCC_EA0_WRREQ_DRAM_sum"),
            "source": os.path.basename(prefix.rstrip("/")), "source_commit": commit,
            "dispatches_averaged": f"last {last} per kernel" if last else "all",
            "note": "per launch (mixed: summed over the per-model launches of one step); "
