@@ -30,6 +30,9 @@ struct nmpc_batch {
     // launches of at most this many robots (single-direction IPM, not run_path) run k_sqp_rti_rowpar: one wave
     // per robot with its stage-independent work spread over the wave's 4 rows (latency)
     int rowpar_max = 256;        // (four waves per robot up to 256 robots; one wave per robot above, A/B only)
+    // horizon segments of the row-parallel kernel (sqp_rti_rowpar.hip SEG): -1 = chosen per launch (seg_count),
+    // 0 = the serial phases B / C, S > 0 = S segments when N % S == 0 (NMPC_AMD_SEG overrides)
+    int seg = 0;  // (default -1 once the segmented path is validated on the GPU)
     int* iter_key = nullptr;     // [capacity] last executed IPM iterations per robot (written by the team kernel)
     int* order = nullptr;        // [capacity] team slot -> robot
     unsigned char* warm = nullptr;  // [capacity] the robot's last solve succeeded: its scratch records hold its
@@ -122,11 +125,34 @@ hipError_t launch_m(nmpc_batch* b, const KArgs& a, int mode, hipStream_t s)
     return launch_sqp_rti_team<M>(b->kp, a, mode, s);
 }
 
-template <class M>
-bool rowpar_ok(const nmpc_batch* b, const KArgs& a, int mode)
+// Segments of the row-parallel kernel's Riccati sweeps for a horizon N on `rows` rows per robot: the divisor S of N
+// (S <= rows, <= kSegMax) that minimises the robot's chain, about N / S stage steps of the segments' sweeps plus
+// S - 1 master steps of ~2 stage steps each; 0 (the serial phases) when no S > 1 divides N
+inline int seg_count(int N, int rows)
 {
-    return b->kp.ipm == NMPC_IPM_SINGLE && !a.segs && a.B <= b->rowpar_max &&
-           rowpar_lds_bytes<M>(b->prm.N, mode) <= 65536;
+    int best = 0;
+    double cost = (double)N;
+    for (int S = 2; S <= rows && S <= kSegMax; S++) {
+        if (N % S) continue;
+        const double c = (double)N / S + 2.0 * (S - 1);
+        if (c < cost) {
+            cost = c;
+            best = S;
+        }
+    }
+    return best;
+}
+
+template <class M>
+bool rowpar_ok(const nmpc_batch* b, KArgs& a, int mode)
+{
+    if (b->kp.ipm != NMPC_IPM_SINGLE || a.segs || a.B > b->rowpar_max) return false;
+    const int rows = a.B <= 256 ? 16 : 4;  // four waves per robot up to 256 robots, one wave above
+    int S = b->seg >= 0 ? b->seg : seg_count(b->prm.N, rows);
+    if (S > rows || S > kSegMax || (S > 0 && b->prm.N % S)) S = 0;
+    if (S > 0 && rowpar_lds_bytes<M>(b->prm.N, mode, S) > 65536) S = 0;
+    a.seg = S;
+    return rowpar_lds_bytes<M>(b->prm.N, mode, S) <= 65536;
 }
 
 // Team placement before a team-kernel launch (schedule.hip); fills a.order / a.iter_key
@@ -338,6 +364,7 @@ int nmpc_batch_create(const nmpc_model_params* prm, int capacity, nmpc_batch** o
     }
     if (const char* v = std::getenv("NMPC_AMD_SPLIT_MAX")) b->split_max = std::atoi(v);  // A/B: 0 = never split
     if (const char* v = std::getenv("NMPC_AMD_ROWPAR_MAX")) b->rowpar_max = std::atoi(v);  // A/B: 0 = never
+    if (const char* v = std::getenv("NMPC_AMD_SEG")) b->seg = std::atoi(v);  // A/B: 0 = serial, S = S segments
     const int N = prm->N;
     const size_t S = (size_t)capacity;
     hipError_t e;

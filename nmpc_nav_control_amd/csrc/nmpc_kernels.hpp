@@ -60,6 +60,8 @@ struct KArgs {
     int rowpar;     // 0: team kernel; W > 0: k_sqp_rti_rowpar with W waves per robot
     int split;      // one 256-lane block per robot: P0's integrations spread over its 16 rows (4 waves, stage k on
                     // row k mod 16, joined by a block barrier); small batches
+    int seg;        // k_sqp_rti_rowpar: horizon segments S (N % S == 0) whose Riccati sweeps run in parallel on S rows,
+                    // joined by a master recursion over the segment boundaries; 0: the serial phases B / C
 };
 
 template <class M>
@@ -70,7 +72,8 @@ hipError_t launch_sqp_rti_team(const KParams& P, const KArgs& a, int mode, hipSt
 template <class M>
 hipError_t launch_sqp_rti_rowpar(const KParams& P, const KArgs& a, int mode, hipStream_t stream);
 template <class M>
-size_t rowpar_lds_bytes(int N, int mode);
+size_t rowpar_lds_bytes(int N, int mode, int seg);
+constexpr int kSegMax = 8;  // most horizon segments of the segmented row-parallel kernel
 template <class M>
 hipError_t launch_fleet_sim(const KParams& P, int B, int stride, float* path, float* s, float* pose, float* vel,
                             float* steer, const float* u0, const int* status, const float* carried, float* traj,

@@ -40,6 +40,51 @@ struct RowRec {
     static_assert(LM + NU <= Z && Z < TL, "LR / LM below Z");
 };
 
+// LDS of the segmented phases (SEG, a.seg = S > 0), in floats from its base (8-byte aligned; fp64 parts at even
+// offsets). Per segment q: the entry quantities of its backward sweep -- P (fp64 rows), pbar, Phi, Gam, t; per master
+// step i: Q_i = Phat_{i+1} X_i^-1 (fp64), c_i, phat_{i+1}; GJ / transpose scratch; the boundary states s_q and
+// costates lam_q; the lam-sensitivity Z of every stage's LR (rows of the NU input lanes).
+template <class M>
+struct SegLayout {
+    static constexpr int NX = M::NX, NU = M::NU, NXP = (M::NX + 3) / 4 * 4;
+    int SUM_P, SUM_PB, SUM_PHI, SUM_GAM, SUM_T, QS, CS, PHS, QT, TV, SL, ZL;
+    __host__ __device__ explicit SegLayout(int S)
+    {
+        SUM_P = 0;                          // [S][NX][NX] double
+        SUM_PB = SUM_P + 2 * S * NX * NX;   // [S][NX]
+        SUM_PHI = SUM_PB + S * NX;          // [S][NX][NX]
+        SUM_GAM = SUM_PHI + S * NX * NX;    // [S][NX][NX]
+        SUM_T = SUM_GAM + S * NX * NX;      // [S][NX]
+        QS = (SUM_T + S * NX + 1) / 2 * 2;  // [S][NX][NX] double
+        CS = QS + 2 * S * NX * NX;          // [S][NX] double
+        PHS = CS + 2 * S * NX;              // [S][NX] double
+        QT = PHS + 2 * S * NX;              // [NX][NX] double
+        TV = QT + 2 * NX * NX;              // [NX] double
+        SL = TV + 2 * NX;                   // [S + 1][2][NX]: s_q, lam_q
+        ZL = SL + (S + 1) * 2 * NX;         // [N + 1][NU][NXP]
+    }
+    __host__ __device__ size_t floats(int N) const { return (size_t)ZL + (size_t)(N + 1) * NU * NXP; }
+};
+
+// layout of the kernel's dynamic LDS (floats): P0's stage inputs [N+1][SF][16], reference poses [N+1][3], block
+// reductions [W][8], dx [N+1][16], unwrapped references [N+1][3]; then (SEG) the segment area, which reuses the
+// stage-input region when it fits there (P0 is done with it before the first IPM iteration)
+template <class M>
+struct RowLds {
+    static constexpr int SF = 5 + M::NGV;
+    __host__ __device__ static constexpr size_t base_floats(int N) { return (size_t)(N + 1) * (16 * SF + 3 + 16 + 3) + 32; }
+    __host__ __device__ static size_t seg_off(int N, int S)
+    {
+        return SegLayout<M>(S).floats(N) <= (size_t)(N + 1) * SF * 16 ? 0 : (base_floats(N) + 3) / 4 * 4;
+    }
+    __host__ __device__ static size_t floats(int N, int S)
+    {
+        if (S <= 0) return base_floats(N);
+        const size_t end = seg_off(N, S) + SegLayout<M>(S).floats(N);
+        return end > base_floats(N) ? end : base_floats(N);
+    }
+};
+
 #ifdef NMPC_STAMPS
 // diagnostic build only: s_memtime after each phase, robots 0..255, lane 0: [0] start, [1] P0a, [2] P0b, then per
 // IPM iteration it: [3 + 4 it + 0..3] after phases A, B, C, D
@@ -65,6 +110,20 @@ __device__ __forceinline__ void ld_range(const float* p, float (&v)[RS])
     rec_load_range<F0, F1, RS, QM>(p, v);
 }
 
+// fp64 value of lane `lane` (wave-uniform) in every lane
+__device__ __forceinline__ double readlane_d(double v, int lane)
+{
+    const int lo = __builtin_amdgcn_readlane(__double2loint(v), lane);
+    const int hi = __builtin_amdgcn_readlane(__double2hiint(v), lane);
+    return __hiloint2double(hi, lo);
+}
+
+// LDS writes of this wave complete before its next LDS reads (the master's cross-lane exchanges within one wave)
+__device__ __forceinline__ void lds_fence()
+{
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+}
+
 // cross-row reductions of the wave (the four rows hold disjoint stages in the stage-parallel phases)
 __device__ __forceinline__ float wave_sum_rows(float v)
 {
@@ -84,8 +143,13 @@ __device__ __forceinline__ float wave_min_rows(float v)
 
 // W waves per robot (one per SIMD): the stage-parallel phases run on all 4 W rows; every wave runs the serial
 // phases (identically) and wave 0 stores their results (the other waves store into dummy stage blocks of the same
-// layout: per-lane scattered dummy addresses made the serial phases' stores 1.6x slower, measured)
-template <class M, int W>
+// layout: per-lane scattered dummy addresses made the serial phases' stores 1.6x slower, measured).
+// SEG: the horizon is cut into a.seg segments of L = N / S stages whose Riccati sweeps (phase B) and forward
+// recursions (phase C) run at the same time, one segment per row, joined by a master recursion over the segment
+// boundaries (DESIGN.md "Segmented Riccati"); a robot's serial chain shrinks from N + 1 stage steps to L + 1 plus S - 1
+// master steps. The rhs is built in absolute form (no adjoint), so the stationarity residual of the stopping rule is
+// evaluated by its own serial adjoint pass, only when the rest of the exit test already holds.
+template <class M, int W, bool SEG>
 __global__ __launch_bounds__(64 * W, 1) void k_sqp_rti_rowpar(KParams P, KArgs a, int mode)
 {
     using R = RowRec<M>;
@@ -440,6 +504,28 @@ __global__ __launch_bounds__(64 * W, 1) void k_sqp_rti_rowpar(KParams P, KArgs a
         }
     };
 
+    // SEG: the segment area of the LDS (RowLds / SegLayout), and the serial adjoint pass of the stopping rule:
+    // pi_k = c0_x + A_k' pi_{k+1} on the state slots, the input stationarity residual c0_u + B_k' pi_{k+1}
+    const SegLayout<M> SegL(SEG ? a.seg : 1);
+    float* const seg_lds = s_row + (SEG ? RowLds<M>::seg_off(N, a.seg) : 0);
+    auto adjoint = [&](float& res_stat, float& cpi_max) {
+        float piv = 0.0f, rs = 0.0f, cm = 0.0f;
+        serial(std::integral_constant<int, R::GV>{}, std::integral_constant<int, R::C0 + 1>{}, std::false_type{}, N, 0,
+               -1, [&](int k, float (&rc)[RS]) {
+            const bool vu = is_u && k < N;
+            const bool vx = is_x && k >= 1;
+            float Gc[NX];
+            column(rc, Gc);
+            const float cpi = (k < N) ? dot_x<NX, NU>(0.0f, piv, Gc) : 0.0f;
+            const float base = rc[R::C0] + cpi;
+            rs = nan_max(rs, vu ? fabsf(base) : 0.0f);
+            cm = fmaxf(cm, vu ? fabsf(cpi) : 0.0f);
+            piv = vx ? base : 0.0f;
+        });
+        res_stat = row_max16(lv ? rs : 0.0f);
+        cpi_max = row_max16(lv ? cm : 0.0f);
+    };
+
     // ---- interior-point iterations (single-direction rule) -----------------------------------------------------
     int status = 0, it_done = 0;
     float exit_res[3] = {0.0f, 0.0f, 0.0f};
@@ -516,34 +602,77 @@ __global__ __launch_bounds__(64 * W, 1) void k_sqp_rti_rowpar(KParams P, KArgs a
         const float mu = sum_c * inv_m2;
         RP_STAMP(3 + 4 * it);
 
-        // phase B (serial, N -> 0): adjoint, fp64 classic Riccati step, rhs / forward substitution
-        double Lrow[NV];
+        if constexpr (SEG) {
+            // ---- stopping rule first (phase A's sums); the stationarity residual needs the exact adjoint, a serial
+            // pass run only when the rest of the first exit clause holds (typically the last one or two iterations)
+            exit_res[1] = res_ineq;
+            exit_res[2] = mu;
+            float res_stat = -1.0f;
+            bool stop = false;
+            if (nanf_ > 0.0f || mu != mu) {
+                status = 1;
+                stop = true;
+            } else if (lam_max > lam_thr && res_ineq > kInfeasRes) {
+                status = 4;
+                stop = true;
+            } else {
+                const bool feas = res_ineq <= P.tol_ineq;
+                const bool cmax_ok = max_c <= kCompMaxRatio * P.tol_comp;
+                const bool stalled = mu <= P.tol_comp && mu > 0.5f * mu_prev;
+                if (feas && (mu <= 1e-2f * P.tol_comp || (stalled && cmax_ok))) {
+                    stop = true;
+                } else if (feas && mu <= P.tol_comp && cmax_ok) {
+                    float cpi_max;
+                    adjoint(res_stat, cpi_max);
+                    if (res_stat <= P.tol_stat || res_stat <= kStatRelT * fmaxf(sc0, cpi_max)) stop = true;
+                }
+                if (it >= P.iter_max) stop = true;
+            }
+            mu_prev = mu;
+            if (stop) {
+                if (res_stat < 0.0f) {
+                    float cm;
+                    adjoint(res_stat, cm);
+                }
+                exit_res[0] = res_stat;
+                it_done = it;
+                break;
+            }
+
+            // ---- phase B (segments in parallel, each N -> its first stage): fp64 Riccati step on the absolute
+            // rhs, plus the sensitivities to the segment's free end costate lam (Phi, Z) and the lam terms of its
+            // value (Gam, t). Row q takes stages [q L, (q + 1) L), the last row also the terminal stage N. Iteration
+            // j = 0 initialises: the last row with the terminal P_N, p_N; the others with P = 0, p = 0, Phi = I
+            const int Sg = a.seg, Ls = N / Sg;
+            const bool srow = q < Sg, slast = q == Sg - 1;
+            double Lrow[NV];
+            float pv = 0.0f, Phi[NX], Gam[NX], tt = 0.0f, nanb = 0.0f;
 #pragma unroll
-        for (int j = 0; j < NV; j++) Lrow[j] = 0.0;
-        float pv = 0.0f, piv = 0.0f, res_stat = 0.0f, cpi_max = 0.0f;
-        bool fail = false;
-        if (!(nanf_ > 0.0f || mu != mu)) {
-            serial(std::integral_constant<int, R::GV>{}, std::integral_constant<int, R::GH + 1>{},
-                   std::false_type{}, N, 0, -1, [&](int k, float (&rc)[RS]) {
-                const bool vu = is_u && k < N;
-                const bool vx = is_x && k >= 1;
-                const bool valid = vu || vx;
-                float Gc[NX];
-                column(rc, Gc);
-                const float cpi = (k < N) ? dot_x<NX, NU>(0.0f, piv, Gc) : 0.0f;
-                const float base = rc[R::C0] + cpi;
-                res_stat = fmaxf(res_stat, vu ? fabsf(base) : 0.0f);
-                cpi_max = fmaxf(cpi_max, vu ? fabsf(cpi) : 0.0f);
-                const float sig = rc[R::SIG];
-                const float ghat = valid ? (vu ? rc[R::GH] + base : rc[R::GH]) : 0.0f;
-                const float pi_new = vx ? base : 0.0f;
-                if (ghat != ghat) nanf_ = 1.0f;
-                if (k == N) {
-                    const double d = is_x ? (double)fmaxf(we_lane + sig, 0.0f) : 0.0;
+            for (int j = 0; j < NV; j++) Lrow[j] = 0.0;
 #pragma unroll
-                    for (int j = 0; j < NV; j++) Lrow[j] = (is_x && j == r) ? d : 0.0;
-                    pv = is_x ? ghat : 0.0f;
-                } else {
+            for (int c = 0; c < NX; c++) Phi[c] = Gam[c] = 0.0f;
+            bool fail = false;
+            if (4 * wave < Sg) {  // (wave-uniform) the wave holds a segment
+                auto kof = [&](int j) { return srow ? (q + 1) * Ls - j : N; };
+                auto bseg = [&](int j, float (&rc)[RS]) {
+                    const int k = kof(j);
+                    const bool vu = srow && is_u && k < N;
+                    const bool vx = srow && is_x && k >= 1;
+                    const bool valid = vu || vx;
+                    float Gc[NX];
+                    column(rc, Gc);
+                    const float sig = rc[R::SIG];
+                    const float ghat = valid ? rc[R::GH] + rc[R::C0] : 0.0f;
+                    if (ghat != ghat) nanb = 1.0f;
+                    if (j == 0) {
+                        const double d = (slast && is_x) ? (double)fmaxf(we_lane + sig, 0.0f) : 0.0;
+#pragma unroll
+                        for (int jj = 0; jj < NV; jj++) Lrow[jj] = (is_x && jj == r) ? d : 0.0;
+                        pv = (slast && is_x) ? ghat : 0.0f;
+#pragma unroll
+                        for (int c = 0; c < NX; c++) Phi[c] = (!slast && is_x && xi == c) ? 1.0f : 0.0f;
+                        return;
+                    }
                     double Gd[NX];
 #pragma unroll
                     for (int l = 0; l < NX; l++) Gd[l] = (l < NGV) ? (double)Gc[l] : gcol64[l];
@@ -554,120 +683,524 @@ __global__ __launch_bounds__(64 * W, 1) void k_sqp_rti_rowpar(KParams P, KArgs a
                     const double dg = valid ? (double)h_stage + (double)sig : 1.0;
                     double Lr[NV];
 #pragma unroll
-                    for (int j = 0; j < NV; j++) Lr[j] = onehot[j] * dg;
+                    for (int jj = 0; jj < NV; jj++) Lr[jj] = onehot[jj] * dg;
                     double pivot;
                     mrow_pg_block<NX, NU>(Lr, pivot, pg, Gd);
                     sfor<0, NU>([&](auto jc) {
-                        constexpr int j = decltype(jc)::value;
-                        if (!(pivot > 0.0)) fail = true;
+                        constexpr int j2 = decltype(jc)::value;
+                        if (!(pivot > 0.0) && srow) fail = true;
                         const double rd = drsq(fmax(pivot, 1e-300));
-                        const double lj = (r >= j) ? Lr[j] * rd : 0.0;
-                        Lr[j] = lj;
-                        chol_update<NX, NU, j>(Lr, lj, pivot);
+                        const double lj = (r >= j2) ? Lr[j2] * rd : 0.0;
+                        Lr[j2] = lj;
+                        chol_update<NX, NU, j2>(Lr, lj, pivot);
                     });
-                    float Lm[NU];
+                    float Lm[NU], rLm[NU];
 #pragma unroll
                     for (int qq = 0; qq < NU; qq++) {
                         Lm[qq] = (float)Lr[qq];
                         rc[R::LM + qq] = Lm[qq];
+                        rLm[qq] = frcp(Lm[qq]);
                     }
+                    // rhs (absolute form): w = g^ + G' p_{k+1}, forward substitution over the input block
                     float y = dot_x<NX, NU>(ghat, pv, Gc);
-                    float my_lr = 0.0f;
+                    float my_lr = 0.0f, lrv[NU];
                     sfor<0, NU>([&](auto jc) {
-                        constexpr int j = decltype(jc)::value;
-                        const float lrj = bc<j>(y * frcp(Lm[j]));
-                        if (r == j) my_lr = lrj;
-                        y -= Lm[j] * lrj;
+                        constexpr int j2 = decltype(jc)::value;
+                        const float lrj = bc<j2>(y * rLm[j2]);
+                        lrv[j2] = lrj;
+                        if (r == j2) my_lr = lrj;
+                        y -= Lm[j2] * lrj;
                     });
                     rc[R::LR] = my_lr;
                     pv = is_x ? y : 0.0f;
-#pragma unroll
-                    for (int j = 0; j < NV; j++) Lrow[j] = Lr[j];
-                    // LR, LM (every row stores the same values; idle slots store into the dummy record)
-                    rec_store_range<R::LR, R::LM + NU, RS, QM>(
-                        lv ? (w0 ? tbase + (size_t)k * KS : wblk + r * rec_lane<RS, QM>()) : tdummy, rc);
-                }
-                piv = pi_new;
-            });
-        }
-        RP_STAMP(4 + 4 * it);
-        res_stat = row_max16(lv ? res_stat : 0.0f);
-        const float stat_scale = fmaxf(sc0, row_max16(lv ? cpi_max : 0.0f));
-        nanf_ = row_max16(nanf_);
-        const float failf = row_max16(fail ? 1.0f : 0.0f);
-        // stopping rule of k_sqp_rti_team (DESIGN.md "Stopping rule")
-        exit_res[0] = res_stat;
-        exit_res[1] = res_ineq;
-        exit_res[2] = mu;
-        bool stop = false;
-        if (nanf_ > 0.0f || mu != mu) {
-            status = 1;
-            stop = true;
-        } else if (failf > 0.0f) {
-            status = (mu <= kBreakdownMuT && res_ineq <= P.tol_ineq * 10.0f) ? 0 : 4;
-            stop = true;
-        } else if (lam_max > lam_thr && res_ineq > kInfeasRes) {
-            status = 4;
-            stop = true;
-        } else {
-            const bool stat_ok = res_stat <= P.tol_stat || res_stat <= kStatRelT * stat_scale;
-            const bool cmax_ok = max_c <= kCompMaxRatio * P.tol_comp;
-            const bool stalled = mu <= P.tol_comp && mu > 0.5f * mu_prev;
-            if (res_ineq <= P.tol_ineq &&
-                ((stat_ok && mu <= P.tol_comp && cmax_ok) || mu <= 1e-2f * P.tol_comp || (stalled && cmax_ok)))
-                stop = true;
-            if (it >= P.iter_max) stop = true;
-        }
-        mu_prev = mu;
-        if (stop) {
-            it_done = it;
-            break;
-        }
-        __syncthreads();  // LR / LM of every stage
-
-        // phase C (serial, 0 -> N): the direction's input part from the stored factor, its state part from the
-        // dynamics; every row the same (identical DZ stores)
-        sigma_mu = tg_rhs;
-        {
-            float dxs = 0.0f;
-            serial(std::integral_constant<int, 0>{}, std::integral_constant<int, R::GV + NGV>{}, std::false_type{},
-                   0, N, 1, [&](int k, float (&rc)[RS]) {
-                const bool vu = is_u && k < N;
-                const bool vx = is_x && k >= 1;
-                const bool valid = vu || vx;
-                float du_all[NU];
-#pragma unroll
-                for (int qq = 0; qq < NU; qq++) du_all[qq] = 0.0f;
-                if (k < N) {
-                    float w[NU];
-                    sfor<0, NU>([&](auto qc) {
-                        constexpr int qq = decltype(qc)::value;
-                        w[qq] = bc<qq>(rc[R::LR]) + ((k > 0) ? row_sum16(is_x ? rc[R::LM + qq] * dxs : 0.0f) : 0.0f);
-                    });
-                    sfor<0, NU>([&](auto qqc) {
-                        constexpr int qq = NU - 1 - decltype(qqc)::value;
-                        float sq = w[qq];
-                        sfor<qq + 1, NU>([&](auto jc) {
-                            constexpr int j = decltype(jc)::value;
-                            sq -= bc<j>(rc[R::LM + qq]) * du_all[j];
+                    // lam sensitivities: column c of Y = G' Phi_{k+1}, Z = L^-1 Y_u (uniform over the row), and
+                    // Phi_k = Y_x - LM Z; the value's lam terms Gam -= Z'Z, t -= Z' LR
+                    float zc[NU][NX];
+                    sfor<0, NX>([&](auto cc) {
+                        constexpr int c = decltype(cc)::value;
+                        float yc = dot_x<NX, NU>(0.0f, Phi[c], Gc);
+                        sfor<0, NU>([&](auto jc) {
+                            constexpr int j2 = decltype(jc)::value;
+                            const float z = bc<j2>(yc * rLm[j2]);
+                            zc[j2][c] = z;
+                            yc -= Lm[j2] * z;
                         });
-                        du_all[qq] = sq * frcp(bc<qq>(rc[R::LM + qq]));
+                        Phi[c] = is_x ? yc : 0.0f;
                     });
+                    float zi[NU], zr[NX];
 #pragma unroll
-                    for (int qq = 0; qq < NU; qq++) du_all[qq] = -du_all[qq];
+                    for (int j2 = 0; j2 < NU; j2++) {
+                        float s = 0.0f;
+#pragma unroll
+                        for (int c = 0; c < NX; c++) s = (xi == c) ? zc[j2][c] : s;
+                        zi[j2] = s;
+                    }
+#pragma unroll
+                    for (int c = 0; c < NX; c++) {
+                        float g = Gam[c];
+#pragma unroll
+                        for (int j2 = 0; j2 < NU; j2++) g -= zi[j2] * zc[j2][c];
+                        Gam[c] = g;
+                        float s = zc[0][c];
+#pragma unroll
+                        for (int j2 = 1; j2 < NU; j2++) s = (r == j2) ? zc[j2][c] : s;
+                        zr[c] = s;  // input lane j: row j of Z
+                    }
+#pragma unroll
+                    for (int j2 = 0; j2 < NU; j2++) tt -= zi[j2] * lrv[j2];
+                    if (srow && is_u) {
+                        float* const zp = seg_lds + SegL.ZL + ((size_t)k * NU + r) * SegLayout<M>::NXP;
+#pragma unroll
+                        for (int c = 0; c < NX; c++) zp[c] = zr[c];
+                    }
+#pragma unroll
+                    for (int jj = 0; jj < NV; jj++) Lrow[jj] = Lr[jj];
+                    rec_store_range<R::LR, R::LM + NU, RS, QM>(
+                        lv ? (srow ? tbase + (size_t)k * KS : wblk + r * rec_lane<RS, QM>()) : tdummy, rc);
+                };
+                auto load = [&](int j, float (&v)[RS]) { ld_range<R::GV, R::GH + 1, RS, QM>(tbase + (size_t)kof(j) * KS, v); };
+                float ra[RS], rb[RS];
+                load(0, ra);
+                for (int j = 0;; j += 2) {
+                    load(j + 1 <= Ls ? j + 1 : Ls, rb);
+                    bseg(j, ra);
+                    if (j == Ls) break;
+                    load(j + 2 <= Ls ? j + 2 : Ls, ra);
+                    bseg(j + 1, rb);
+                    if (j + 1 == Ls) break;
                 }
-                float dz = 0.0f;
+                // the segment's entry quantities for the master (state lanes: row xi)
+                if (srow && is_x) {
+                    double* const sp = reinterpret_cast<double*>(seg_lds + SegL.SUM_P) + ((size_t)q * NX + xi) * NX;
 #pragma unroll
-                for (int qq = 0; qq < NU; qq++)
-                    if (r == qq) dz = du_all[qq];
-                dz = is_x ? ((k >= 1) ? dxs : 0.0f) : dz;
-                dz = valid ? dz : 0.0f;
-                *(w0 ? dzbase + (size_t)k * 16 : wdz) = dz;  // every slot its own entry (idle slots: 0)
-                if (k < N) dxs = dyn(rc, dz);
-            });
+                    for (int l = 0; l < NX; l++) sp[l] = Lrow[NU + l];
+                    seg_lds[SegL.SUM_PB + q * NX + xi] = pv;
+                    seg_lds[SegL.SUM_T + q * NX + xi] = tt;
+#pragma unroll
+                    for (int c = 0; c < NX; c++) {
+                        seg_lds[SegL.SUM_PHI + (q * NX + xi) * NX + c] = Phi[c];
+                        seg_lds[SegL.SUM_GAM + (q * NX + xi) * NX + c] = Gam[c];
+                    }
+                }
+            }
+            {
+                float v[6] = {wave_max_rows(row_max16(fail ? 1.0f : 0.0f)), wave_max_rows(row_max16(nanb)), 0.0f,
+                              0.0f, 0.0f, 0.0f};
+                const int op[6] = {1, 1, 0, 0, 0, 0};
+                block_combine(v, op, 2);  // (also the barrier: every segment's summary and LR / LM are stored)
+                if (v[1] > 0.0f || v[0] > 0.0f) {
+                    status = (v[1] > 0.0f) ? 1 : ((mu <= kBreakdownMuT && res_ineq <= P.tol_ineq * 10.0f) ? 0 : 4);
+                    float cm;
+                    adjoint(res_stat, cm);
+                    exit_res[0] = res_stat;
+                    it_done = it;
+                    break;
+                }
+            }
+            RP_STAMP(4 + 4 * it);
+
+            // ---- master (row 0 of wave 0, fp64): the two-point recursion over the segment boundaries,
+            //   s_{i+1} = Phi_i' s_i + Gam_i lam_{i+1} + t_i,   lam_i = P_i s_i + pbar_i + Phi_i lam_{i+1},
+            // backward lam_i = Phat_i s_i + phat_i with Q_i = Phat_{i+1} X_i^-1, X_i = I - Gam_i Phat_{i+1} (I + PSD x
+            // PSD: eigenvalues >= 1; Gauss-Jordan with partial pivoting on X_i'), forward from s_0 = 0. Lane r < NX
+            // holds row r of the matrices; vectors are held whole by every lane; segment data come from LDS
+            if (tid < 16 && Sg > 1) {
+                const int rr = r < NX ? r : 0;
+                double* const qt = reinterpret_cast<double*>(seg_lds + SegL.QT);
+                double* const tv = reinterpret_cast<double*>(seg_lds + SegL.TV);
+                double Ph[NX], ph[NX];
+                {
+                    const double* sp = reinterpret_cast<const double*>(seg_lds + SegL.SUM_P) + ((size_t)(Sg - 1) * NX + rr) * NX;
+#pragma unroll
+                    for (int c = 0; c < NX; c++) {
+                        Ph[c] = sp[c];
+                        ph[c] = (double)seg_lds[SegL.SUM_PB + (Sg - 1) * NX + c];
+                    }
+                }
+                for (int i = Sg - 2; i >= 0; i--) {
+                    const float* const Gi = seg_lds + SegL.SUM_GAM + i * NX * NX;
+                    const float* const Fi = seg_lds + SegL.SUM_PHI + i * NX * NX;
+                    const float* const ti = seg_lds + SegL.SUM_T + i * NX;
+                    // row rr of X' = I - Phat Gam, and of the rhs Phat
+                    double A[NX], Rw[NX];
+#pragma unroll
+                    for (int c = 0; c < NX; c++) {
+                        A[c] = (rr == c) ? 1.0 : 0.0;
+                        Rw[c] = Ph[c];
+                    }
+#pragma unroll
+                    for (int l = 0; l < NX; l++)
+#pragma unroll
+                        for (int c = 0; c < NX; c++) A[c] -= Ph[l] * (double)Gi[l * NX + c];
+                    int pst = -1;
+                    sfor<0, NX>([&](auto jc) {
+                        constexpr int j = decltype(jc)::value;
+                        const bool cand_ok = r < NX && pst < 0;
+                        const float cand = cand_ok ? (float)fabs(A[j]) : -1.0f;
+                        const float m = row_max16(cand);
+                        const unsigned long long bal = __ballot(cand_ok && cand == m);
+                        const int p = (int)__builtin_ctzll(bal | (1ull << 15));
+                        double Ap[NX], Rp[NX];
+#pragma unroll
+                        for (int c = 0; c < NX; c++) {
+                            Ap[c] = readlane_d(A[c], p);
+                            Rp[c] = readlane_d(Rw[c], p);
+                        }
+                        const double inv = 1.0 / Ap[j];
+                        const bool me = r == p;
+                        const double f = A[j] * inv;
+#pragma unroll
+                        for (int c = 0; c < NX; c++) {
+                            A[c] = me ? A[c] * inv : A[c] - f * Ap[c];
+                            Rw[c] = me ? Rw[c] * inv : Rw[c] - f * Rp[c];
+                        }
+                        if (me) pst = j;
+                    });
+                    // the lane that pivoted at step j holds row j of Q_i
+                    if (r < NX) {
+#pragma unroll
+                        for (int c = 0; c < NX; c++) qt[pst * NX + c] = Rw[c];
+                    }
+                    lds_fence();
+                    double Qr[NX];
+                    double* const Qi = reinterpret_cast<double*>(seg_lds + SegL.QS) + (size_t)i * NX * NX;
+#pragma unroll
+                    for (int c = 0; c < NX; c++) Qr[c] = qt[rr * NX + c];
+                    if (r < NX) {
+#pragma unroll
+                        for (int c = 0; c < NX; c++) Qi[rr * NX + c] = Qr[c];
+                    }
+                    // c_i = t_i + Gam_i phat_{i+1}
+                    double cv[NX];
+#pragma unroll
+                    for (int c = 0; c < NX; c++) {
+                        double s = (double)ti[c];
+#pragma unroll
+                        for (int l = 0; l < NX; l++) s += (double)Gi[c * NX + l] * ph[l];
+                        cv[c] = s;
+                    }
+                    if (r == 0) {
+                        double* const ci = reinterpret_cast<double*>(seg_lds + SegL.CS) + (size_t)i * NX;
+                        double* const phi = reinterpret_cast<double*>(seg_lds + SegL.PHS) + (size_t)i * NX;
+#pragma unroll
+                        for (int c = 0; c < NX; c++) {
+                            ci[c] = cv[c];
+                            phi[c] = ph[c];
+                        }
+                    }
+                    if (i >= 1) {
+                        // Phat_i = P_i + Phi_i Q_i Phi_i',  phat_i = pbar_i + Phi_i (Q_i c_i + phat_{i+1})
+                        double T[NX];
+#pragma unroll
+                        for (int j = 0; j < NX; j++) {
+                            double s = 0.0;
+#pragma unroll
+                            for (int m = 0; m < NX; m++) s += Qr[m] * (double)Fi[j * NX + m];
+                            T[j] = s;
+                        }
+                        double w = ph[0];
+#pragma unroll
+                        for (int c = 1; c < NX; c++) w = (rr == c) ? ph[c] : w;
+#pragma unroll
+                        for (int m = 0; m < NX; m++) w += Qr[m] * cv[m];
+                        lds_fence();  // (every lane has read its Q row before qt is reused)
+                        if (r < NX) {
+#pragma unroll
+                            for (int j = 0; j < NX; j++) qt[rr * NX + j] = T[j];
+                            tv[rr] = w;
+                        }
+                        lds_fence();
+                        const double* const Pi = reinterpret_cast<const double*>(seg_lds + SegL.SUM_P) + ((size_t)i * NX + rr) * NX;
+#pragma unroll
+                        for (int j = 0; j < NX; j++) Ph[j] = Pi[j];
+#pragma unroll
+                        for (int l = 0; l < NX; l++) {
+                            const double fl = (double)Fi[rr * NX + l];
+#pragma unroll
+                            for (int j = 0; j < NX; j++) Ph[j] += fl * qt[l * NX + j];
+                        }
+                        double wv[NX];
+#pragma unroll
+                        for (int l = 0; l < NX; l++) wv[l] = tv[l];
+#pragma unroll
+                        for (int c = 0; c < NX; c++) {
+                            double s = (double)seg_lds[SegL.SUM_PB + i * NX + c];
+#pragma unroll
+                            for (int l = 0; l < NX; l++) s += (double)Fi[c * NX + l] * wv[l];
+                            ph[c] = s;
+                        }
+                        lds_fence();  // (qt / tv reads done before the next step rewrites them)
+                    }
+                }
+                // forward: s_0 = 0; lam_{i+1} = Q_i (Phi_i' s_i + c_i) + phat_{i+1}; s_{i+1} = Phi_i' s_i + Gam_i lam_{i+1} + t_i
+                double s[NX];
+#pragma unroll
+                for (int c = 0; c < NX; c++) s[c] = 0.0;
+                float* const sl = seg_lds + SegL.SL;
+                for (int i = 0; i <= Sg - 2; i++) {
+                    const float* const Gi = seg_lds + SegL.SUM_GAM + i * NX * NX;
+                    const float* const Fi = seg_lds + SegL.SUM_PHI + i * NX * NX;
+                    const float* const ti = seg_lds + SegL.SUM_T + i * NX;
+                    const double* const Qi = reinterpret_cast<const double*>(seg_lds + SegL.QS) + (size_t)i * NX * NX;
+                    const double* const ci = reinterpret_cast<const double*>(seg_lds + SegL.CS) + (size_t)i * NX;
+                    const double* const phi = reinterpret_cast<const double*>(seg_lds + SegL.PHS) + (size_t)i * NX;
+                    double v[NX], fs[NX];
+#pragma unroll
+                    for (int c = 0; c < NX; c++) {
+                        double acc = 0.0;
+#pragma unroll
+                        for (int l = 0; l < NX; l++) acc += (double)Fi[l * NX + c] * s[l];
+                        fs[c] = acc;
+                        v[c] = acc + ci[c];
+                    }
+                    double lrr = phi[rr];
+#pragma unroll
+                    for (int m = 0; m < NX; m++) lrr += Qi[rr * NX + m] * v[m];
+                    if (r < NX) tv[rr] = lrr;
+                    lds_fence();
+                    double lam[NX];
+#pragma unroll
+                    for (int c = 0; c < NX; c++) lam[c] = tv[c];
+#pragma unroll
+                    for (int c = 0; c < NX; c++) {
+                        double acc = fs[c] + (double)ti[c];
+#pragma unroll
+                        for (int l = 0; l < NX; l++) acc += (double)Gi[c * NX + l] * lam[l];
+                        s[c] = acc;
+                    }
+                    if (r < NX) {
+                        sl[(i + 1) * 2 * NX + r] = (float)s[rr];
+                        sl[(i + 1) * 2 * NX + NX + r] = (float)lam[rr];
+                    }
+                    lds_fence();  // (tv read by every lane before the next boundary rewrites it)
+                }
+            }
+            __syncthreads();  // the boundary states and costates
+            RP_STAMP(5 + 4 * it);
+
+            // ---- phase C (segments in parallel, 0 -> N): row q starts at x_{qL} = s_q and takes the stored
+            // factor with LR + Z lam_{q+1}; rows other than the last stop before the next segment's first stage
+            sigma_mu = tg_rhs;
+            if (4 * wave < Sg) {
+                const float* const sl = seg_lds + SegL.SL;
+                float lam[NX];
+                float dxs = 0.0f;
+#pragma unroll
+                for (int c = 0; c < NX; c++) {
+                    lam[c] = (srow && !slast) ? sl[(q + 1) * 2 * NX + NX + c] : 0.0f;
+                    const float s0 = (srow && q > 0) ? sl[q * 2 * NX + c] : 0.0f;
+                    dxs = (is_x && xi == c) ? s0 : dxs;
+                }
+                auto kof = [&](int j) { return srow ? q * Ls + j : N; };
+                auto cseg = [&](int j, float (&rc)[RS]) {
+                    const int k = kof(j);
+                    const bool live = srow && (j < Ls || slast);
+                    const bool vu = is_u && k < N;
+                    const bool vx = is_x && k >= 1;
+                    const bool valid = live && (vu || vx);
+                    float du_all[NU];
+#pragma unroll
+                    for (int qq = 0; qq < NU; qq++) du_all[qq] = 0.0f;
+                    if (k < N) {
+                        // LR of the segment's end costate (input lane j: row j of Z_k . lam)
+                        const float* const zp = seg_lds + SegL.ZL + ((size_t)k * NU + (is_u ? r : 0)) * SegLayout<M>::NXP;
+                        float lr = rc[R::LR];
+#pragma unroll
+                        for (int c = 0; c < NX; c++) lr += zp[c] * lam[c];
+                        rc[R::LR] = is_u ? lr : rc[R::LR];
+                        float w[NU];
+                        sfor<0, NU>([&](auto qc) {
+                            constexpr int qq = decltype(qc)::value;
+                            w[qq] = bc<qq>(rc[R::LR]) + row_sum16(is_x ? rc[R::LM + qq] * dxs : 0.0f);
+                        });
+                        sfor<0, NU>([&](auto qqc) {
+                            constexpr int qq = NU - 1 - decltype(qqc)::value;
+                            float sq = w[qq];
+                            sfor<qq + 1, NU>([&](auto jc) {
+                                constexpr int j2 = decltype(jc)::value;
+                                sq -= bc<j2>(rc[R::LM + qq]) * du_all[j2];
+                            });
+                            du_all[qq] = sq * frcp(bc<qq>(rc[R::LM + qq]));
+                        });
+#pragma unroll
+                        for (int qq = 0; qq < NU; qq++) du_all[qq] = -du_all[qq];
+                    }
+                    float dz = 0.0f;
+#pragma unroll
+                    for (int qq = 0; qq < NU; qq++)
+                        if (r == qq) dz = du_all[qq];
+                    dz = is_x ? ((k >= 1) ? dxs : 0.0f) : dz;
+                    dz = valid ? dz : 0.0f;
+                    *(live ? dzbase + (size_t)k * 16 : wdz) = dz;
+                    if (k < N) dxs = dyn(rc, dz);
+                };
+                auto load = [&](int j, float (&v)[RS]) { ld_range<0, R::GV + NGV, RS, QM>(tbase + (size_t)kof(j) * KS, v); };
+                float ra[RS], rb[RS];
+                load(0, ra);
+                for (int j = 0;; j += 2) {
+                    load(j + 1 <= Ls ? j + 1 : Ls, rb);
+                    cseg(j, ra);
+                    if (j == Ls) break;
+                    load(j + 2 <= Ls ? j + 2 : Ls, ra);
+                    cseg(j + 1, rb);
+                    if (j + 1 == Ls) break;
+                }
+            }
+            __syncthreads();  // the directions of every stage
+        } else {
+            // phase B (serial, N -> 0): adjoint, fp64 classic Riccati step, rhs / forward substitution
+            double Lrow[NV];
+    #pragma unroll
+            for (int j = 0; j < NV; j++) Lrow[j] = 0.0;
+            float pv = 0.0f, piv = 0.0f, res_stat = 0.0f, cpi_max = 0.0f;
+            bool fail = false;
+            if (!(nanf_ > 0.0f || mu != mu)) {
+                serial(std::integral_constant<int, R::GV>{}, std::integral_constant<int, R::GH + 1>{},
+                       std::false_type{}, N, 0, -1, [&](int k, float (&rc)[RS]) {
+                    const bool vu = is_u && k < N;
+                    const bool vx = is_x && k >= 1;
+                    const bool valid = vu || vx;
+                    float Gc[NX];
+                    column(rc, Gc);
+                    const float cpi = (k < N) ? dot_x<NX, NU>(0.0f, piv, Gc) : 0.0f;
+                    const float base = rc[R::C0] + cpi;
+                    res_stat = fmaxf(res_stat, vu ? fabsf(base) : 0.0f);
+                    cpi_max = fmaxf(cpi_max, vu ? fabsf(cpi) : 0.0f);
+                    const float sig = rc[R::SIG];
+                    const float ghat = valid ? (vu ? rc[R::GH] + base : rc[R::GH]) : 0.0f;
+                    const float pi_new = vx ? base : 0.0f;
+                    if (ghat != ghat) nanf_ = 1.0f;
+                    if (k == N) {
+                        const double d = is_x ? (double)fmaxf(we_lane + sig, 0.0f) : 0.0;
+    #pragma unroll
+                        for (int j = 0; j < NV; j++) Lrow[j] = (is_x && j == r) ? d : 0.0;
+                        pv = is_x ? ghat : 0.0f;
+                    } else {
+                        double Gd[NX];
+    #pragma unroll
+                        for (int l = 0; l < NX; l++) Gd[l] = (l < NGV) ? (double)Gc[l] : gcol64[l];
+                        double pg[NX];
+    #pragma unroll
+                        for (int i = 0; i < NX; i++) pg[i] = 0.0;
+                        pg_block<NX, NU>(pg, Lrow, Gd);
+                        const double dg = valid ? (double)h_stage + (double)sig : 1.0;
+                        double Lr[NV];
+    #pragma unroll
+                        for (int j = 0; j < NV; j++) Lr[j] = onehot[j] * dg;
+                        double pivot;
+                        mrow_pg_block<NX, NU>(Lr, pivot, pg, Gd);
+                        sfor<0, NU>([&](auto jc) {
+                            constexpr int j = decltype(jc)::value;
+                            if (!(pivot > 0.0)) fail = true;
+                            const double rd = drsq(fmax(pivot, 1e-300));
+                            const double lj = (r >= j) ? Lr[j] * rd : 0.0;
+                            Lr[j] = lj;
+                            chol_update<NX, NU, j>(Lr, lj, pivot);
+                        });
+                        float Lm[NU];
+    #pragma unroll
+                        for (int qq = 0; qq < NU; qq++) {
+                            Lm[qq] = (float)Lr[qq];
+                            rc[R::LM + qq] = Lm[qq];
+                        }
+                        float y = dot_x<NX, NU>(ghat, pv, Gc);
+                        float my_lr = 0.0f;
+                        sfor<0, NU>([&](auto jc) {
+                            constexpr int j = decltype(jc)::value;
+                            const float lrj = bc<j>(y * frcp(Lm[j]));
+                            if (r == j) my_lr = lrj;
+                            y -= Lm[j] * lrj;
+                        });
+                        rc[R::LR] = my_lr;
+                        pv = is_x ? y : 0.0f;
+    #pragma unroll
+                        for (int j = 0; j < NV; j++) Lrow[j] = Lr[j];
+                        // LR, LM (every row stores the same values; idle slots store into the dummy record)
+                        rec_store_range<R::LR, R::LM + NU, RS, QM>(
+                            lv ? (w0 ? tbase + (size_t)k * KS : wblk + r * rec_lane<RS, QM>()) : tdummy, rc);
+                    }
+                    piv = pi_new;
+                });
+            }
+            RP_STAMP(4 + 4 * it);
+            res_stat = row_max16(lv ? res_stat : 0.0f);
+            const float stat_scale = fmaxf(sc0, row_max16(lv ? cpi_max : 0.0f));
+            nanf_ = row_max16(nanf_);
+            const float failf = row_max16(fail ? 1.0f : 0.0f);
+            // stopping rule of k_sqp_rti_team (DESIGN.md "Stopping rule")
+            exit_res[0] = res_stat;
+            exit_res[1] = res_ineq;
+            exit_res[2] = mu;
+            bool stop = false;
+            if (nanf_ > 0.0f || mu != mu) {
+                status = 1;
+                stop = true;
+            } else if (failf > 0.0f) {
+                status = (mu <= kBreakdownMuT && res_ineq <= P.tol_ineq * 10.0f) ? 0 : 4;
+                stop = true;
+            } else if (lam_max > lam_thr && res_ineq > kInfeasRes) {
+                status = 4;
+                stop = true;
+            } else {
+                const bool stat_ok = res_stat <= P.tol_stat || res_stat <= kStatRelT * stat_scale;
+                const bool cmax_ok = max_c <= kCompMaxRatio * P.tol_comp;
+                const bool stalled = mu <= P.tol_comp && mu > 0.5f * mu_prev;
+                if (res_ineq <= P.tol_ineq &&
+                    ((stat_ok && mu <= P.tol_comp && cmax_ok) || mu <= 1e-2f * P.tol_comp || (stalled && cmax_ok)))
+                    stop = true;
+                if (it >= P.iter_max) stop = true;
+            }
+            mu_prev = mu;
+            if (stop) {
+                it_done = it;
+                break;
+            }
+            __syncthreads();  // LR / LM of every stage
+
+            // phase C (serial, 0 -> N): the direction's input part from the stored factor, its state part from the
+            // dynamics; every row the same (identical DZ stores)
+            sigma_mu = tg_rhs;
+            {
+                float dxs = 0.0f;
+                serial(std::integral_constant<int, 0>{}, std::integral_constant<int, R::GV + NGV>{}, std::false_type{},
+                       0, N, 1, [&](int k, float (&rc)[RS]) {
+                    const bool vu = is_u && k < N;
+                    const bool vx = is_x && k >= 1;
+                    const bool valid = vu || vx;
+                    float du_all[NU];
+    #pragma unroll
+                    for (int qq = 0; qq < NU; qq++) du_all[qq] = 0.0f;
+                    if (k < N) {
+                        float w[NU];
+                        sfor<0, NU>([&](auto qc) {
+                            constexpr int qq = decltype(qc)::value;
+                            w[qq] = bc<qq>(rc[R::LR]) + ((k > 0) ? row_sum16(is_x ? rc[R::LM + qq] * dxs : 0.0f) : 0.0f);
+                        });
+                        sfor<0, NU>([&](auto qqc) {
+                            constexpr int qq = NU - 1 - decltype(qqc)::value;
+                            float sq = w[qq];
+                            sfor<qq + 1, NU>([&](auto jc) {
+                                constexpr int j = decltype(jc)::value;
+                                sq -= bc<j>(rc[R::LM + qq]) * du_all[j];
+                            });
+                            du_all[qq] = sq * frcp(bc<qq>(rc[R::LM + qq]));
+                        });
+    #pragma unroll
+                        for (int qq = 0; qq < NU; qq++) du_all[qq] = -du_all[qq];
+                    }
+                    float dz = 0.0f;
+    #pragma unroll
+                    for (int qq = 0; qq < NU; qq++)
+                        if (r == qq) dz = du_all[qq];
+                    dz = is_x ? ((k >= 1) ? dxs : 0.0f) : dz;
+                    dz = valid ? dz : 0.0f;
+                    *(w0 ? dzbase + (size_t)k * 16 : wdz) = dz;  // every slot its own entry (idle slots: 0)
+                    if (k < N) dxs = dyn(rc, dz);
+                });
+            }
+            __syncthreads();  // the directions of every stage
+            RP_STAMP(5 + 4 * it);
         }
-        __syncthreads();  // the directions of every stage
-        RP_STAMP(5 + 4 * it);
 
         // phase D (stage-parallel): bound directions, fraction-to-boundary step bound, complementarity polynomial
         float amax = 1e30f, s1 = 0.0f, s2 = 0.0f;
@@ -784,28 +1317,34 @@ __global__ __launch_bounds__(64 * W, 1) void k_sqp_rti_rowpar(KParams P, KArgs a
 }  // namespace
 
 template <class M>
-size_t rowpar_lds_bytes(int N, int mode)
+size_t rowpar_lds_bytes(int N, int mode, int seg)
 {
-    // stage inputs, reference poses, [4][8] reductions, dx [N+1][16] and unwrapped references [N+1][3] (P0b)
-    return ((size_t)(N + 1) * (16 * (5 + M::NGV) + 3 + 16 + 3) + 32) * sizeof(float);
+    (void)mode;
+    return RowLds<M>::floats(N, seg) * sizeof(float);
 }
 
 template <class M>
 hipError_t launch_sqp_rti_rowpar(const KParams& P, const KArgs& a, int mode, hipStream_t stream)
 {
     if (a.B <= 0) return hipSuccess;
-    const size_t lds = rowpar_lds_bytes<M>(P.N, mode);
+    const size_t lds = rowpar_lds_bytes<M>(P.N, mode, a.seg);
     if (lds > 65536 || P.ipm != 1 || a.segs) return hipErrorInvalidValue;
+    // segments: N % S == 0, at most kSegMax and at most one per row of the block
+    if (a.seg < 0 || a.seg > kSegMax || a.seg > 4 * (a.rowpar >= 4 ? 4 : 1) || (a.seg > 0 && P.N % a.seg != 0))
+        return hipErrorInvalidValue;
     if (a.rowpar >= 4)  // four waves per robot (one per SIMD of its CU)
-        hipLaunchKernelGGL((k_sqp_rti_rowpar<M, 4>), dim3(a.B), dim3(256), lds, stream, P, a, mode);
+        if (a.seg > 0) hipLaunchKernelGGL((k_sqp_rti_rowpar<M, 4, true>), dim3(a.B), dim3(256), lds, stream, P, a, mode);
+        else hipLaunchKernelGGL((k_sqp_rti_rowpar<M, 4, false>), dim3(a.B), dim3(256), lds, stream, P, a, mode);
+    else if (a.seg > 0)
+        hipLaunchKernelGGL((k_sqp_rti_rowpar<M, 1, true>), dim3(a.B), dim3(64), lds, stream, P, a, mode);
     else
-        hipLaunchKernelGGL((k_sqp_rti_rowpar<M, 1>), dim3(a.B), dim3(64), lds, stream, P, a, mode);
+        hipLaunchKernelGGL((k_sqp_rti_rowpar<M, 1, false>), dim3(a.B), dim3(64), lds, stream, P, a, mode);
     return hipGetLastError();
 }
 
 #define INST(M)                                                                                                      \
     template hipError_t launch_sqp_rti_rowpar<M>(const KParams&, const KArgs&, int, hipStream_t);                   \
-    template size_t rowpar_lds_bytes<M>(int, int);
+    template size_t rowpar_lds_bytes<M>(int, int, int);
 INST(Diff2)
 INST(Omni4)
 INST(Tric3)
