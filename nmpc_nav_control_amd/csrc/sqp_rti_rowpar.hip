@@ -504,6 +504,29 @@ __global__ __launch_bounds__(64 * W, 1) void k_sqp_rti_rowpar(KParams P, KArgs a
         }
     };
 
+    // stage-parallel rounds j = 0 .. NR-1 (row q: stage j ROWS + q, clamped to N) with the next round's record fields
+    // [F0, F1) and DZ in flight while body(j, fields, dz) runs (loads never predicated; past the last round the
+    // last one is re-read)
+    auto spar = [&](auto f0c, auto f1c, auto&& body) {
+        constexpr int F0 = decltype(f0c)::value, F1 = decltype(f1c)::value;
+        auto load = [&](int j, float (&v)[RS], float& dzv) {
+            const int kr = j * ROWS + q;
+            const int k = kr <= N ? kr : N;
+            ld_range<F0, F1, RS, QM>(tbase + (size_t)k * KS, v);
+            dzv = dzbase[(size_t)k * 16];
+        };
+        float ra[RS], rb[RS], da, db;
+        load(0, ra, da);
+        for (int j = 0;; j += 2) {
+            load(j + 1 < NR ? j + 1 : NR - 1, rb, db);
+            body(j, ra, da);
+            if (j + 1 >= NR) break;
+            load(j + 2 < NR ? j + 2 : NR - 1, ra, da);
+            body(j + 1, rb, db);
+            if (j + 2 >= NR) break;
+        }
+    };
+
     // SEG: the segment area of the LDS (RowLds / SegLayout), and the serial adjoint pass of the stopping rule:
     // pi_k = c0_x + A_k' pi_{k+1} on the state slots, the input stationarity residual c0_u + B_k' pi_{k+1}
     const SegLayout<M> SegL(SEG ? a.seg : 1);
@@ -535,13 +558,11 @@ __global__ __launch_bounds__(64 * W, 1) void k_sqp_rti_rowpar(KParams P, KArgs a
         // phase A (stage-parallel): apply the previous step, residuals, barrier weight, rhs terms
         const float a_upd = (it > 0) ? alpha : 0.0f;
         float res_ineq = 0.0f, sum_c = 0.0f, max_c = 0.0f, lam_max = 0.0f, sc0 = 1.0f, nanf_ = 0.0f;
-        for (int j = 0; j < NR; j++) {
+        spar(std::integral_constant<int, R::Z>{}, std::integral_constant<int, R::GR + 1>{},
+             [&](int j, float (&rc)[RS], float dz) {
             const int kr = j * ROWS + q;
             const bool kv = kr <= N;       // rows past the last stage redo stage N into the dummy record
             const int k = kv ? kr : N;
-            float rc[RS];
-            ld_range<R::Z, R::GR + 1, RS, QM>(tbase + (size_t)k * KS, rc);
-            const float dz = dzbase[(size_t)k * 16];
             const bool vu = is_u && k < N && kv;
             const bool vx = is_x && k >= 1 && kv;
             const bool valid = vu || vx;
@@ -585,7 +606,7 @@ __global__ __launch_bounds__(64 * W, 1) void k_sqp_rti_rowpar(KParams P, KArgs a
             float* const pk = (lv && kv) ? tbase + (size_t)k * KS : tdummy;
             rec_store_range<R::Z, R::LU + 1, RS, QM>(pk, rc);
             rec_store_range<R::SIG, R::GH + 1, RS, QM>(pk, rc);
-        }
+        });
         {
             float v[6] = {wave_sum_rows(row_sum16(lv ? sum_c : 0.0f)), wave_max_rows(row_max16(lv ? max_c : 0.0f)),
                           wave_max_rows(row_max16(lv ? lam_max : 0.0f)), wave_max_rows(row_max16(lv ? res_ineq : 0.0f)),
@@ -1204,13 +1225,11 @@ __global__ __launch_bounds__(64 * W, 1) void k_sqp_rti_rowpar(KParams P, KArgs a
 
         // phase D (stage-parallel): bound directions, fraction-to-boundary step bound, complementarity polynomial
         float amax = 1e30f, s1 = 0.0f, s2 = 0.0f;
-        for (int j = 0; j < NR; j++) {
+        spar(std::integral_constant<int, R::Z>{}, std::integral_constant<int, R::UB + 1>{},
+             [&](int j, float (&rc)[RS], float dz) {
             const int kr = j * ROWS + q;
             const bool kv = kr <= N;
             const int k = kv ? kr : N;
-            float rc[RS];
-            ld_range<R::Z, R::UB + 1, RS, QM>(tbase + (size_t)k * KS, rc);
-            const float dz = dzbase[(size_t)k * 16];
             const bool valid = kv && ((is_u && k < N) || (is_x && k >= 1));
             const bool bnd = valid && has_b;
             const float z = rc[R::Z];
@@ -1226,7 +1245,7 @@ __global__ __launch_bounds__(64 * W, 1) void k_sqp_rti_rowpar(KParams P, KArgs a
             }
             s1 += bnd ? ll * d.dtl + tl * d.dll + lu * d.dtu + tu * d.dlu : 0.0f;
             s2 += bnd ? d.dll * d.dtl + d.dlu * d.dtu : 0.0f;
-        }
+        });
         {
             float v[6] = {wave_min_rows(row_min16(lv ? amax : 1e30f)), wave_sum_rows(row_sum16(lv ? s1 : 0.0f)),
                           wave_sum_rows(row_sum16(lv ? s2 : 0.0f)), 0.0f, 0.0f, 0.0f};
