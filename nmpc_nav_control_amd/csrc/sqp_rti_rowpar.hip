@@ -72,7 +72,9 @@ struct SegLayout {
 template <class M>
 struct RowLds {
     static constexpr int SF = 5 + M::NGV;
-    __host__ __device__ static constexpr size_t base_floats(int N) { return (size_t)(N + 1) * (16 * SF + 3 + 16 + 3) + 32; }
+    // ... followed by 64 pad floats (per-lane store targets nobody reads)
+    __host__ __device__ static constexpr size_t pad_off(int N) { return (size_t)(N + 1) * (16 * SF + 3 + 16 + 3) + 32; }
+    __host__ __device__ static constexpr size_t base_floats(int N) { return pad_off(N) + 64; }
     __host__ __device__ static size_t seg_off(int N, int S)
     {
         return SegLayout<M>(S).floats(N) <= (size_t)(N + 1) * SF * 16 ? 0 : (base_floats(N) + 3) / 4 * 4;
@@ -109,6 +111,9 @@ __device__ __forceinline__ void ld_range(const float* p, float (&v)[RS])
 {
     rec_load_range<F0, F1, RS, QM>(p, v);
 }
+
+// zeros: the warm-start multiplier source of a cold robot (the flag selects the address, not the value)
+__device__ float g_rp_zero4[4];
 
 // fp64 value of lane `lane` (wave-uniform) in every lane
 __device__ __forceinline__ double readlane_d(double v, int lane)
@@ -265,11 +270,18 @@ __global__ __launch_bounds__(64 * W, 1) void k_sqp_rti_rowpar(KParams P, KArgs a
     };
 
     const int len = (mode == kModeRun) ? (a.traj_len ? a.traj_len[inst] : N + 1) : 0;
+    // a per-lane LDS slot nobody reads: the target of P0's stores for lanes / rounds without data (a store under a
+    // lane mask leaves the compiler's later waits uncounted, i.e. full drains)
+    float* const lpad = s_row + RowLds<M>::pad_off(N) + (tid & 63);
     {
         struct In {
             float x[NX], u[NU], y, xnext, tq;
             float2 l;
         };
+        // every load unconditional at a valid address (values selected afterwards): a load under a lane mask or a
+        // runtime condition made the compiler drain the memory counter before the round's stores
+        const int jy = is_u ? NX + r : xi;
+        const bool use_y = lv && jy < a.ny_in;
         auto ld = [&](int k, In& v) {
             const int kk = k <= N ? k : N;
 #pragma unroll
@@ -278,26 +290,23 @@ __global__ __launch_bounds__(64 * W, 1) void k_sqp_rti_rowpar(KParams P, KArgs a
 #pragma unroll
             for (int j = 0; j < NU; j++) v.u[j] = UBAR(ku, j);
             v.xnext = XB(kk < N ? kk + 1 : N, xi);
-            v.y = 0.0f;
-            v.tq = 0.0f;
             if (mode != kModeRun) {
-                const int j = is_u ? NX + r : xi;
-                v.y = (lv && j < a.ny_in) ? a.yref[((size_t)kk * a.ny_in + j) * Bn + inst] : 0.0f;
-            } else if (r < 3) {
+                const float y = a.yref[((size_t)kk * a.ny_in + (use_y ? jy : 0)) * Bn + inst];
+                v.y = use_y ? y : 0.0f;
+                v.tq = 0.0f;
+            } else {
                 const int kt = kk < len ? kk : (len > 0 ? len - 1 : 0);
-                v.tq = a.traj[((size_t)kt * 3 + r) * Bn + inst];
+                v.tq = a.traj[((size_t)kt * 3 + (r < 3 ? r : 0)) * Bn + inst];
+                v.y = 0.0f;
             }
-            v.l = warm ? *reinterpret_cast<const float2*>(tbase + (size_t)kk * KS + rec_off<RS, QM>(R::LL))
-                       : make_float2(0.0f, 0.0f);
+            v.l = *reinterpret_cast<const float2*>(warm ? tbase + (size_t)kk * KS + rec_off<RS, QM>(R::LL) : g_rp_zero4);
         };
-        In cur, nxt;
-        ld(q, cur);
-        // wave-uniform trip count: rows past the last stage repeat stage N and write nothing
-        for (int j = 0; j < NR; j++) {
+        // rounds j = 0 .. NR-1 (row q: stage j ROWS + q) with the next round's inputs in flight (two buffers used in
+        // turn: a copy between them would wait for the load still in flight)
+        auto round = [&](int j, const In& cur) {
             const int k = j * ROWS + q;
-            ld(k + ROWS, nxt);
             const bool kv = k <= N;
-            if (mode == kModeRun && r < 3 && kv) my_traj[k * 3 + r] = cur.tq;
+            if (mode == kModeRun) *((r < 3 && kv) ? my_traj + k * 3 + r : lpad) = cur.tq;
             float xn[NX], g[NX];
 #pragma unroll
             for (int i = 0; i < NX; i++) { xn[i] = 0.0f; g[i] = 0.0f; }
@@ -310,22 +319,29 @@ __global__ __launch_bounds__(64 * W, 1) void k_sqp_rti_rowpar(KParams P, KArgs a
             }
             float zb = 0.0f;
 #pragma unroll
-            for (int j = 0; j < NU; j++)
-                if (r == j) zb = cur.u[j];
+            for (int j2 = 0; j2 < NU; j2++)
+                if (r == j2) zb = cur.u[j2];
 #pragma unroll
-            for (int j = 0; j < NX; j++)
-                if (is_x && xi == j) zb = cur.x[j];
-            if (kv) {
-                float* const st = s_stg + (size_t)k * SF * 16 + r;
-                st[0] = zb;
-                st[16] = cur.y;
-                st[32] = cur.l.x;
-                st[48] = cur.l.y;
-                st[64] = bk;
+            for (int j2 = 0; j2 < NX; j2++)
+                if (is_x && xi == j2) zb = cur.x[j2];
+            float* const st = kv ? s_stg + (size_t)k * SF * 16 + r : nullptr;
+            *(kv ? st : lpad) = zb;
+            *(kv ? st + 16 : lpad) = cur.y;
+            *(kv ? st + 32 : lpad) = cur.l.x;
+            *(kv ? st + 48 : lpad) = cur.l.y;
+            *(kv ? st + 64 : lpad) = bk;
 #pragma unroll
-                for (int i = 0; i < NGV; i++) st[(5 + i) * 16] = g[i];
-            }
-            cur = nxt;
+            for (int i = 0; i < NGV; i++) *(kv ? st + (5 + i) * 16 : lpad) = g[i];
+        };
+        In ca, cb;
+        ld(q, ca);
+        for (int j = 0;; j += 2) {
+            ld((j + 1) * ROWS + q, cb);
+            round(j, ca);
+            if (j + 1 >= NR) break;
+            ld((j + 2) * ROWS + q, ca);
+            round(j + 1, cb);
+            if (j + 2 >= NR) break;
         }
     }
     // constant rows of [B A] (rows >= NGV) from stage 0 (every row, identically)
@@ -373,23 +389,19 @@ __global__ __launch_bounds__(64 * W, 1) void k_sqp_rti_rowpar(KParams P, KArgs a
 #pragma unroll
             for (int j = 0; j < 3; j++) o.t[j] = (mode == kModeRun) ? my_traj[kk * 3 + j] : 0.0f;
         };
-        Stg cur, nxt;
-        lds_ld(0, cur);
-        for (int k = 0; k <= N; k++) {
-            lds_ld(k + 1, nxt);
+        // one stage of the recursion (branch-free reference unwrap; every LDS store unconditional: lanes without
+        // an entry write their pad slot, rows 1-3 of wave 0 write row 0's identical values)
+        auto step = [&](int k, const Stg& cur) {
             if (mode == kModeRun) {
-                if (k < len) {
-                    ref_x = cur.t[0];
-                    ref_y = cur.t[1];
-                    float th = cur.t[2];
-                    const float d = th - ref_t;
-                    if (d > kPi) th -= 2.0f * kPi;
-                    else if (d < -kPi) th += 2.0f * kPi;
-                    ref_t = th;
-                }
-                if (tid < 3) s_ref[k * 3 + tid] = (tid == 0) ? ref_x : ((tid == 1) ? ref_y : ref_t);
+                const bool in = k < len;
+                const float th = cur.t[2], d = th - ref_t;
+                const float thu = (d > kPi) ? th - 2.0f * kPi : ((d < -kPi) ? th + 2.0f * kPi : th);
+                ref_x = in ? cur.t[0] : ref_x;
+                ref_y = in ? cur.t[1] : ref_y;
+                ref_t = in ? thu : ref_t;
+                *(r < 3 ? s_ref + k * 3 + r : lpad) = (r == 0) ? ref_x : ((r == 1) ? ref_y : ref_t);
             }
-            if (tid < 16) s_dx[k * 16 + r] = dx;
+            s_dx[k * 16 + r] = dx;
             if (k < N) {
                 const float dzd = is_x ? dx : 0.0f;
                 float nx_ = dot_v<NX, NU>(0.0f, dzd, grow);
@@ -400,7 +412,16 @@ __global__ __launch_bounds__(64 * W, 1) void k_sqp_rti_rowpar(KParams P, KArgs a
                 }
                 dx = is_x ? nx_ + cur.b : 0.0f;
             }
-            cur = nxt;
+        };
+        Stg ca, cb;  // two buffers used in turn (no copies: a copy waits for the LDS read in flight)
+        lds_ld(0, ca);
+        for (int k = 0;; k += 2) {
+            lds_ld(k + 1, cb);
+            step(k, ca);
+            if (k == N) break;
+            lds_ld(k + 2, ca);
+            step(k + 1, cb);
+            if (k + 1 == N) break;
         }
     }
     __syncthreads();
