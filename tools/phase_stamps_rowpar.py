@@ -36,16 +36,21 @@ assert L.nmpc_debug_stamps_rowpar(buf) == 0
 st = np.frombuffer(buf, dtype=np.uint64).reshape(256, W).astype(np.int64)[:B]
 it = f.qp_iter.cpu().numpy()
 print("kernel ms", ev0.elapsed_time(ev1), "qp_iter", it.tolist())
-ph = {"A": [], "B": [], "C": [], "D": []}
+# serial kernel: A, B (Riccati), C (forward), D; segmented (NMPC_AMD_SEG > 0): A, B (segment sweeps), M (master),
+# C+D (segment forward + step); the segmented kernel decides to stop before its phase B
+seg = int(os.environ.get("NMPC_AMD_SEG", "0")) > 0
+names = ["A", "Bseg", "M", "CD"] if seg else ["A", "B", "C", "D"]
+ph = {n: [] for n in names}
 for b in range(B):
     for i in range(int(it[b]) + 1):
         base = 3 + 4 * i
         prev = st[b, 2] if i == 0 else st[b, base - 1]
-        ph["A"].append(st[b, base] - prev)
-        ph["B"].append(st[b, base + 1] - st[b, base])
+        ph[names[0]].append(st[b, base] - prev)
+        if not seg or i < it[b]:
+            ph[names[1]].append(st[b, base + 1] - st[b, base])
         if i < it[b]:
-            ph["C"].append(st[b, base + 2] - st[b, base + 1])
-            ph["D"].append(st[b, base + 3] - st[b, base + 2])
+            ph[names[2]].append(st[b, base + 2] - st[b, base + 1])
+            ph[names[3]].append(st[b, base + 3] - st[b, base + 2])
 print("P0a cycles", (st[:, 1] - st[:, 0]).tolist(), "P0b", (st[:, 2] - st[:, 1]).tolist())
 for k, v in ph.items():
     v = np.array(v)
