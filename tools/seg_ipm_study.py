@@ -1,0 +1,139 @@
+#!/usr/bin/env python3
+"""The segmented Riccati inside the device IPM, on real bench QPs (design check for k_sqp_rti_rowpar SEG).
+
+tools/seg_emu.py checks one Newton direction on synthetic QPs; this runs the whole single-direction IPM of the
+device (tools/ipm_emu.py, warm rule as dumped by tools/tick_dump.py) on the QPs of dumped stationary metric ticks
+twice: with the serial Riccati and with the segmented one in the kernel's precision (the factor in fp64, the lam
+sensitivities Phi / Z / Gam / t rounded to fp32 at every stage, the master in fp64). Reports the iteration counts of
+both and the largest u0 difference at exit (the parity tolerance is 1e-3).
+usage: python tools/seg_ipm_study.py gpurun_out/tick_dump_metric.npz [--S 4] [--ticks 2] [--n 1024]"""
+import argparse
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+
+
+def f32(a, on):
+    return a.astype(np.float32).astype(np.float64) if on else a
+
+
+def seg_riccati(emu, sig, ghat, S, sens32=True):
+    """Batched segmented solve of emu's Newton system (segments [qL, (q+1)L), the last one through N)."""
+    Q, N, nx, nu = emu.Q, emu.N, emu.nx, emu.nu
+    Bn = emu.B
+    D = emu.H + sig
+    L = N // S
+    assert L * S == N
+    idx = np.arange(nx)
+    segs = []
+    fac = {}
+    for q in range(S):
+        last = q == S - 1
+        P = np.zeros((Bn, nx, nx))
+        p = np.zeros((Bn, nx))
+        Phi = np.zeros((Bn, nx, nx))
+        if last:
+            P[:, idx, idx] = D[:, N, nu:]
+            p[:] = ghat[:, N, nu:]
+        else:
+            Phi[:, idx, idx] = 1.0
+        Gam = np.zeros((Bn, nx, nx))
+        t = np.zeros((Bn, nx))
+        for k in range((q + 1) * L - 1, q * L - 1, -1):
+            G = np.concatenate([Q["B"][:, k], Q["A"][:, k]], axis=2)  # [B][nx][nv]
+            M = np.einsum("bli,blm,bmj->bij", G, P, G)
+            M[:, np.arange(nu + nx), np.arange(nu + nx)] += D[:, k]
+            w = ghat[:, k] + np.einsum("bli,bl->bi", G, p)
+            Y = f32(np.einsum("bli,blc->bic", G, Phi), sens32)
+            Lc = np.linalg.cholesky(M[:, :nu, :nu])
+            LM = np.linalg.solve(Lc, M[:, :nu, nu:]).transpose(0, 2, 1)  # [B][nx][nu]
+            lr = np.linalg.solve(Lc, w[:, :nu, None])[..., 0]
+            Z = f32(np.linalg.solve(Lc, Y[:, :nu]), sens32)                # [B][nu][nx]
+            P = M[:, nu:, nu:] - LM @ LM.transpose(0, 2, 1)
+            P = 0.5 * (P + P.transpose(0, 2, 1))
+            p = w[:, nu:] - np.einsum("bij,bj->bi", LM, lr)
+            Phi = f32(Y[:, nu:] - LM @ Z, sens32)
+            Gam = f32(Gam - Z.transpose(0, 2, 1) @ Z, sens32)
+            t = f32(t - np.einsum("bji,bj->bi", Z, lr), sens32)
+            fac[k] = (Lc, LM, lr, Z)
+        segs.append(dict(P=P, p=p, Phi=Phi, Gam=Gam, t=t))
+    # master (fp64)
+    Ph, ph = segs[S - 1]["P"], segs[S - 1]["p"]
+    Qs, cs, phs = [None] * S, [None] * S, [None] * S
+    eye = np.broadcast_to(np.eye(nx), (Bn, nx, nx))
+    for i in range(S - 2, -1, -1):
+        sg = segs[i]
+        X = eye - sg["Gam"] @ Ph
+        Qm = np.linalg.solve(X.transpose(0, 2, 1), Ph)  # X^-T Phat (= Phat X^-1, symmetric)
+        c = sg["t"] + np.einsum("bij,bj->bi", sg["Gam"], ph)
+        Qs[i], cs[i], phs[i] = Qm, c, ph
+        if i >= 1:
+            Ph = sg["P"] + sg["Phi"] @ Qm @ sg["Phi"].transpose(0, 2, 1)
+            ph = sg["p"] + np.einsum("bij,bj->bi", sg["Phi"], np.einsum("bij,bj->bi", Qm, c) + ph)
+    s = [np.zeros((Bn, nx))]
+    lam = [None] * (S + 1)
+    lam[S] = np.zeros((Bn, nx))
+    for i in range(S - 1):
+        sg = segs[i]
+        v = np.einsum("bli,bl->bi", sg["Phi"], s[i]) + cs[i]
+        lam[i + 1] = np.einsum("bij,bj->bi", Qs[i], v) + phs[i]
+        s.append(np.einsum("bli,bl->bi", sg["Phi"], s[i]) + np.einsum("bij,bj->bi", sg["Gam"], lam[i + 1]) + sg["t"])
+    dz = np.zeros((Bn, N + 1, nu + nx))
+    for q in range(S):
+        x = f32(s[q], True)  # the kernel hands s_q and lam_{q+1} to the segments in fp32
+        lm = f32(lam[q + 1], True)
+        dz[:, q * L, nu:] = x if q > 0 else dz[:, 0, nu:]
+        for k in range(q * L, (q + 1) * L):
+            Lc, LM, lr, Z = fac[k]
+            lrt = lr + np.einsum("bjc,bc->bj", Z, lm)
+            u = -np.linalg.solve(Lc.transpose(0, 2, 1), (lrt + np.einsum("bij,bi->bj", LM, x))[..., None])[..., 0]
+            dz[:, k, :nu] = u
+            x = np.einsum("bij,bj->bi", Q["A"][:, k], x) + np.einsum("bij,bj->bi", Q["B"][:, k], u)
+            dz[:, k + 1, nu:] = x
+    return dz, np.ones(Bn, bool)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("dump")
+    ap.add_argument("--model", default="diff")
+    ap.add_argument("--N", type=int, default=40)
+    ap.add_argument("--n", type=int, default=1024)
+    ap.add_argument("--ticks", type=int, default=2)
+    ap.add_argument("--S", type=int, nargs="+", default=[4])
+    ap.add_argument("--kappa", type=float, default=0.2)
+    ap.add_argument("--f64-sens", action="store_true")
+    a = ap.parse_args()
+    from ipm_emu import Emu
+    from warm_study import build
+    d = np.load(a.dump)
+    single = lambda mu, al, it: np.clip((1 - al) ** 2, 0.01, 0.5)  # noqa: E731
+    for t in range(a.ticks):
+        Q, lam, warm, gpu = build(d, t, a.model, a.N, a.n)
+        wst = (np.nan_to_num(lam[..., 0]), np.nan_to_num(lam[..., 1]), a.kappa, 1e3)
+
+        def run(riccati=None):
+            e_c, e_w = Emu(Q), Emu(Q)
+            if riccati is not None:
+                e_c.riccati = lambda sig, gh, e=e_c: riccati(e, sig, gh)
+                e_w.riccati = lambda sig, gh, e=e_w: riccati(e, sig, gh)
+            rc, rw = e_c.solve(single=single), e_w.solve(single=single, warm=wst)
+            it = np.where(warm, rw["iters"], rc["iters"])
+            u0 = np.where(warm[:, None], rw["z"][:, 0, :e_c.nu], rc["z"][:, 0, :e_c.nu])
+            return it, u0
+        it_s, u_s = run()
+        print(f"tick {t}: serial   iters mean {it_s.mean():.2f} max {it_s.max()} (gpu mean {gpu.mean():.2f} max "
+              f"{gpu.max()})")
+        for S in a.S:
+            it_g, u_g = run(lambda e, sig, gh, S=S: seg_riccati(e, sig, gh, S, not a.f64_sens))
+            print(f"tick {t}: S={S:2d}     iters mean {it_g.mean():.2f} max {it_g.max()}; |diff iters| max "
+                  f"{np.abs(it_g - it_s).max()}; u0 max-abs diff {np.abs(u_g - u_s).max():.2e}")
+
+
+if __name__ == "__main__":
+    main()
