@@ -32,11 +32,15 @@ struct RowRec {
     using T = TeamRec<M, true>;
     static constexpr int NX = M::NX, NU = M::NU, NV = NX + NU, NGV = M::NGV;
     static constexpr int LR = T::LR, LM = T::LM, Z = T::Z, TL = T::TL, TU = T::TU, LL = T::LL, LU = T::LU;
-    static constexpr int LB = T::LB, UB = T::UB, GV = T::GV, GR = T::GR, RS = T::RS;
-    static constexpr int SIG = GR + 1, C0 = GR + 2, GH = GR + 3;
-    static_assert(GH < RS, "phase-A fields fit the team record");
+    static constexpr int LB = T::LB, UB = T::UB, GV = T::GV, GR = T::GR, RS = T::RS, RSS = T::RSS;
+    // GH goes to the LR slot when the stored record has no room past C0 (tric: 16 stored floats): phase A writes
+    // it there after the previous phase C has read LR, and phase B reads it before it stores the new LR
+    static constexpr bool GH_IN_LR = GR + 3 >= RSS;
+    static constexpr int SIG = GR + 1, C0 = GR + 2, GH = GH_IN_LR ? T::LR : GR + 3;
+    static_assert(C0 < RSS && GH < RSS, "phase-A fields fit the stored team record");
     static_assert(T::L2 ? (SIG == T::RU && C0 == T::DZA) : (SIG > T::DZA && SIG > T::RU),
                   "phase-A fields reuse only slots the single-direction team kernel leaves unused");
+    static constexpr int BF1 = GH_IN_LR ? C0 + 1 : GH + 1;  // phase B's contiguous fields [GV, BF1) (+ GH)
     static_assert(LM + NU <= Z && Z < TL, "LR / LM below Z");
 };
 
@@ -158,7 +162,7 @@ template <class M, int W, bool SEG>
 __global__ __launch_bounds__(64 * W, 1) void k_sqp_rti_rowpar(KParams P, KArgs a, int mode)
 {
     using R = RowRec<M>;
-    constexpr int NX = M::NX, NU = M::NU, NV = R::NV, NGV = R::NGV, RS = R::RS;
+    constexpr int NX = M::NX, NU = M::NU, NV = R::NV, NGV = R::NGV, RS = R::RS, RSS = R::RSS;
     constexpr bool QM = rec_quad_major<NV>();
     constexpr int ROWS = 4 * W;
     const int inst = (int)blockIdx.x;
@@ -187,21 +191,21 @@ __global__ __launch_bounds__(64 * W, 1) void k_sqp_rti_rowpar(KParams P, KArgs a
 #pragma unroll
     for (int c = 0; c < M::NBX; c++)
         if (cx == c) { lo_b = P.lbx[c]; hi_b = P.ubx[c]; }
-    constexpr int KS = 16 * RS;
+    constexpr int KS = 16 * RSS;  // floats per stage block (the team kernel's layout)
     const int NR = (N + 1 + ROWS - 1) / ROWS;  // rounds of the stage-parallel phases
     float* const rbase = a.scratch + (size_t)inst * (N + 1) * KS;
-    float* const tbase = rbase + (lv ? r : 0) * rec_lane<RS, QM>();   // idle slots read slot 0
-    float* const tbase_own = rbase + r * rec_lane<RS, QM>();          // every lane's own slot
+    float* const tbase = rbase + (lv ? r : 0) * rec_lane<RSS, QM>();   // idle slots read slot 0
+    float* const tbase_own = rbase + r * rec_lane<RSS, QM>();          // every lane's own slot
     float* const dzbase = a.scratch + (size_t)a.sstride * (N + 1) * KS + (size_t)inst * (N + 1) * 16 + r;
     // Stores of the serial phases: wave 0 stores (its four rows the same values to the same addresses, as one
     // row would); waves 1.. store into a dummy stage block of their own with the same slot layout (the same
     // coalescing as the real store; nobody reads it). Idle slots and rows past the last stage of a stage-parallel
     // phase store into tdummy.
-    float* const dummy = a.scratch + (size_t)a.sstride * (N + 1) * 16 * (RS + 1);
+    float* const dummy = a.scratch + (size_t)a.sstride * (N + 1) * 16 * (RSS + 1);
     float* const wblk = dummy + ((size_t)(inst & 255) * 4 + wave) * KS;      // this wave's dummy stage block
     float* const wdz = dummy + (size_t)256 * 4 * KS + ((size_t)(inst & 255) * 4 + wave) * 16 + r;  // dummy DZ
     const bool w0 = wave == 0;
-    float* const tdummy = rbase + (size_t)N * KS + 15 * rec_lane<RS, QM>();  // nobody reads it
+    float* const tdummy = rbase + (size_t)N * KS + 15 * rec_lane<RSS, QM>();  // nobody reads it
     const bool warm = P.warm && a.warm && a.warm[inst] && !(a.reset && a.reset[inst]);
     RP_STAMP(0);
 
@@ -471,7 +475,7 @@ __global__ __launch_bounds__(64 * W, 1) void k_sqp_rti_rowpar(KParams P, KArgs a
         }
 #pragma unroll
         for (int i = 0; i < NGV; i++) rec[R::GV + i] = (k < N && lv) ? st[(5 + i) * 16] : 0.0f;
-        rec_store<RS, QM>(kv ? tbase_own + (size_t)k * KS : tdummy, rec);  // idle slots: their own unused slot
+        rec_store_range<0, RSS, RS, QM>(kv ? tbase_own + (size_t)k * KS : tdummy, rec);  // idle slots: own unused slot
         dzbase[(size_t)k * 16] = 0.0f;  // (rows past the end repeat stage N's zero)
     }
     {
@@ -504,13 +508,20 @@ __global__ __launch_bounds__(64 * W, 1) void k_sqp_rti_rowpar(KParams P, KArgs a
         const float cr = dot_v<NX, NU>(0.0f, dzv, grow);
         return (xi >= NGV) ? cr : nx_;
     };
-    // serial sweep k0 -> k1 with the next stage's fields [F0, F1) (+ the DZ plane) in flight (ping-pong buffers,
-    // loads never predicated: the loop is wave-uniform)
-    auto serial = [&](auto f0c, auto f1c, auto dzc, int k0, int k1, int dir, auto&& body) {
+    // phase B's record fields: [GV, BF1) and GH (in the LR slot when the stored record has no room past C0)
+    auto ld_bfields = [&](const float* p, float (&v)[RS]) {
+        ld_range<R::GV, R::BF1, RS, QM>(p, v);
+        if constexpr (R::GH_IN_LR) ld_range<R::GH, R::GH + 1, RS, QM>(p, v);
+    };
+    // serial sweep k0 -> k1 with the next stage's fields [F0, F1) in flight (BF: phase B's fields, ld_bfields)
+    // (ping-pong buffers, loads never predicated: the loop is wave-uniform)
+    auto serial = [&](auto f0c, auto f1c, auto bfc, int k0, int k1, int dir, auto&& body) {
         constexpr int F0 = decltype(f0c)::value, F1 = decltype(f1c)::value;
-        constexpr bool DZ = decltype(dzc)::value;
-        static_assert(!DZ, "the serial phases read no DZ");
-        auto load = [&](int k, float (&v)[RS]) { ld_range<F0, F1, RS, QM>(tbase + (size_t)k * KS, v); };
+        constexpr bool BF = decltype(bfc)::value;
+        auto load = [&](int k, float (&v)[RS]) {
+            if constexpr (BF) ld_bfields(tbase + (size_t)k * KS, v);
+            else ld_range<F0, F1, RS, QM>(tbase + (size_t)k * KS, v);
+        };
         float ra[RS], rb[RS];
         load(k0, ra);
         for (int k = k0;; k += 2 * dir) {
@@ -626,7 +637,12 @@ __global__ __launch_bounds__(64 * W, 1) void k_sqp_rti_rowpar(KParams P, KArgs a
             rc[R::GH] = valid ? gh : 0.0f;
             float* const pk = (lv && kv) ? tbase + (size_t)k * KS : tdummy;
             rec_store_range<R::Z, R::LU + 1, RS, QM>(pk, rc);
-            rec_store_range<R::SIG, R::GH + 1, RS, QM>(pk, rc);
+            if constexpr (R::GH_IN_LR) {
+                rec_store_range<R::SIG, R::C0 + 1, RS, QM>(pk, rc);
+                rec_store_range<R::GH, R::GH + 1, RS, QM>(pk, rc);
+            } else {
+                rec_store_range<R::SIG, R::GH + 1, RS, QM>(pk, rc);
+            }
         });
         {
             float v[6] = {wave_sum_rows(row_sum16(lv ? sum_c : 0.0f)), wave_max_rows(row_max16(lv ? max_c : 0.0f)),
@@ -798,9 +814,9 @@ __global__ __launch_bounds__(64 * W, 1) void k_sqp_rti_rowpar(KParams P, KArgs a
 #pragma unroll
                     for (int jj = 0; jj < NV; jj++) Lrow[jj] = Lr[jj];
                     rec_store_range<R::LR, R::LM + NU, RS, QM>(
-                        lv ? (srow ? tbase + (size_t)k * KS : wblk + r * rec_lane<RS, QM>()) : tdummy, rc);
+                        lv ? (srow ? tbase + (size_t)k * KS : wblk + r * rec_lane<RSS, QM>()) : tdummy, rc);
                 };
-                auto load = [&](int j, float (&v)[RS]) { ld_range<R::GV, R::GH + 1, RS, QM>(tbase + (size_t)kof(j) * KS, v); };
+                auto load = [&](int j, float (&v)[RS]) { ld_bfields(tbase + (size_t)kof(j) * KS, v); };
                 float ra[RS], rb[RS];
                 load(0, ra);
                 for (int j = 0;; j += 2) {
@@ -1097,8 +1113,8 @@ __global__ __launch_bounds__(64 * W, 1) void k_sqp_rti_rowpar(KParams P, KArgs a
             float pv = 0.0f, piv = 0.0f, res_stat = 0.0f, cpi_max = 0.0f;
             bool fail = false;
             if (!(nanf_ > 0.0f || mu != mu)) {
-                serial(std::integral_constant<int, R::GV>{}, std::integral_constant<int, R::GH + 1>{},
-                       std::false_type{}, N, 0, -1, [&](int k, float (&rc)[RS]) {
+                serial(std::integral_constant<int, R::GV>{}, std::integral_constant<int, R::BF1>{},
+                       std::true_type{}, N, 0, -1, [&](int k, float (&rc)[RS]) {
                     const bool vu = is_u && k < N;
                     const bool vx = is_x && k >= 1;
                     const bool valid = vu || vx;
@@ -1159,7 +1175,7 @@ __global__ __launch_bounds__(64 * W, 1) void k_sqp_rti_rowpar(KParams P, KArgs a
                         for (int j = 0; j < NV; j++) Lrow[j] = Lr[j];
                         // LR, LM (every row stores the same values; idle slots store into the dummy record)
                         rec_store_range<R::LR, R::LM + NU, RS, QM>(
-                            lv ? (w0 ? tbase + (size_t)k * KS : wblk + r * rec_lane<RS, QM>()) : tdummy, rc);
+                            lv ? (w0 ? tbase + (size_t)k * KS : wblk + r * rec_lane<RSS, QM>()) : tdummy, rc);
                     }
                     piv = pi_new;
                 });

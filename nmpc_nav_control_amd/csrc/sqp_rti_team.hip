@@ -61,9 +61,9 @@ __device__ unsigned long long g_stamps_c1[256][kStampIts];
 template <class M>
 size_t team_scratch_floats(int N, int stride)
 {
-    // the lane records [robot][stage][slot][RS], the DZ plane [robot][stage][16], then the row-parallel kernel's
-    // dummy stage blocks [256 robots][4 waves][16][RS] and dummy DZ rows [256][4][16] (sqp_rti_rowpar.hip)
-    return (size_t)stride * (N + 1) * 16 * (TeamRec<M>::RS + 1) + (size_t)256 * 4 * 16 * (TeamRec<M>::RS + 1) + 64;
+    // the lane records [robot][stage][slot][RSS], the DZ plane [robot][stage][16], then the row-parallel kernel's
+    // dummy stage blocks [256 robots][4 waves][16][RSS] and dummy DZ rows [256][4][16] (sqp_rti_rowpar.hip)
+    return (size_t)stride * (N + 1) * 16 * (TeamRec<M>::RSS + 1) + (size_t)256 * 4 * 16 * (TeamRec<M>::RSS + 1) + 64;
 }
 
 namespace {
@@ -101,8 +101,9 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a)
 {
     constexpr int mode = MODE == kModeRunPath ? kModeRun : MODE;
     using R = TeamRec<M, SD>;
-    constexpr int NX = M::NX, NU = M::NU, NV = R::NV, NGV = R::NGV, RS = R::RS;
+    constexpr int NX = M::NX, NU = M::NU, NV = R::NV, NGV = R::NGV, RS = R::RS, RSS = R::RSS;
     constexpr bool QM = rec_quad_major<NV>();
+    constexpr int KS = 16 * RSS;  // floats per stage block (16 slots of RSS stored floats)
     const int gt = blockIdx.x * blockDim.x + threadIdx.x;
     // split launches (a.split: small batches on an otherwise idle chip): one 256-lane block per robot. Row 0 of
     // the block is the robot's team; rows 1-15 share the stage-parallel part of P0 with it and leave.
@@ -132,22 +133,21 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a)
 #pragma unroll
     for (int c = 0; c < M::NBX; c++)
         if (cx == c) { lo_b = P.lbx[c]; hi_b = P.ubx[c]; }
-    // this lane's record of stage k: tbase + k * 16 * RS
+    // this lane's record of stage k: tbase + k * KS
     // idle slots (r >= NV) alias slot 0's record: their (unpredicated) loads then read valid data and touch no
     // extra cache lines; they never store
     // the robot's records (indexed by the robot, not the team slot, so that they carry its multipliers to its next
     // solve whatever the placement)
-    float* const tbase = a.scratch + (size_t)inst * (N + 1) * 16 * RS + (lv ? r : 0) * rec_lane<RS, QM>();
+    float* const tbase = a.scratch + (size_t)inst * (N + 1) * KS + (lv ? r : 0) * rec_lane<RSS, QM>();
     // every lane's own slot (idle lanes: one nobody reads), for P0's unconditional record stores
-    float* const tbase_own = a.scratch + (size_t)inst * (N + 1) * 16 * RS + r * rec_lane<RS, QM>();
+    float* const tbase_own = a.scratch + (size_t)inst * (N + 1) * KS + r * rec_lane<RSS, QM>();
     // a record nobody reads (slot 15 of the robot's stage-N block: the idle slot of every model), the target of
     // stores that lanes without work issue unconditionally
-    float* const tdummy = a.scratch + (size_t)inst * (N + 1) * 16 * RS + (size_t)N * 16 * RS + 15 * rec_lane<RS, QM>();
+    float* const tdummy = a.scratch + (size_t)inst * (N + 1) * KS + (size_t)N * KS + 15 * rec_lane<RSS, QM>();
     // this lane's DZ in the dense plane after the records: dzbase + k * 16 (every lane its own float)
-    float* const dzbase = a.scratch + (size_t)a.sstride * (N + 1) * 16 * RS + (size_t)inst * (N + 1) * 16 + r;
+    float* const dzbase = a.scratch + (size_t)a.sstride * (N + 1) * KS + (size_t)inst * (N + 1) * 16 + r;
     // IPM warm start: the bound multipliers of the robot's previous successful solve are still in its records
     const bool warm = P.warm && a.warm && a.warm[inst] && !(a.reset && a.reset[inst]);
-    constexpr int KS = 16 * RS;
 
 #define XB(k, j) a.xbar[((size_t)(k) * NX + (j)) * S + inst]
 #define UBAR(k, j) a.ubar[((size_t)(k) * NU + (j)) * S + inst]
@@ -423,12 +423,12 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a)
         // drain the whole memory counter, these stores included. Same-box A/B: omni4 kernel 1.303 -> 1.256 ms;
         // diff (7 idle lanes, +78 % P0 store bytes) 1.043 -> 1.065 ms, so 9-slot teams keep the masked store
         // (profiles/r02/ab/uncond_stores.txt)
-        if constexpr (NV > 12) rec_store<RS, QM>(tbase_own + (size_t)k * KS, rec);
+        if constexpr (NV > 12) rec_store_range<0, RSS, RS, QM>(tbase_own + (size_t)k * KS, rec);
 #ifdef P0_MASKED_STORE
-        else if (lv) rec_store<RS, QM>(tbase + (size_t)k * KS, rec);
+        else if (lv) rec_store_range<0, RSS, RS, QM>(tbase + (size_t)k * KS, rec);
 #else
         // 9-slot teams: the idle lanes all store into the team's dummy record (one record's bytes, not seven)
-        else rec_store<RS, QM>(lv ? tbase + (size_t)k * KS : tdummy, rec);
+        else rec_store_range<0, RSS, RS, QM>(lv ? tbase + (size_t)k * KS : tdummy, rec);
 #endif
         if constexpr (kDzPlane) dzbase[(size_t)k * 16] = 0.0f;  // P1 of iteration 0 applies a zero step
         // dynamics-feasible initial states: dx_{k+1} = A dx_k + b_k (inputs start at du = 0, dx_0 = x0 - xbar_0);

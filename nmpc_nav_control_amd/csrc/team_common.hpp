@@ -51,10 +51,15 @@ struct TeamRec {
     static_assert(LU < P1S1 && Z < P1S1 && LM + NU <= P1S1, "P1 store block");
     static constexpr int NF = NL, NB = NL;
     static constexpr int MAXF = (GR > RU ? GR : RU) > (DZA > DZ ? DZA : DZ) ? (GR > RU ? GR : RU) : (DZA > DZ ? DZA : DZ);
-    static constexpr int RS = (MAXF + 1 + 3) / 4 * 4;  // dwordx4 records (and the register image of one)
+    static constexpr int RS = (MAXF + 1 + 3) / 4 * 4;  // register image of a record (dwordx4 pieces)
+    // stored floats per lane record: fields [0, GR] (every kernel stores nothing past the gradient; the register
+    // image may hold more: the DZ slot of the DZ plane and, in the single-direction layout, the corrector-only RU /
+    // DZA). tric (NGV = 3): 16 stored against a 20-float image, 64-B instead of 80-B records
+    static constexpr int RSS = (GR + 1 + 3) / 4 * 4;
     static constexpr int NQ = RS / 4;
     static_assert(NV <= 16, "a team holds at most 16 variables");
     static_assert(TL % 4 == 0, "bound quad aligned");
+    static_assert(RSS <= RS && (kDzPlane || DZ < RSS) && (L2 || (RU < RSS && DZA < RSS)), "stored fields");
 };
 
 namespace {
@@ -195,9 +200,11 @@ __device__ __forceinline__ void rec_load_range(const float* p, float (&v)[RS])
     sfor<F0 / 4, (F1 + 3) / 4>([&](auto qc) {
         constexpr int q = decltype(qc)::value;
         constexpr int a = (F0 > 4 * q) ? F0 : 4 * q, b = (F1 < 4 * q + 4) ? F1 : 4 * q + 4, L = b - a;
-        static_assert(L != 2 || a % 2 == 0, "dwordx2 piece 8-byte aligned");
         const float* pq = p + q * QS + (a - 4 * q);
-        if constexpr (L == 4) {
+        if constexpr (L == 2 && a % 2 != 0) {  // (unaligned pair: two dword accesses)
+            v[a] = pq[0];
+            v[a + 1] = pq[1];
+        } else if constexpr (L == 4) {
             const float4 t = *reinterpret_cast<const float4*>(pq);
             v[a] = t.x; v[a + 1] = t.y; v[a + 2] = t.z; v[a + 3] = t.w;
         } else if constexpr (L == 3) {
@@ -219,9 +226,11 @@ __device__ __forceinline__ void rec_store_range(float* p, const float (&v)[RS])
     sfor<F0 / 4, (F1 + 3) / 4>([&](auto qc) {
         constexpr int q = decltype(qc)::value;
         constexpr int a = (F0 > 4 * q) ? F0 : 4 * q, b = (F1 < 4 * q + 4) ? F1 : 4 * q + 4, L = b - a;
-        static_assert(L != 2 || a % 2 == 0, "dwordx2 piece 8-byte aligned");
         float* pq = p + q * QS + (a - 4 * q);
-        if constexpr (L == 4) *reinterpret_cast<float4*>(pq) = make_float4(v[a], v[a + 1], v[a + 2], v[a + 3]);
+        if constexpr (L == 2 && a % 2 != 0) {  // (unaligned pair: two dword accesses)
+            pq[0] = v[a];
+            pq[1] = v[a + 1];
+        } else if constexpr (L == 4) *reinterpret_cast<float4*>(pq) = make_float4(v[a], v[a + 1], v[a + 2], v[a + 3]);
         else if constexpr (L == 3) *reinterpret_cast<float3*>(pq) = make_float3(v[a], v[a + 1], v[a + 2]);
         else if constexpr (L == 2) *reinterpret_cast<float2*>(pq) = make_float2(v[a], v[a + 1]);
         else pq[0] = v[a];
