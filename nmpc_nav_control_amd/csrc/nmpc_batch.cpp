@@ -38,6 +38,13 @@ struct nmpc_batch {
     unsigned char* warm = nullptr;  // [capacity] the robot's last solve succeeded: its scratch records hold its
                                     // multipliers (IPM warm start)
     int* sorted = nullptr;       // [capacity] sort scratch
+    // hybrid launch (A/B, NMPC_AMD_HYBRID=H): in a team-kernel launch the robots whose last IPM count was >= H (at
+    // most hybrid_cap of them, the hardest first) run the segmented row-parallel kernel (one wave each) on aux,
+    // concurrently with the team kernel on the caller's stream for the rest (DESIGN.md "Hybrid launch")
+    int hybrid_h = 0, hybrid_cap = 1024;
+    int* hyb_n = nullptr;        // [1] robots taken by the segmented part (device)
+    hipStream_t aux = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
 };
 
 namespace {
@@ -171,6 +178,12 @@ hipError_t schedule(nmpc_batch* b, KArgs& a, int mode, hipStream_t s)
     // small batches leave most of the chip idle: one wave per robot, whose spare rows integrate P0's stages
     a.split = (!a.dense && a.B <= b->split_max) ? 1 : 0;
     if (a.split) return hipSuccess;  // one robot per wave: nothing to place
+    if (b->hybrid_h > 0 && b->kp.ipm == NMPC_IPM_SINGLE && !a.segs && b->hyb_n) {
+        a.hyb_role = 1;  // launch() adds the segmented part on the aux stream
+        a.hyb_n = b->hyb_n;
+        a.order = b->order;
+        return launch_hybrid_order(b->iter_key, a.B, b->hybrid_h, b->hybrid_cap, b->order, b->hyb_n, s);
+    }
     int layout = b->sched;
     if (layout == NMPC_SCHED_AUTO) layout = a.dense ? NMPC_SCHED_SORTED : NMPC_SCHED_OFF;
     if (layout == NMPC_SCHED_OFF) return hipSuccess;
@@ -178,10 +191,43 @@ hipError_t schedule(nmpc_batch* b, KArgs& a, int mode, hipStream_t s)
     return launch_team_order(b->iter_key, a.B, layout, b->sorted, b->order, s);
 }
 
+template <class M>
+hipError_t launch_hybrid(nmpc_batch* b, KArgs& a, int mode, hipStream_t s)
+{
+    // the segmented part: one wave per robot (4 rows, segments per seg_count), ranks [0, hyb_n) of the order
+    KArgs g = a;
+    g.hyb_role = 2;
+    g.hyb_cap = b->hybrid_cap;
+    g.rowpar = 1;
+    g.seg = b->seg >= 0 ? b->seg : seg_count(b->prm.N, 4);
+    if (g.seg > 4 || (g.seg > 0 && b->prm.N % g.seg)) g.seg = 0;
+    if (rowpar_lds_bytes<M>(b->prm.N, mode, g.seg) > 65536) g.seg = 0;
+    hipError_t e;
+    if (!b->aux) {
+        if ((e = hipStreamCreateWithFlags(&b->aux, hipStreamNonBlocking)) != hipSuccess ||
+            (e = hipEventCreateWithFlags(&b->ev_fork, hipEventDisableTiming)) != hipSuccess ||
+            (e = hipEventCreateWithFlags(&b->ev_join, hipEventDisableTiming)) != hipSuccess)
+            return e;
+    }
+    if ((e = hipEventRecord(b->ev_fork, s)) != hipSuccess || (e = hipStreamWaitEvent(b->aux, b->ev_fork, 0)) != hipSuccess)
+        return e;
+    if ((e = launch_sqp_rti_rowpar<M>(b->kp, g, mode, b->aux)) != hipSuccess) return e;
+    if ((e = launch_sqp_rti_team<M>(b->kp, a, mode, s)) != hipSuccess) return e;
+    if ((e = hipEventRecord(b->ev_join, b->aux)) != hipSuccess) return e;
+    return hipStreamWaitEvent(s, b->ev_join, 0);
+}
+
 hipError_t launch(nmpc_batch* b, KArgs& a, int mode, hipStream_t s)
 {
     const hipError_t e = schedule(b, a, mode, s);
     if (e != hipSuccess) return e;
+    if (a.hyb_role == 1) {
+        switch (b->prm.model) {
+        case NMPC_MODEL_DIFF2AMR: return launch_hybrid<Diff2>(b, a, mode, s);
+        case NMPC_MODEL_OMNI4AMR: return launch_hybrid<Omni4>(b, a, mode, s);
+        default: return launch_hybrid<Tric3>(b, a, mode, s);
+        }
+    }
     switch (b->prm.model) {
     case NMPC_MODEL_DIFF2AMR: return launch_m<Diff2>(b, a, mode, s);
     case NMPC_MODEL_OMNI4AMR: return launch_m<Omni4>(b, a, mode, s);
@@ -365,6 +411,8 @@ int nmpc_batch_create(const nmpc_model_params* prm, int capacity, nmpc_batch** o
     if (const char* v = std::getenv("NMPC_AMD_SPLIT_MAX")) b->split_max = std::atoi(v);  // A/B: 0 = never split
     if (const char* v = std::getenv("NMPC_AMD_ROWPAR_MAX")) b->rowpar_max = std::atoi(v);  // A/B: 0 = never
     if (const char* v = std::getenv("NMPC_AMD_SEG")) b->seg = std::atoi(v);  // A/B: 0 = serial, S = S segments
+    if (const char* v = std::getenv("NMPC_AMD_HYBRID")) b->hybrid_h = std::atoi(v);  // A/B: 0 = off
+    if (const char* v = std::getenv("NMPC_AMD_HYBRID_CAP")) b->hybrid_cap = std::atoi(v);
     const int N = prm->N;
     const size_t S = (size_t)capacity;
     hipError_t e;
@@ -373,7 +421,8 @@ int nmpc_batch_create(const nmpc_model_params* prm, int capacity, nmpc_batch** o
     if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&props, dev) == hipSuccess &&
         props.multiProcessorCount > 0)
         b->n_simd = 4 * props.multiProcessorCount;
-    if ((e = hipMalloc(&b->iter_key, sizeof(int) * S)) != hipSuccess ||
+    if ((e = hipMalloc(&b->hyb_n, sizeof(int))) != hipSuccess || (e = hipMemset(b->hyb_n, 0, sizeof(int))) != hipSuccess ||
+        (e = hipMalloc(&b->iter_key, sizeof(int) * S)) != hipSuccess ||
         (e = hipMalloc(&b->order, sizeof(int) * S)) != hipSuccess ||
         (e = hipMalloc(&b->sorted, sizeof(int) * S)) != hipSuccess ||
         (e = hipMemset(b->iter_key, 0, sizeof(int) * S)) != hipSuccess ||
@@ -406,6 +455,10 @@ int nmpc_batch_destroy(nmpc_batch* b)
     (void)hipFree(b->order);
     (void)hipFree(b->sorted);
     (void)hipFree(b->warm);
+    (void)hipFree(b->hyb_n);
+    if (b->ev_fork) (void)hipEventDestroy(b->ev_fork);
+    if (b->ev_join) (void)hipEventDestroy(b->ev_join);
+    if (b->aux) (void)hipStreamDestroy(b->aux);
     delete b;
     return NMPC_OK;
 }

@@ -62,6 +62,11 @@ struct KArgs {
                     // row k mod 16, joined by a block barrier); small batches
     int seg;        // k_sqp_rti_rowpar: horizon segments S (N % S == 0) whose Riccati sweeps run in parallel on S rows,
                     // joined by a master recursion over the segment boundaries; 0: the serial phases B / C
+    // hybrid launch (nmpc_batch.cpp): the robots of the first hyb_n[0] ranks of `order` (the hardest by last tick's
+    // IPM count) run the segmented row-parallel kernel on a second stream (role 2, at most hyb_cap blocks), the
+    // rest the team kernel (role 1, team slot t -> order[hyb_n[0] + t]); role 0: a plain launch
+    const int* hyb_n;
+    int hyb_role, hyb_cap;
 };
 
 template <class M>
@@ -79,6 +84,8 @@ hipError_t launch_fleet_sim(const KParams& P, int B, int stride, float* path, fl
                             float* steer, const float* u0, const int* status, const float* carried, float* traj,
                             int* traj_len, int advance, const nmpc_fleet_renew* renew, hipStream_t stream);
 hipError_t launch_team_order(const int* key, int B, int layout, int* sorted, int* order, hipStream_t stream);
+// sorted order (hardest first) plus nhard[0] = min(#robots with key >= H, cap): the hybrid launch's split
+hipError_t launch_hybrid_order(const int* key, int B, int H, int cap, int* order, int* nhard, hipStream_t stream);
 hipError_t launch_path_discretize(int B, const nmpc_path_segment* segs, int seg_stride, const int* nseg,
                                   const double* nearest_u, double period, int num_poses, int holo, float* traj,
                                   double* traj64, hipStream_t stream);

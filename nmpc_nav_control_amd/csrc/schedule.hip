@@ -24,12 +24,15 @@ constexpr int kOrderThreads = 1024;
 constexpr int kOrderBins = 32;  // keys clamp to [0, 31] (IPM iterations; iter_max reaches 50 only on failures)
 
 __global__ __launch_bounds__(kOrderThreads) void k_team_order(const int* __restrict__ key, int B, int layout,
-                                                               int* __restrict__ sorted, int* __restrict__ order)
+                                                               int* __restrict__ sorted, int* __restrict__ order,
+                                                               int H = 0, int cap = 0, int* __restrict__ nhard = nullptr)
 {
     // cnt[bin][thread]: private column per thread, then one exclusive scan in (bin descending, thread) order
     __shared__ unsigned cnt[kOrderBins][kOrderThreads];
     __shared__ unsigned part[kOrderThreads];
+    __shared__ unsigned hcnt;
     const int t = threadIdx.x;
+    if (t == 0) hcnt = 0;
     const int E = (B + kOrderThreads - 1) / kOrderThreads;
     const int i0 = min(B, t * E), i1 = min(B, i0 + E);
     for (int b = 0; b < kOrderBins; b++) cnt[b][t] = 0;
@@ -65,9 +68,16 @@ __global__ __launch_bounds__(kOrderThreads) void k_team_order(const int* __restr
     }
     __syncthreads();
     int* dst = (layout == NMPC_SCHED_SORTED) ? order : sorted;
+    unsigned nh = 0;
     for (int i = i0; i < i1; i++) {
         const int k = min(max(key[i], 0), kOrderBins - 1);
         dst[cnt[kOrderBins - 1 - k][t]++] = i;
+        nh += (nhard && key[i] >= H) ? 1u : 0u;
+    }
+    if (nhard) {  // the hybrid split: how many of the hardest ranks go to the segmented kernel
+        if (nh) atomicAdd(&hcnt, nh);
+        __syncthreads();
+        if (t == 0) nhard[0] = min((int)hcnt, cap);
     }
     if (layout == NMPC_SCHED_SORTED) return;
     __threadfence_block();
@@ -97,7 +107,16 @@ __global__ __launch_bounds__(kOrderThreads) void k_team_order(const int* __restr
 hipError_t launch_team_order(const int* key, int B, int layout, int* sorted, int* order, hipStream_t stream)
 {
     if (B <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_team_order, dim3(1), dim3(kOrderThreads), 0, stream, key, B, layout, sorted, order);
+    hipLaunchKernelGGL(k_team_order, dim3(1), dim3(kOrderThreads), 0, stream, key, B, layout, sorted, order, 0, 0,
+                       nullptr);
+    return hipGetLastError();
+}
+
+hipError_t launch_hybrid_order(const int* key, int B, int H, int cap, int* order, int* nhard, hipStream_t stream)
+{
+    if (B <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_team_order, dim3(1), dim3(kOrderThreads), 0, stream, key, B, (int)NMPC_SCHED_SORTED, order,
+                       order, H, cap, nhard);
     return hipGetLastError();
 }
 

@@ -117,7 +117,7 @@ __device__ __forceinline__ void ld_range(const float* p, float (&v)[RS])
 }
 
 // zeros: the warm-start multiplier source of a cold robot (the flag selects the address, not the value)
-__device__ float g_rp_zero4[4];
+__device__ __attribute__((aligned(16))) float g_rp_zero4[4];
 
 // fp64 value of lane `lane` (wave-uniform) in every lane
 __device__ __forceinline__ double readlane_d(double v, int lane)
@@ -165,7 +165,9 @@ __global__ __launch_bounds__(64 * W, 1) void k_sqp_rti_rowpar(KParams P, KArgs a
     constexpr int NX = M::NX, NU = M::NU, NV = R::NV, NGV = R::NGV, RS = R::RS, RSS = R::RSS;
     constexpr bool QM = rec_quad_major<NV>();
     constexpr int ROWS = 4 * W;
-    const int inst = (int)blockIdx.x;
+    // hybrid launch (role 2): block i takes the robot of rank i of the order, for the first hyb_n[0] ranks
+    if (a.hyb_role == 2 && (int)blockIdx.x >= a.hyb_n[0]) return;
+    const int inst = (a.hyb_role == 2) ? a.order[blockIdx.x] : (int)blockIdx.x;
     if (inst >= a.B) return;
     const int tid = (int)threadIdx.x;
     const int wave = tid >> 6;
@@ -1388,13 +1390,14 @@ hipError_t launch_sqp_rti_rowpar(const KParams& P, const KArgs& a, int mode, hip
     // segments: N % S == 0, at most kSegMax and at most one per row of the block
     if (a.seg < 0 || a.seg > kSegMax || a.seg > 4 * (a.rowpar >= 4 ? 4 : 1) || (a.seg > 0 && P.N % a.seg != 0))
         return hipErrorInvalidValue;
+    const int grid = (a.hyb_role == 2) ? (a.B < a.hyb_cap ? a.B : a.hyb_cap) : a.B;
     if (a.rowpar >= 4)  // four waves per robot (one per SIMD of its CU)
-        if (a.seg > 0) hipLaunchKernelGGL((k_sqp_rti_rowpar<M, 4, true>), dim3(a.B), dim3(256), lds, stream, P, a, mode);
-        else hipLaunchKernelGGL((k_sqp_rti_rowpar<M, 4, false>), dim3(a.B), dim3(256), lds, stream, P, a, mode);
+        if (a.seg > 0) hipLaunchKernelGGL((k_sqp_rti_rowpar<M, 4, true>), dim3(grid), dim3(256), lds, stream, P, a, mode);
+        else hipLaunchKernelGGL((k_sqp_rti_rowpar<M, 4, false>), dim3(grid), dim3(256), lds, stream, P, a, mode);
     else if (a.seg > 0)
-        hipLaunchKernelGGL((k_sqp_rti_rowpar<M, 1, true>), dim3(a.B), dim3(64), lds, stream, P, a, mode);
+        hipLaunchKernelGGL((k_sqp_rti_rowpar<M, 1, true>), dim3(grid), dim3(64), lds, stream, P, a, mode);
     else
-        hipLaunchKernelGGL((k_sqp_rti_rowpar<M, 1, false>), dim3(a.B), dim3(64), lds, stream, P, a, mode);
+        hipLaunchKernelGGL((k_sqp_rti_rowpar<M, 1, false>), dim3(grid), dim3(64), lds, stream, P, a, mode);
     return hipGetLastError();
 }
 

@@ -110,11 +110,13 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a)
     const int team = a.split ? (int)blockIdx.x : (gt >> 4);
     const int row = a.split ? (int)(threadIdx.x >> 4) : 0;
     const int r = gt & 15;
-    if (team >= a.B) return;  // whole DPP rows leave together
+    // hybrid launch: the first hyb_n[0] ranks of the order run the segmented kernel on another stream
+    const int hoff = (a.hyb_role == 1) ? a.hyb_n[0] : 0;
+    if (team >= a.B - hoff) return;  // whole DPP rows leave together
     const int N = P.N;
     const size_t S = (size_t)a.stride;  // resident state stride (capacity)
     const size_t Bn = (size_t)a.B;
-    const int inst = a.order ? a.order[team] : team;  // difficulty-ordered placement (schedule.hip)
+    const int inst = a.order ? a.order[hoff + team] : team;  // difficulty-ordered placement (schedule.hip)
     const bool lv = r < NV;
     const bool is_u = r < NU;
     const bool is_x = lv && !is_u;

@@ -98,3 +98,41 @@ def test_seg_one_wave_per_robot(built, monkeypatch, model):
         assert (sg["status"] == 0).all() and (se["status"] == 0).all(), tick
         assert close(sg["u0"], se["u0"]) <= TOL_SEG, (tick, close(sg["u0"], se["u0"]))
     assert float(np.abs(out[0][0]["u0"].cpu().numpy().T - u0_o).max()) <= TOL
+
+
+@pytest.mark.parametrize("model", ["diff", "tric"])
+def test_hybrid_launch_matches_plain(built, monkeypatch, model):
+    """NMPC_AMD_HYBRID=H: in a team-kernel launch the robots whose last IPM count was >= H run the segmented kernel
+    on a second stream while the team kernel takes the rest (DESIGN.md "Hybrid launch"). Every robot's result equals
+    the plain team launch's to the row-parallel kernel's tolerance, over ticks whose split changes with the counts."""
+    N, B = 40, 600
+    o, rec = oracle_closed_loop(model, N, B, 2)
+    nx, nu = o.nx, o.nu
+    monkeypatch.setenv("NMPC_AMD_HYBRID", "8")
+    monkeypatch.setenv("NMPC_AMD_SPLIT_MAX", "0")
+    hy = BatchSolver(model, N, B, params=default_params(model, N))
+    monkeypatch.delenv("NMPC_AMD_HYBRID")
+    pl = BatchSolver(model, N, B, params=default_params(model, N))
+    monkeypatch.delenv("NMPC_AMD_SPLIT_MAX")
+    x0 = t(np.stack([r[0] for r in rec]).T)
+    yref = t(np.stack([r[1] for r in rec]).transpose(1, 2, 0))
+    We = t(np.stack([r[2] for r in rec]).T)
+    for s in (hy, pl):
+        xv, uv, _ = s.state()
+        xv.copy_from(t(np.stack([r[3] for r in rec]).reshape(B, -1).T))
+        uv.copy_from(t(np.stack([r[4] for r in rec]).reshape(B, -1).T))
+    u0_o = np.stack([o.sqp_rti(r[3], r[4], r[0], r[1], r[2])[3][0] for r in rec])
+    for tick in range(3):
+        res = []
+        for s in (hy, pl):
+            d = dict(u0=torch.zeros(nu, B, device=DEV), status=torch.full((B,), -7, dtype=torch.int32, device=DEV),
+                     qp_iter=torch.zeros(B, dtype=torch.int32, device=DEV))
+            s.solve(x0, yref, We=We, u0=d["u0"], status=d["status"], qp_iter=d["qp_iter"])
+            res.append(d)
+        torch.cuda.synchronize()
+        a, b = res
+        assert (a["status"] == 0).all() and (b["status"] == 0).all(), tick
+        assert close(a["u0"], b["u0"]) <= TOL_SEG, (tick, close(a["u0"], b["u0"]))
+        if tick == 0:
+            assert float(np.abs(a["u0"].cpu().numpy().T - u0_o).max()) <= TOL
+            assert int((b["qp_iter"] >= 8).sum()) > 0  # the next ticks split the batch
