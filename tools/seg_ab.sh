@@ -11,7 +11,7 @@ OUT=$GRAFT_REPO_ROOT/gpurun_out
 mkdir -p $OUT
 cd $GRAFT_REPO_ROOT
 ok() { local rc=$1; if [ $rc -ne 0 ]; then echo "STOP rc=$rc at $2"; exit $rc; fi; }
-timeout -k 10 300 python -u -m pytest tests/test_gpu_seg.py -x -q --timeout 120 --timeout-method thread > $OUT/${TAG}_tests.log 2>&1; ok $? tests
+timeout -k 10 400 python -u -m pytest tests/test_gpu_seg.py -x -q --timeout 120 --timeout-method thread > $OUT/${TAG}_tests.log 2>&1; ok $? tests
 tail -1 $OUT/${TAG}_tests.log
 for S in $SEGS; do
   for mode in warm cold; do
@@ -19,4 +19,7 @@ for S in $SEGS; do
     echo "S=$S $mode $(cat $OUT/${TAG}_cap_s${S}_$mode.json)"
   done
 done
-python tools/ab_env.py $TAG "$CONFIGS" rp4=NMPC_AMD_ROWPAR_MAX=8192,NMPC_AMD_SEG=4 rp0=NMPC_AMD_ROWPAR_MAX=8192,NMPC_AMD_SEG=0 --reps=2; ok $? ab
+# rp4: every robot on the segmented kernel (one wave each, 4 segments); rp0: the serial row-parallel phases;
+# hybN: the hybrid launch with the robots whose last count was >= N on the segmented kernel
+python tools/ab_env.py $TAG "$CONFIGS" rp4=NMPC_AMD_ROWPAR_MAX=8192,NMPC_AMD_SEG=4 rp0=NMPC_AMD_ROWPAR_MAX=8192,NMPC_AMD_SEG=0 \
+    hyb12=NMPC_AMD_HYBRID=12 hyb10=NMPC_AMD_HYBRID=10 --reps=2; ok $? ab
