@@ -55,7 +55,11 @@ struct TeamRec {
     // stored floats per lane record: fields [0, GR] (every kernel stores nothing past the gradient; the register
     // image may hold more: the DZ slot of the DZ plane and, in the single-direction layout, the corrector-only RU /
     // DZA). tric (NGV = 3): 16 stored against a 20-float image, 64-B instead of 80-B records
+#ifndef NMPC_RSS_FULL
     static constexpr int RSS = (GR + 1 + 3) / 4 * 4;
+#else
+    static constexpr int RSS = RS;  // A/B: the round-3 stride (records as long as the register image)
+#endif
     static constexpr int NQ = RS / 4;
     static_assert(NV <= 16, "a team holds at most 16 variables");
     static_assert(TL % 4 == 0, "bound quad aligned");
