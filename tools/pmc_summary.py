@@ -31,9 +31,9 @@ from collections import defaultdict
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def load(prefix, last=None):
+def load(prefix, last=None, runs="_pmc*"):
     acc = defaultdict(lambda: defaultdict(list))
-    for path in glob.glob(prefix + "_pmc*/**/*counter_collection.csv", recursive=True):
+    for path in glob.glob(prefix + runs + "/**/*counter_collection.csv", recursive=True):
         with open(path) as fh:
             rows = sorted(csv.DictReader(fh), key=lambda r: int(r.get("Dispatch_Id") or 0))
             for row in rows:
@@ -72,7 +72,7 @@ def mall(prefix):
     verdict on TCC_EA0_RDREQ_DRAM (the last launch of each run; its JSON line is in the run's log)."""
     res = {}
     for mib in (64, 2048):
-        d = load(f"{prefix}_{mib}", None)
+        d = load(f"{prefix}_{mib}", None, runs="")
         k = next((n for n in d if "k_stream" in n), None)
         line = next((ln for ln in open(f"{prefix}_{mib}.log") if ln.startswith("{")), None)
         bench = json.loads(line) if line else {}
