@@ -149,13 +149,13 @@ def roofline(fleets, node, kernel_ms, steps, step_s=None):
                        "the launches of %d decoupled streams overlapping" % len(fleets)) if node.decoupled else
                       "HIP events on the launch stream(s), timed region",
             "compulsory_bytes_per_launch": cbytes, "achieved_compulsory_GBs": round(cbytes / t_k / 1e9, 2),
-            "hbm": hbm_block(pmc, src, traffic, cbytes, t_k),
+            "hbm": hbm_block(pmc, src, traffic, cbytes, t_k, node.groups),
             "note": "VALU-bound, latency-limited: <=15x15 per-robot blocks, no GEMM-shaped work (no MFMA); "
                     "traffic = 2*FETCH_SIZE + WRITE_SIZE (L2<->fabric incl. Infinity-Cache hits) per step (the sum "
                     "over the step's launches: one per model and stream group)"}
 
 
-def hbm_block(pmc, src, traffic, cbytes, t_k):
+def hbm_block(pmc, src, traffic, cbytes, t_k, groups=1):
     """North-star HBM reporting: the memory-side bytes of the step's solve launches from the PMC record
     (2 x FETCH_SIZE + WRITE_SIZE, the gfx950 correction of MI355X_MICROARCH.md "HBM"), their rate over the launch
     time and its fraction of the 8 TB/s HBM peak, beside the compulsory bytes and their fraction. The
@@ -170,8 +170,17 @@ def hbm_block(pmc, src, traffic, cbytes, t_k):
                     "pmc_over_compulsory": round(traffic / cbytes, 1) if cbytes else None, "pmc_source": src,
                     "includes_mall_hits": True})
     if pmc and pmc.get("ea_rdreq"):
+        # the L2's memory-side requests, sized by tools/ubench_mall.hip (read requests 128 B, write requests 64 B:
+        # 8.00 read requests per KiB streamed, profiles/<round>/pmc/mall_calibration.json): a second, independent
+        # count of the same L2<->fabric bytes. The _DRAM-tagged share is 1.0 for an Infinity-Cache-resident table
+        # as well, so it cannot separate MALL hits from DRAM reads on gfx950
+        g = groups if groups else 1
         rd, rdd = pmc["ea_rdreq"], pmc.get("ea_rdreq_dram")
         wr, wrd = pmc.get("ea_wrreq"), pmc.get("ea_wrreq_dram")
+        ea = g * (rd * 128 + (wr or 0) * 64)
+        out["ea_bytes_per_step"] = ea
+        out["ea_GBs"] = round(ea / t_k / 1e9, 1)
+        out["ea_frac"] = round(ea / t_k / 1e9 / HBM_PEAK_GBS, 4)
         out["dram_destined_share"] = {"read": round(rdd / rd, 4) if rdd is not None else None,
                                       "write": round(wrd / wr, 4) if wr and wrd is not None else None}
         cal, csrc = _profile_json("pmc/mall_calibration.json")
