@@ -45,26 +45,25 @@ struct RowRec {
 };
 
 // LDS of the segmented phases (SEG, a.seg = S > 0), in floats from its base (8-byte aligned; fp64 parts at even
-// offsets). Per segment q: the entry quantities of its backward sweep -- P (fp64 rows), pbar, Phi, Gam, t; per master
-// step i: Q_i = Phat_{i+1} X_i^-1 (fp64), c_i, phat_{i+1}; GJ / transpose scratch; the boundary states s_q and
+// offsets). Per segment q: the entry quantities of its backward sweep -- P (fp64 rows), the factor C_q of -Gam_q
+// (fp64 rows), pbar, Phi, Gam, t; per master step i: Q_i (fp64), c_i, phat_{i+1}; the boundary states s_q and
 // costates lam_q; the lam-sensitivity Z of every stage's LR (rows of the NU input lanes).
 template <class M>
 struct SegLayout {
     static constexpr int NX = M::NX, NU = M::NU, NXP = (M::NX + 3) / 4 * 4;
-    int SUM_P, SUM_PB, SUM_PHI, SUM_GAM, SUM_T, QS, CS, PHS, QT, TV, SL, ZL;
+    int SUM_P, SUM_C, SUM_PB, SUM_PHI, SUM_GAM, SUM_T, QS, CS, PHS, SL, ZL;
     __host__ __device__ explicit SegLayout(int S)
     {
         SUM_P = 0;                          // [S][NX][NX] double
-        SUM_PB = SUM_P + 2 * S * NX * NX;   // [S][NX]
+        SUM_C = SUM_P + 2 * S * NX * NX;    // [S][NX][NX] double (lower triangular)
+        SUM_PB = SUM_C + 2 * S * NX * NX;   // [S][NX]
         SUM_PHI = SUM_PB + S * NX;          // [S][NX][NX]
         SUM_GAM = SUM_PHI + S * NX * NX;    // [S][NX][NX]
         SUM_T = SUM_GAM + S * NX * NX;      // [S][NX]
         QS = (SUM_T + S * NX + 1) / 2 * 2;  // [S][NX][NX] double
         CS = QS + 2 * S * NX * NX;          // [S][NX] double
         PHS = CS + 2 * S * NX;              // [S][NX] double
-        QT = PHS + 2 * S * NX;              // [NX][NX] double
-        TV = QT + 2 * NX * NX;              // [NX] double
-        SL = TV + 2 * NX;                   // [S + 1][2][NX]: s_q, lam_q
+        SL = PHS + 2 * S * NX;              // [S + 1][2][NX]: s_q, lam_q
         ZL = SL + (S + 1) * 2 * NX;         // [N + 1][NU][NXP]
     }
     __host__ __device__ size_t floats(int N) const { return (size_t)ZL + (size_t)(N + 1) * NU * NXP; }
@@ -119,12 +118,22 @@ __device__ __forceinline__ void ld_range(const float* p, float (&v)[RS])
 // zeros: the warm-start multiplier source of a cold robot (the flag selects the address, not the value)
 __device__ __attribute__((aligned(16))) float g_rp_zero4[4];
 
-// fp64 value of lane `lane` (wave-uniform) in every lane
-__device__ __forceinline__ double readlane_d(double v, int lane)
+// Right-looking Cholesky of the NX x NX matrix held row-wise on the state lanes of a 16-lane row (lane NU + i: row
+// i in lr, xi = i), in place: lane NU + i ends with row i of L. rdv[j] = 1 / L[j][j]. A pivot <= thr is dropped
+// (DROP: its column becomes zero, the factor of a positive semidefinite matrix) or poisons the factor with NaN
+// (!DROP: a breakdown the IPM's NaN test reports); a NaN pivot always propagates.
+template <int NX, int NU, bool DROP>
+__device__ __forceinline__ void rowchol(double (&lr)[NX], double (&rdv)[NX], int xi, double thr)
 {
-    const int lo = __builtin_amdgcn_readlane(__double2loint(v), lane);
-    const int hi = __builtin_amdgcn_readlane(__double2hiint(v), lane);
-    return __hiloint2double(hi, lo);
+    double piv = bc64<NU>(lr[0]);
+    sfor<0, NX>([&](auto jc) {
+        constexpr int j = decltype(jc)::value;
+        const double rd = (piv > thr) ? drsq(piv) : ((DROP && piv == piv) ? 0.0 : __builtin_nan(""));
+        rdv[j] = rd;
+        const double lj = (xi >= j) ? lr[j] * rd : 0.0;
+        lr[j] = lj;
+        if constexpr (j + 1 < NX) mst_chol<NX, NU, j>(lr, lj, piv);
+    });
 }
 
 // LDS writes of this wave complete before its next LDS reads (the master's cross-lane exchanges within one wave)
@@ -842,6 +851,25 @@ __global__ __launch_bounds__(64 * W, 1) void k_sqp_rti_rowpar(KParams P, KArgs a
                         seg_lds[SegL.SUM_GAM + (q * NX + xi) * NX + c] = Gam[c];
                     }
                 }
+                // C_q C_q' = -Gam_q (= sum of Z'Z over the segment, positive semidefinite), every row but the
+                // last at once, off the master's serial chain. Pivots below 1e-10 of the largest diagonal entry
+                // (fp32 rounding of a rank-deficient sum) drop their column
+                if (srow && !slast) {
+                    double Cr[NX], rdv[NX];
+                    float dg = 0.0f;
+#pragma unroll
+                    for (int c = 0; c < NX; c++) {
+                        Cr[c] = is_x ? -(double)Gam[c] : 0.0;
+                        dg = (is_x && xi == c) ? -Gam[c] : dg;
+                    }
+                    const double thr = 1e-10 * (double)fmaxf(row_max16(dg), 1e-30f);
+                    rowchol<NX, NU, true>(Cr, rdv, xi, thr);
+                    if (is_x) {
+                        double* const cp = reinterpret_cast<double*>(seg_lds + SegL.SUM_C) + ((size_t)q * NX + xi) * NX;
+#pragma unroll
+                        for (int c = 0; c < NX; c++) cp[c] = Cr[c];
+                    }
+                }
             }
             {
                 float v[6] = {wave_max_rows(row_max16(fail ? 1.0f : 0.0f)), wave_max_rows(row_max16(nanb)), 0.0f,
@@ -861,178 +889,95 @@ __global__ __launch_bounds__(64 * W, 1) void k_sqp_rti_rowpar(KParams P, KArgs a
 
             // ---- master (row 0 of wave 0, fp64): the two-point recursion over the segment boundaries,
             //   s_{i+1} = Phi_i' s_i + Gam_i lam_{i+1} + t_i,   lam_i = P_i s_i + pbar_i + Phi_i lam_{i+1},
-            // backward lam_i = Phat_i s_i + phat_i with Q_i = Phat_{i+1} X_i^-1, X_i = I - Gam_i Phat_{i+1} (I + PSD x
-            // PSD: eigenvalues >= 1; Gauss-Jordan with partial pivoting on X_i'), forward from s_0 = 0. Lane r < NX
-            // holds row r of the matrices; vectors are held whole by every lane; segment data come from LDS
+            // backward lam_i = Phat_i s_i + phat_i with Q_i = Phat_{i+1} (I - Gam_i Phat_{i+1})^-1, formed through the
+            // factor C_i C_i' = -Gam_i as Q_i = Phat - Y Y', Y = Phat C_i R^-T, R R' = K = I + C_i' Phat C_i (K >= I:
+            // Cholesky without pivoting), forward from s_0 = 0. Lane NU + r holds row r of every matrix and element r
+            // of every vector (the fused-DPP blocks of team_asm_gen.hpp); segment data come from LDS
             if (tid < 16 && Sg > 1) {
-                const int rr = r < NX ? r : 0;
-                double* const qt = reinterpret_cast<double*>(seg_lds + SegL.QT);
-                double* const tv = reinterpret_cast<double*>(seg_lds + SegL.TV);
-                double Ph[NX], ph[NX];
-                {
-                    const double* sp = reinterpret_cast<const double*>(seg_lds + SegL.SUM_P) + ((size_t)(Sg - 1) * NX + rr) * NX;
+                const double* const sP = reinterpret_cast<const double*>(seg_lds + SegL.SUM_P);
+                const double* const sC = reinterpret_cast<const double*>(seg_lds + SegL.SUM_C);
+                double* const sQ = reinterpret_cast<double*>(seg_lds + SegL.QS);
+                double* const sCv = reinterpret_cast<double*>(seg_lds + SegL.CS);
+                double* const sPh = reinterpret_cast<double*>(seg_lds + SegL.PHS);
+                auto ldrow = [&](int i, int off, double (&v)[NX]) {  // row xi of segment i's fp32 matrix at off
 #pragma unroll
-                    for (int c = 0; c < NX; c++) {
-                        Ph[c] = sp[c];
-                        ph[c] = (double)seg_lds[SegL.SUM_PB + (Sg - 1) * NX + c];
-                    }
-                }
+                    for (int c = 0; c < NX; c++) v[c] = (double)seg_lds[off + (i * NX + xi) * NX + c];
+                };
+                double Ph[NX], ph;
+#pragma unroll
+                for (int c = 0; c < NX; c++) Ph[c] = sP[((size_t)(Sg - 1) * NX + xi) * NX + c];
+                ph = (double)seg_lds[SegL.SUM_PB + (Sg - 1) * NX + xi];
                 for (int i = Sg - 2; i >= 0; i--) {
-                    const float* const Gi = seg_lds + SegL.SUM_GAM + i * NX * NX;
-                    const float* const Fi = seg_lds + SegL.SUM_PHI + i * NX * NX;
-                    const float* const ti = seg_lds + SegL.SUM_T + i * NX;
-                    // row rr of X' = I - Phat Gam, and of the rhs Phat
-                    double A[NX], Rw[NX];
+                    double Cr[NX], Cc[NX], Fr[NX], Gr[NX];
 #pragma unroll
                     for (int c = 0; c < NX; c++) {
-                        A[c] = (rr == c) ? 1.0 : 0.0;
-                        Rw[c] = Ph[c];
+                        Cr[c] = sC[((size_t)i * NX + xi) * NX + c];
+                        Cc[c] = sC[((size_t)i * NX + c) * NX + xi];
                     }
+                    ldrow(i, SegL.SUM_PHI, Fr);
+                    ldrow(i, SegL.SUM_GAM, Gr);
+                    const double ti = (double)seg_lds[SegL.SUM_T + i * NX + xi];
+                    double U[NX], K[NX], rdv[NX];
 #pragma unroll
-                    for (int l = 0; l < NX; l++)
-#pragma unroll
-                        for (int c = 0; c < NX; c++) A[c] -= Ph[l] * (double)Gi[l * NX + c];
-                    int pst = -1;
+                    for (int c = 0; c < NX; c++) {
+                        U[c] = 0.0;
+                        K[c] = (xi == c) ? 1.0 : 0.0;
+                    }
+                    mst_rowmul<NX, NU>(U, Ph, Cr);  // U = Phat C
+                    mst_rowmul<NX, NU>(K, Cc, U);   // K = I + C' U
+                    rowchol<NX, NU, false>(K, rdv, xi, 0.5);
+                    // Y = U R^-T (row-wise forward substitution), in place of U
                     sfor<0, NX>([&](auto jc) {
                         constexpr int j = decltype(jc)::value;
-                        const bool cand_ok = r < NX && pst < 0;
-                        const float cand = cand_ok ? (float)fabs(A[j]) : -1.0f;
-                        const float m = row_max16(cand);
-                        const unsigned long long bal = __ballot(cand_ok && cand == m);
-                        const int p = (int)__builtin_ctzll(bal | (1ull << 15));
-                        double Ap[NX], Rp[NX];
-#pragma unroll
-                        for (int c = 0; c < NX; c++) {
-                            Ap[c] = readlane_d(A[c], p);
-                            Rp[c] = readlane_d(Rw[c], p);
-                        }
-                        const double inv = 1.0 / Ap[j];
-                        const bool me = r == p;
-                        const double f = A[j] * inv;
-#pragma unroll
-                        for (int c = 0; c < NX; c++) {
-                            A[c] = me ? A[c] * inv : A[c] - f * Ap[c];
-                            Rw[c] = me ? Rw[c] * inv : Rw[c] - f * Rp[c];
-                        }
-                        if (me) pst = j;
+                        const double y = U[j] * rdv[j];
+                        U[j] = y;
+                        if constexpr (j + 1 < NX) mst_trsv<NX, NU, j>(U, K[j], y);
                     });
-                    // the lane that pivoted at step j holds row j of Q_i
-                    if (r < NX) {
+                    double Q[NX];
 #pragma unroll
-                        for (int c = 0; c < NX; c++) qt[pst * NX + c] = Rw[c];
-                    }
-                    lds_fence();
-                    double Qr[NX];
-                    double* const Qi = reinterpret_cast<double*>(seg_lds + SegL.QS) + (size_t)i * NX * NX;
+                    for (int c = 0; c < NX; c++) Q[c] = Ph[c];
+                    mst_rowdot_neg<NX, NU>(Q, U, U);  // Q = Phat - Y Y'
+                    const double cv = mst_vdot<NX, NU>(ti, ph, Gr);  // c_i = t_i + Gam_i phat_{i+1}
+                    if (is_x) {
 #pragma unroll
-                    for (int c = 0; c < NX; c++) Qr[c] = qt[rr * NX + c];
-                    if (r < NX) {
-#pragma unroll
-                        for (int c = 0; c < NX; c++) Qi[rr * NX + c] = Qr[c];
-                    }
-                    // c_i = t_i + Gam_i phat_{i+1}
-                    double cv[NX];
-#pragma unroll
-                    for (int c = 0; c < NX; c++) {
-                        double s = (double)ti[c];
-#pragma unroll
-                        for (int l = 0; l < NX; l++) s += (double)Gi[c * NX + l] * ph[l];
-                        cv[c] = s;
-                    }
-                    if (r == 0) {
-                        double* const ci = reinterpret_cast<double*>(seg_lds + SegL.CS) + (size_t)i * NX;
-                        double* const phi = reinterpret_cast<double*>(seg_lds + SegL.PHS) + (size_t)i * NX;
-#pragma unroll
-                        for (int c = 0; c < NX; c++) {
-                            ci[c] = cv[c];
-                            phi[c] = ph[c];
-                        }
+                        for (int c = 0; c < NX; c++) sQ[((size_t)i * NX + xi) * NX + c] = Q[c];
+                        sCv[i * NX + xi] = cv;
+                        sPh[i * NX + xi] = ph;
                     }
                     if (i >= 1) {
                         // Phat_i = P_i + Phi_i Q_i Phi_i',  phat_i = pbar_i + Phi_i (Q_i c_i + phat_{i+1})
                         double T[NX];
 #pragma unroll
-                        for (int j = 0; j < NX; j++) {
-                            double s = 0.0;
-#pragma unroll
-                            for (int m = 0; m < NX; m++) s += Qr[m] * (double)Fi[j * NX + m];
-                            T[j] = s;
-                        }
-                        double w = ph[0];
-#pragma unroll
-                        for (int c = 1; c < NX; c++) w = (rr == c) ? ph[c] : w;
-#pragma unroll
-                        for (int m = 0; m < NX; m++) w += Qr[m] * cv[m];
-                        lds_fence();  // (every lane has read its Q row before qt is reused)
-                        if (r < NX) {
-#pragma unroll
-                            for (int j = 0; j < NX; j++) qt[rr * NX + j] = T[j];
-                            tv[rr] = w;
-                        }
-                        lds_fence();
-                        const double* const Pi = reinterpret_cast<const double*>(seg_lds + SegL.SUM_P) + ((size_t)i * NX + rr) * NX;
-#pragma unroll
-                        for (int j = 0; j < NX; j++) Ph[j] = Pi[j];
-#pragma unroll
-                        for (int l = 0; l < NX; l++) {
-                            const double fl = (double)Fi[rr * NX + l];
-#pragma unroll
-                            for (int j = 0; j < NX; j++) Ph[j] += fl * qt[l * NX + j];
-                        }
-                        double wv[NX];
-#pragma unroll
-                        for (int l = 0; l < NX; l++) wv[l] = tv[l];
-#pragma unroll
                         for (int c = 0; c < NX; c++) {
-                            double s = (double)seg_lds[SegL.SUM_PB + i * NX + c];
-#pragma unroll
-                            for (int l = 0; l < NX; l++) s += (double)Fi[c * NX + l] * wv[l];
-                            ph[c] = s;
+                            T[c] = 0.0;
+                            Ph[c] = sP[((size_t)i * NX + xi) * NX + c];
                         }
-                        lds_fence();  // (qt / tv reads done before the next step rewrites them)
+                        mst_rowdot<NX, NU>(T, Q, Fr);  // T = Q Phi'
+                        mst_rowmul<NX, NU>(Ph, Fr, T);  // Phat_i = P_i + Phi T
+                        const double w = mst_vdot<NX, NU>(ph, cv, Q);
+                        ph = mst_vdot<NX, NU>((double)seg_lds[SegL.SUM_PB + i * NX + xi], w, Fr);
                     }
                 }
+                lds_fence();  // (Q_i, c_i, phat_{i+1} of every lane stored)
                 // forward: s_0 = 0; lam_{i+1} = Q_i (Phi_i' s_i + c_i) + phat_{i+1}; s_{i+1} = Phi_i' s_i + Gam_i lam_{i+1} + t_i
-                double s[NX];
-#pragma unroll
-                for (int c = 0; c < NX; c++) s[c] = 0.0;
+                double sv = 0.0;
                 float* const sl = seg_lds + SegL.SL;
                 for (int i = 0; i <= Sg - 2; i++) {
-                    const float* const Gi = seg_lds + SegL.SUM_GAM + i * NX * NX;
-                    const float* const Fi = seg_lds + SegL.SUM_PHI + i * NX * NX;
-                    const float* const ti = seg_lds + SegL.SUM_T + i * NX;
-                    const double* const Qi = reinterpret_cast<const double*>(seg_lds + SegL.QS) + (size_t)i * NX * NX;
-                    const double* const ci = reinterpret_cast<const double*>(seg_lds + SegL.CS) + (size_t)i * NX;
-                    const double* const phi = reinterpret_cast<const double*>(seg_lds + SegL.PHS) + (size_t)i * NX;
-                    double v[NX], fs[NX];
+                    double Fc[NX], Gr[NX], Qr[NX];
 #pragma unroll
-                    for (int c = 0; c < NX; c++) {
-                        double acc = 0.0;
-#pragma unroll
-                        for (int l = 0; l < NX; l++) acc += (double)Fi[l * NX + c] * s[l];
-                        fs[c] = acc;
-                        v[c] = acc + ci[c];
+                    for (int l = 0; l < NX; l++) {
+                        Fc[l] = (double)seg_lds[SegL.SUM_PHI + (i * NX + l) * NX + xi];
+                        Qr[l] = sQ[((size_t)i * NX + xi) * NX + l];
                     }
-                    double lrr = phi[rr];
-#pragma unroll
-                    for (int m = 0; m < NX; m++) lrr += Qi[rr * NX + m] * v[m];
-                    if (r < NX) tv[rr] = lrr;
-                    lds_fence();
-                    double lam[NX];
-#pragma unroll
-                    for (int c = 0; c < NX; c++) lam[c] = tv[c];
-#pragma unroll
-                    for (int c = 0; c < NX; c++) {
-                        double acc = fs[c] + (double)ti[c];
-#pragma unroll
-                        for (int l = 0; l < NX; l++) acc += (double)Gi[c * NX + l] * lam[l];
-                        s[c] = acc;
+                    ldrow(i, SegL.SUM_GAM, Gr);
+                    const double fs = mst_vdot<NX, NU>(0.0, sv, Fc);
+                    const double v = fs + sCv[i * NX + xi];
+                    const double lam = mst_vdot<NX, NU>(sPh[i * NX + xi], v, Qr);
+                    sv = mst_vdot<NX, NU>(fs + (double)seg_lds[SegL.SUM_T + i * NX + xi], lam, Gr);
+                    if (is_x) {
+                        sl[(i + 1) * 2 * NX + xi] = (float)sv;
+                        sl[(i + 1) * 2 * NX + NX + xi] = (float)lam;
                     }
-                    if (r < NX) {
-                        sl[(i + 1) * 2 * NX + r] = (float)s[rr];
-                        sl[(i + 1) * 2 * NX + NX + r] = (float)lam[rr];
-                    }
-                    lds_fence();  // (tv read by every lane before the next boundary rewrites it)
                 }
             }
             __syncthreads();  // the boundary states and costates

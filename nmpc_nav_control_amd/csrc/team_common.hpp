@@ -116,6 +116,44 @@ __device__ __forceinline__ float dot_v(float acc, float a, const float (&b)[NX +
     else return dot_v_11_4(acc, a, b);
 }
 
+// segmented-Riccati master blocks (team_asm_gen.hpp): NX x NX matrices on the state lanes NU .. NU + NX - 1
+template <int NX, int NU>
+__device__ __forceinline__ void mst_rowmul(double (&acc)[NX], const double (&a)[NX], const double (&b)[NX])
+{
+    if constexpr (NX == 7 && NU == 2) mst_rowmul_7_2(acc, a, b);
+    else mst_rowmul_11_4(acc, a, b);
+}
+template <int NX, int NU>
+__device__ __forceinline__ void mst_rowdot(double (&acc)[NX], const double (&a)[NX], const double (&b)[NX])
+{
+    if constexpr (NX == 7 && NU == 2) mst_rowdot_7_2(acc, a, b);
+    else mst_rowdot_11_4(acc, a, b);
+}
+template <int NX, int NU>
+__device__ __forceinline__ void mst_rowdot_neg(double (&acc)[NX], const double (&a)[NX], const double (&b)[NX])
+{
+    if constexpr (NX == 7 && NU == 2) mst_rowdot_neg_7_2(acc, a, b);
+    else mst_rowdot_neg_11_4(acc, a, b);
+}
+template <int NX, int NU, int J>
+__device__ __forceinline__ void mst_chol(double (&lr)[NX], double lj, double& piv)
+{
+    if constexpr (NX == 7 && NU == 2) mst_chol_7_2<J>(lr, lj, piv);
+    else mst_chol_11_4<J>(lr, lj, piv);
+}
+template <int NX, int NU, int J>
+__device__ __forceinline__ void mst_trsv(double (&u)[NX], double lc, double y)
+{
+    if constexpr (NX == 7 && NU == 2) mst_trsv_7_2<J>(u, lc, y);
+    else mst_trsv_11_4<J>(u, lc, y);
+}
+template <int NX, int NU>
+__device__ __forceinline__ double mst_vdot(double acc, double x, const double (&a)[NX])
+{
+    if constexpr (NX == 7 && NU == 2) return mst_vdot_7_2(acc, x, a);
+    else return mst_vdot_11_4(acc, x, a);
+}
+
 template <class M>
 __device__ __forceinline__ int xcomp(int xi)
 {

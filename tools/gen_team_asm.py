@@ -90,6 +90,96 @@ def dot_f32(n, j0, name):
             f"    return acc + p1;\n}}\n")
 
 
+# ---- segmented Riccati master (sqp_rti_rowpar.hip SEG): n x n blocks on the state lanes off .. off + n - 1 of
+# one 16-lane row, lane off + r holding row r of every matrix and element r of every vector
+
+def mst_rowmul(n, off):
+    # acc[c] (+|-)= bcast_{off+l}(B[c]) * a[l]: row r of A B (lane off+l holds row l of B); operands acc, B, a
+    out = []
+    for sign, nm in (("", "mst_rowmul"), ("-", "mst_rowmul_neg")):
+        lines = ["s_nop 1"]
+        for l in range(n):
+            for c in range(n):
+                lines.append(f"v_fmac_f64_dpp %{c}, {sign}%{n + c}, %{2 * n + l} row_newbcast:{off + l}{M}")
+        outs = ", ".join(f'"+v"(acc[{c}])' for c in range(n))
+        ins = ", ".join([f'"v"(b[{c}])' for c in range(n)] + [f'"v"(a[{l}])' for l in range(n)])
+        body = "\\n\\t".join(lines)
+        out.append(f"__device__ __forceinline__ void {nm}_{n}_{off}(double (&acc)[{n}], const double (&a)[{n}],"
+                   f" const double (&b)[{n}])\n{{\n    asm(\"{body}\"\n        : {outs}\n        : {ins});\n}}\n")
+    return "\n".join(out)
+
+
+def mst_rowdot(n, off):
+    # acc[c] (+|-)= bcast_{off+c}(b[m]) * a[m]: row r of A B' (lane off+c holds row c of B); operands acc, b, a
+    out = []
+    for sign, nm in (("", "mst_rowdot"), ("-", "mst_rowdot_neg")):
+        lines = ["s_nop 1"]
+        for m in range(n):
+            for c in range(n):
+                lines.append(f"v_fmac_f64_dpp %{c}, {sign}%{n + m}, %{2 * n + m} row_newbcast:{off + c}{M}")
+        outs = ", ".join(f'"+v"(acc[{c}])' for c in range(n))
+        ins = ", ".join([f'"v"(b[{m}])' for m in range(n)] + [f'"v"(a[{m}])' for m in range(n)])
+        body = "\\n\\t".join(lines)
+        out.append(f"__device__ __forceinline__ void {nm}_{n}_{off}(double (&acc)[{n}], const double (&a)[{n}],"
+                   f" const double (&b)[{n}])\n{{\n    asm(\"{body}\"\n        : {outs}\n        : {ins});\n}}\n")
+    return "\n".join(out)
+
+
+def mst_chol(n, off):
+    # right-looking row-distributed Cholesky, column j done: lr[jp] -= bcast_{off+jp}(lj) * lj for jp > j, then the
+    # next pivot bcast_{off+j+1}(lr[j+1])
+    out = []
+    for j in range(n - 1):
+        lines = ["s_nop 1"]
+        ops = []
+        for k, jp in enumerate(range(j + 1, n)):
+            lines.append(f"v_fmac_f64_dpp %{k}, -%{n - j}, %{n - j} row_newbcast:{off + jp}{M}")
+            ops.append(f'"+v"(lr[{jp}])')
+        m = n - j - 1
+        if m < 3:
+            lines.append("s_nop 1")
+        lines.append(f"v_mov_b64_dpp %{m}, %0 row_newbcast:{off + j + 1}{M}")
+        outs = ", ".join(ops + ['"=&v"(piv)'])
+        body = "\\n\\t".join(lines)
+        out.append(f"__device__ __forceinline__ void mst_chol_{n}_{off}_{j}(double (&lr)[{n}], double lj, double& piv)\n"
+                   f"{{\n    asm(\"{body}\"\n        : {outs}\n        : \"v\"(lj));\n}}\n")
+    cases = "\n".join(f"    if constexpr (J == {j}) mst_chol_{n}_{off}_{j}(lr, lj, piv);" for j in range(n - 1))
+    out.append(f"template <int J>\n__device__ __forceinline__ void mst_chol_{n}_{off}(double (&lr)[{n}], double lj,"
+               f" double& piv)\n{{\n{cases}\n}}\n")
+    return "\n".join(out)
+
+
+def mst_trsv(n, off):
+    # forward substitution y L' = u, y_j known: u[m] -= bcast_{off+m}(lc) * y for m > j (lc: the lane's L[.][j])
+    out = []
+    for j in range(n - 1):
+        lines = ["s_nop 1"]
+        ops = []
+        for k, m in enumerate(range(j + 1, n)):
+            lines.append(f"v_fmac_f64_dpp %{k}, -%{n - j - 1}, %{n - j} row_newbcast:{off + m}{M}")
+            ops.append(f'"+v"(u[{m}])')
+        outs = ", ".join(ops)
+        body = "\\n\\t".join(lines)
+        out.append(f"__device__ __forceinline__ void mst_trsv_{n}_{off}_{j}(double (&u)[{n}], double lc, double y)\n"
+                   f"{{\n    asm(\"{body}\"\n        : {outs}\n        : \"v\"(lc), \"v\"(y));\n}}\n")
+    cases = "\n".join(f"    if constexpr (J == {j}) mst_trsv_{n}_{off}_{j}(u, lc, y);" for j in range(n - 1))
+    out.append(f"template <int J>\n__device__ __forceinline__ void mst_trsv_{n}_{off}(double (&u)[{n}], double lc,"
+               f" double y)\n{{\n{cases}\n}}\n")
+    return "\n".join(out)
+
+
+def mst_vdot(n, off):
+    # acc + sum_l bcast_{off+l}(x) * a[l] as two interleaved partial sums (x: a lane-distributed vector)
+    lines = ["s_nop 1"]
+    for l in range(n):
+        lines.append(f"v_fmac_f64_dpp %{l % 2}, %2, %{3 + l} row_newbcast:{off + l}{M}")
+    ins = ", ".join(['"v"(x)'] + [f'"v"(a[{l}])' for l in range(n)])
+    body = "\\n\\t".join(lines)
+    return (f"__device__ __forceinline__ double mst_vdot_{n}_{off}(double acc, double x, const double (&a)[{n}])\n{{\n"
+            f"    double p1 = 0.0;\n    asm(\"{body}\"\n        : \"+v\"(acc), \"+v\"(p1)\n        : {ins});\n"
+            f"    return acc + p1;\n}}\n")
+
+
 def main():
     parts = ["// team_asm_gen.hpp -- GENERATED by tools/gen_team_asm.py; do not edit.",
              "// Whole-block fused-DPP kernels of the team Riccati step (see the generator's docstring).",
@@ -97,7 +187,8 @@ def main():
     for nx, nu in SHAPES:
         nv = nx + nu
         parts += [pg_block(nx, nu), mrow_pg_block(nx, nu), chol_update(nx, nu),
-                  dot_f32(nx, nu, f"dot_x_{nx}_{nu}"), dot_f32(nv, 0, f"dot_v_{nx}_{nu}")]
+                  dot_f32(nx, nu, f"dot_x_{nx}_{nu}"), dot_f32(nv, 0, f"dot_v_{nx}_{nu}"),
+                  mst_rowmul(nx, nu), mst_rowdot(nx, nu), mst_chol(nx, nu), mst_trsv(nx, nu), mst_vdot(nx, nu)]
     parts += ["}  // namespace nmpc", ""]
     with open(OUT, "w") as fh:
         fh.write("\n".join(parts))

@@ -6,7 +6,7 @@
 # usage: gpurun --timeout 1100 -- 'bash tools/seg_ab.sh <tag> [segs] [configs]'
 TAG=${1:-seg}
 SEGS=${2:-"0 4 5 8"}
-CONFIGS=${3:-"diff1024 metric"}
+CONFIGS=${3-"diff1024 metric"}
 OUT=$GRAFT_REPO_ROOT/gpurun_out
 mkdir -p $OUT
 cd $GRAFT_REPO_ROOT
@@ -20,6 +20,7 @@ for S in $SEGS; do
   done
 done
 # rp4: every robot on the segmented kernel (one wave each, 4 segments); rp0: the serial row-parallel phases;
-# hybN: the hybrid launch with the robots whose last count was >= N on the segmented kernel
-python tools/ab_env.py $TAG "$CONFIGS" rp4=NMPC_AMD_ROWPAR_MAX=8192,NMPC_AMD_SEG=4 rp0=NMPC_AMD_ROWPAR_MAX=8192,NMPC_AMD_SEG=0 \
-    hyb12=NMPC_AMD_HYBRID=12 hyb10=NMPC_AMD_HYBRID=10 --reps=2; ok $? ab
+# (VARIANTS overrides the list, REPS the repetitions)
+[ -z "$CONFIGS" ] && exit 0
+python tools/ab_env.py $TAG "$CONFIGS" ${VARIANTS:-rp4=NMPC_AMD_ROWPAR_MAX=8192,NMPC_AMD_SEG=4 rp0=NMPC_AMD_ROWPAR_MAX=8192,NMPC_AMD_SEG=0} \
+    --reps=${REPS:-2}; ok $? ab
