@@ -118,24 +118,6 @@ __device__ __forceinline__ void ld_range(const float* p, float (&v)[RS])
 // zeros: the warm-start multiplier source of a cold robot (the flag selects the address, not the value)
 __device__ __attribute__((aligned(16))) float g_rp_zero4[4];
 
-// Right-looking Cholesky of the NX x NX matrix held row-wise on the state lanes of a 16-lane row (lane NU + i: row
-// i in lr, xi = i), in place: lane NU + i ends with row i of L. rdv[j] = 1 / L[j][j]. A pivot <= thr is dropped
-// (DROP: its column becomes zero, the factor of a positive semidefinite matrix) or poisons the factor with NaN
-// (!DROP: a breakdown the IPM's NaN test reports); a NaN pivot always propagates.
-template <int NX, int NU, bool DROP>
-__device__ __forceinline__ void rowchol(double (&lr)[NX], double (&rdv)[NX], int xi, double thr)
-{
-    double piv = bc64<NU>(lr[0]);
-    sfor<0, NX>([&](auto jc) {
-        constexpr int j = decltype(jc)::value;
-        const double rd = (piv > thr) ? drsq(piv) : ((DROP && piv == piv) ? 0.0 : __builtin_nan(""));
-        rdv[j] = rd;
-        const double lj = (xi >= j) ? lr[j] * rd : 0.0;
-        lr[j] = lj;
-        if constexpr (j + 1 < NX) mst_chol<NX, NU, j>(lr, lj, piv);
-    });
-}
-
 // LDS writes of this wave complete before its next LDS reads (the master's cross-lane exchanges within one wave)
 __device__ __forceinline__ void lds_fence()
 {

@@ -152,6 +152,50 @@ def master(segs, nx):
     return s, lam, Xs
 
 
+def psd_chol(A, thr, drop=True):
+    """Row-distributed right-looking Cholesky of the device (sqp_rti_rowpar.hip rowchol): pivots <= thr drop their
+    column (drop) or give NaN."""
+    n = len(A)
+    L = A.copy()
+    for j in range(n):
+        p = L[j, j]
+        rd = 1.0 / np.sqrt(p) if p > thr else (0.0 if drop and p == p else np.nan)
+        L[j:, j] *= rd
+        L[:j, j] = 0.0
+        for jp in range(j + 1, n):
+            L[jp:, jp] -= L[jp:, j] * L[jp, j]
+    return np.tril(L)
+
+
+def master_chol(segs, nx):
+    """The device master (sqp_rti_rowpar.hip SEG): Q_i = Phat - Y Y', Y = Phat C R^-T, C C' = -Gam_i,
+    R R' = I + C' Phat C; forward lam_{i+1} = Q_i (Phi' s_i + c_i) + phat_{i+1}, s_{i+1} = Phi' s_i + Gam lam + t."""
+    S = len(segs)
+    Ph, ph = segs[S - 1]["P"], segs[S - 1]["p"]
+    Qs, cs, phs = [None] * S, [None] * S, [None] * S
+    for i in range(S - 2, -1, -1):
+        sg = segs[i]
+        G = -sg["Gam"]
+        C = psd_chol(G, 1e-10 * max(G.diagonal().max(), 1e-30))
+        U = Ph @ C
+        R = psd_chol(np.eye(nx) + C.T @ U, 0.5, drop=False)
+        Y = np.linalg.solve(R, U.T).T
+        Q = Ph - Y @ Y.T
+        c = sg["t"] + sg["Gam"] @ ph
+        Qs[i], cs[i], phs[i] = Q, c, ph
+        if i >= 1:
+            Ph = sg["P"] + sg["Phi"] @ (Q @ sg["Phi"].T)
+            ph = sg["p"] + sg["Phi"] @ (ph + Q @ c)
+    s = [np.zeros(nx)]
+    lam = [None] * (S + 1)
+    lam[S] = np.zeros(nx)
+    for i in range(S - 1):
+        fs = segs[i]["Phi"].T @ s[i]
+        lam[i + 1] = Qs[i] @ (fs + cs[i]) + phs[i]
+        s.append(fs + segs[i]["Gam"] @ lam[i + 1] + segs[i]["t"])
+    return s, lam, [np.eye(nx)]
+
+
 def kkt_res(G, H, g, nx, nu, N, us, xs):
     """Largest input-stationarity residual of (us, xs) with the exact adjoint, relative to its terms' size."""
     pi = H[N][nu:] * xs[N] + g[N][nu:]
@@ -164,10 +208,10 @@ def kkt_res(G, H, g, nx, nu, N, us, xs):
     return worst
 
 
-def riccati_segmented(G, H, g, nx, nu, N, S, sens_dtype=np.float64):
+def riccati_segmented(G, H, g, nx, nu, N, S, sens_dtype=np.float64, chol_master=False):
     bnd = np.linspace(0, N + 1, S + 1).round().astype(int)
     segs = [seg_backward(G, H, g, nx, nu, N, bnd[i], bnd[i + 1], sens_dtype) for i in range(S)]
-    s, lam, Xs = master(segs, nx)
+    s, lam, Xs = (master_chol if chol_master else master)(segs, nx)
     us, xs = np.zeros((N, nu)), np.zeros((N + 1, nx))
     gap = 0.0
     for i in range(S):
@@ -194,6 +238,7 @@ def main():
     ap.add_argument("--trials", type=int, default=50)
     ap.add_argument("--sig-max", type=float, default=1e12)
     ap.add_argument("--f32-sens", action="store_true", help="Phi / Z / Gam / t in fp32 (P, the factor in fp64)")
+    ap.add_argument("--chol-master", action="store_true", help="the device's master (factor of -Gam, no pivoting)")
     ap.add_argument("--pinned", action="store_true", help="a vel-ref state and an input at sig_max over stages N/4..3N/4")
     args = ap.parse_args()
     from oracle.oracle import Oracle
@@ -205,7 +250,7 @@ def main():
             G, H, g = make_qp(o, args.N, rng, args.sig_max, args.pinned)
             u_ref, x_ref = riccati_serial(G, H, g, o.nx, o.nu, args.N)
             u, x, gap, cond = riccati_segmented(G, H, g, o.nx, o.nu, args.N, S,
-                                                np.float32 if args.f32_sens else np.float64)
+                                                np.float32 if args.f32_sens else np.float64, args.chol_master)
             scale = max(1.0, np.abs(u_ref).max())
             du.append(np.abs(u - u_ref).max() / scale)
             dxm.append(np.abs(x - x_ref).max() / max(1.0, np.abs(x_ref).max()))

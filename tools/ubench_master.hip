@@ -1,0 +1,209 @@
+// ubench_master.hip -- unit check of the segmented-Riccati master's fused-DPP blocks (team_asm_gen.hpp mst_*,
+// team_common.hpp rowchol) on one 16-lane row against a host fp64 reference: C = chol(G) of a positive
+// semidefinite G (dropped pivots), Q = Phat (I + G Phat)^-1 through Y = Phat C R^-T (R R' = I + C' Phat C),
+// Phat' = Phat + F Q F', the vector blocks c = t + (-G) phat and w = phat + Q c. Prints one JSON line per case.
+// build: make -C nmpc_nav_control_amd/csrc ubench_master   run: build/ubench_master
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <random>
+#include <vector>
+
+#include "team_common.hpp"
+
+using namespace nmpc;
+constexpr int NX = 7, NU = 2;
+
+__global__ void k_master(const double* Ph, const double* G, const double* F, const double* vt, const double* vp,
+                         double thr, double* oC, double* oQ, double* oPn, double* oc, double* ow)
+{
+    __shared__ double sC[NX * NX];
+    const int r = threadIdx.x & 15;
+    const bool is_x = r >= NU && r < NU + NX;
+    const int xi = is_x ? r - NU : 0;
+    double Phr[NX], Cr[NX], Fr[NX], Gn[NX], rdv[NX];
+#pragma unroll
+    for (int c = 0; c < NX; c++) {
+        Phr[c] = Ph[xi * NX + c];
+        Cr[c] = is_x ? G[xi * NX + c] : 0.0;
+        Fr[c] = F[xi * NX + c];
+        Gn[c] = -G[xi * NX + c];
+    }
+    rowchol<NX, NU, true>(Cr, rdv, xi, thr);
+    if (is_x)
+        for (int c = 0; c < NX; c++) {
+            sC[xi * NX + c] = Cr[c];
+            oC[xi * NX + c] = Cr[c];
+        }
+    __syncthreads();
+    double Cc[NX], U[NX], K[NX];
+#pragma unroll
+    for (int c = 0; c < NX; c++) {
+        Cc[c] = sC[c * NX + xi];
+        U[c] = 0.0;
+        K[c] = (xi == c) ? 1.0 : 0.0;
+    }
+    mst_rowmul<NX, NU>(U, Phr, Cr);
+    mst_rowmul<NX, NU>(K, Cc, U);
+    rowchol<NX, NU, false>(K, rdv, xi, 0.5);
+    sfor<0, NX>([&](auto jc) {
+        constexpr int j = decltype(jc)::value;
+        const double y = U[j] * rdv[j];
+        U[j] = y;
+        if constexpr (j + 1 < NX) mst_trsv<NX, NU, j>(U, K[j], y);
+    });
+    double Q[NX], T[NX], Pn[NX];
+#pragma unroll
+    for (int c = 0; c < NX; c++) {
+        Q[c] = Phr[c];
+        T[c] = 0.0;
+        Pn[c] = Phr[c];
+    }
+    mst_rowdot_neg<NX, NU>(Q, U, U);
+    mst_rowdot<NX, NU>(T, Q, Fr);
+    mst_rowmul<NX, NU>(Pn, Fr, T);
+    const double cv = mst_vdot<NX, NU>(vt[xi], vp[xi], Gn);
+    const double w = mst_vdot<NX, NU>(vp[xi], cv, Q);
+    if (is_x) {
+        for (int c = 0; c < NX; c++) {
+            oQ[xi * NX + c] = Q[c];
+            oPn[xi * NX + c] = Pn[c];
+        }
+        oc[xi] = cv;
+        ow[xi] = w;
+    }
+}
+
+// host reference: A^-1 B by Gauss-Jordan with partial pivoting (n x n, row-major)
+static void solve(std::vector<double> A, std::vector<double>& B, int n)
+{
+    for (int j = 0; j < n; j++) {
+        int p = j;
+        for (int i = j + 1; i < n; i++)
+            if (std::fabs(A[i * n + j]) > std::fabs(A[p * n + j])) p = i;
+        for (int c = 0; c < n; c++) {
+            std::swap(A[j * n + c], A[p * n + c]);
+            std::swap(B[j * n + c], B[p * n + c]);
+        }
+        const double d = A[j * n + j];
+        for (int c = 0; c < n; c++) {
+            A[j * n + c] /= d;
+            B[j * n + c] /= d;
+        }
+        for (int i = 0; i < n; i++) {
+            if (i == j) continue;
+            const double f = A[i * n + j];
+            for (int c = 0; c < n; c++) {
+                A[i * n + c] -= f * A[j * n + c];
+                B[i * n + c] -= f * B[j * n + c];
+            }
+        }
+    }
+}
+
+int main()
+{
+    std::mt19937_64 rng(7);
+    std::normal_distribution<double> nd;
+    const int n = NX, nn = NX * NX;
+    int bad = 0;
+    for (int cs = 0; cs < 6; cs++) {
+        const int rank = (cs % 3 == 0) ? 7 : ((cs % 3 == 1) ? 3 : 0);
+        const double pscale = (cs < 3) ? 1e2 : 1e8;
+        std::vector<double> A(nn), H(n * 7), Ph(nn), G(nn, 0.0), F(nn), vt(n), vp(n);
+        for (auto& v : A) v = nd(rng);
+        for (auto& v : H) v = 3.0 * nd(rng);
+        for (auto& v : F) v = nd(rng);
+        for (auto& v : vt) v = nd(rng);
+        for (auto& v : vp) v = nd(rng);
+        for (int i = 0; i < n; i++)
+            for (int j = 0; j < n; j++) {
+                double s = 0.0, g = 0.0;
+                for (int l = 0; l < n; l++) s += A[i * n + l] * A[j * n + l];
+                for (int l = 0; l < rank; l++) g += H[i * 7 + l] * H[j * 7 + l];
+                Ph[i * n + j] = pscale * s;
+                G[i * n + j] = (double)(float)g;  // the kernel's -Gam is an fp32 sum
+            }
+        for (int i = 0; i < n; i++)
+            for (int j = 0; j < i; j++) G[i * n + j] = G[j * n + i];
+        double dmax = 1e-30;
+        for (int i = 0; i < n; i++) dmax = std::fmax(dmax, G[i * n + i]);
+        double *dPh, *dG, *dF, *dvt, *dvp, *dout;
+        (void)hipMalloc(&dPh, nn * 8);
+        (void)hipMalloc(&dG, nn * 8);
+        (void)hipMalloc(&dF, nn * 8);
+        (void)hipMalloc(&dvt, n * 8);
+        (void)hipMalloc(&dvp, n * 8);
+        (void)hipMalloc(&dout, (3 * nn + 2 * n) * 8);
+        (void)hipMemcpy(dPh, Ph.data(), nn * 8, hipMemcpyHostToDevice);
+        (void)hipMemcpy(dG, G.data(), nn * 8, hipMemcpyHostToDevice);
+        (void)hipMemcpy(dF, F.data(), nn * 8, hipMemcpyHostToDevice);
+        (void)hipMemcpy(dvt, vt.data(), n * 8, hipMemcpyHostToDevice);
+        (void)hipMemcpy(dvp, vp.data(), n * 8, hipMemcpyHostToDevice);
+        hipLaunchKernelGGL(k_master, dim3(1), dim3(64), 0, nullptr, dPh, dG, dF, dvt, dvp, 1e-10 * dmax, dout,
+                           dout + nn, dout + 2 * nn, dout + 3 * nn, dout + 3 * nn + n);
+        std::vector<double> out(3 * nn + 2 * n);
+        if (hipMemcpy(out.data(), dout, out.size() * 8, hipMemcpyDeviceToHost) != hipSuccess) {
+            std::fprintf(stderr, "hip error\n");
+            return 2;
+        }
+        // reference: Q = Phat (I + G Phat)^-1 = ((I + G Phat)^-T Phat)^T; X' Q' = Phat with X = I + G Phat
+        // (with the device's own factor: G_eff = C C', so that the check isolates the blocks from the
+        // semidefinite projection of an fp32-rounded rank-deficient G; CCt_err reports that projection)
+        std::vector<double> Xt(nn), Qr(Ph), Ge(nn);
+        for (int i = 0; i < n; i++)
+            for (int j = 0; j < n; j++) {
+                double s = 0.0;
+                for (int l = 0; l < n; l++) s += out[i * n + l] * out[j * n + l];
+                Ge[i * n + j] = s;
+            }
+        for (int i = 0; i < n; i++)
+            for (int j = 0; j < n; j++) {
+                double s = (i == j) ? 1.0 : 0.0;
+                for (int l = 0; l < n; l++) s += Ge[j * n + l] * Ph[l * n + i];  // (I + G Ph)^T [i][j]
+                Xt[i * n + j] = s;
+            }
+        solve(Xt, Qr, n);  // Qr = X^-T Ph = Q^T (= Q)
+        double eq = 0.0, mq = 0.0, ep = 0.0, mp = 0.0, ec = 0.0, ew = 0.0, ecc = 0.0;
+        for (int i = 0; i < n; i++)
+            for (int j = 0; j < n; j++) {
+                eq = std::fmax(eq, std::fabs(out[nn + i * n + j] - Qr[j * n + i]));
+                mq = std::fmax(mq, std::fabs(Qr[i * n + j]));
+                double fqf = 0.0;
+                for (int a = 0; a < n; a++)
+                    for (int b = 0; b < n; b++) fqf += F[i * n + a] * Qr[a * n + b] * F[j * n + b];
+                const double pn = Ph[i * n + j] + fqf;
+                ep = std::fmax(ep, std::fabs(out[2 * nn + i * n + j] - pn));
+                mp = std::fmax(mp, std::fabs(pn));
+                double cc = 0.0;
+                for (int l = 0; l < n; l++) cc += out[i * n + l] * out[j * n + l];
+                ecc = std::fmax(ecc, std::fabs(cc - G[i * n + j]) / dmax);
+            }
+        std::vector<double> cref(n);
+        for (int i = 0; i < n; i++) {
+            double s = vt[i];
+            for (int l = 0; l < n; l++) s -= G[i * n + l] * vp[l];
+            cref[i] = s;
+            ec = std::fmax(ec, std::fabs(out[3 * nn + i] - s) / (1.0 + std::fabs(s)));
+        }
+        for (int i = 0; i < n; i++) {
+            double s = vp[i];
+            for (int l = 0; l < n; l++) s += Qr[i * n + l] * cref[l];
+            ew = std::fmax(ew, std::fabs(out[3 * nn + n + i] - s) / (1.0 + std::fabs(s)));
+        }
+        const bool ok = eq / mq < 1e-9 && ep / mp < 1e-9 && ec < 1e-9 && ew < 1e-6 && ecc < 1e-5;
+        bad += !ok;
+        std::printf("{\"case\": %d, \"rank_G\": %d, \"phat_scale\": %g, \"Q_rel_err\": %.3e, \"Pnext_rel_err\": %.3e, "
+                    "\"CCt_err\": %.3e, \"c_err\": %.3e, \"w_err\": %.3e, \"ok\": %s}\n",
+                    cs, rank, pscale, eq / mq, ep / mp, ecc, ec, ew, ok ? "true" : "false");
+        (void)hipFree(dPh);
+        (void)hipFree(dG);
+        (void)hipFree(dF);
+        (void)hipFree(dvt);
+        (void)hipFree(dvp);
+        (void)hipFree(dout);
+    }
+    return bad ? 1 : 0;
+}
