@@ -46,12 +46,13 @@ struct RowRec {
 
 // LDS of the segmented phases (SEG, a.seg = S > 0), in floats from its base (8-byte aligned; fp64 parts at even
 // offsets). Per segment q: the entry quantities of its backward sweep -- P (fp64 rows), the factor C_q of -Gam_q
-// (fp64 rows), pbar, Phi, Gam, t; per master step i: Q_i (fp64), c_i, phat_{i+1}; the boundary states s_q and
+// (fp64 rows), pbar, Phi, Gam, t; per master step i: Q_i (fp64), c_i, phat_{i+1}; a transpose scratch; the
+// boundary states s_q and
 // costates lam_q; the lam-sensitivity Z of every stage's LR (rows of the NU input lanes).
 template <class M>
 struct SegLayout {
     static constexpr int NX = M::NX, NU = M::NU, NXP = (M::NX + 3) / 4 * 4;
-    int SUM_P, SUM_C, SUM_PB, SUM_PHI, SUM_GAM, SUM_T, QS, CS, PHS, SL, ZL;
+    int SUM_P, SUM_C, SUM_PB, SUM_PHI, SUM_GAM, SUM_T, QS, CS, PHS, LT, SL, ZL;
     __host__ __device__ explicit SegLayout(int S)
     {
         SUM_P = 0;                          // [S][NX][NX] double
@@ -63,7 +64,8 @@ struct SegLayout {
         QS = (SUM_T + S * NX + 1) / 2 * 2;  // [S][NX][NX] double
         CS = QS + 2 * S * NX * NX;          // [S][NX] double
         PHS = CS + 2 * S * NX;              // [S][NX] double
-        SL = PHS + 2 * S * NX;              // [S + 1][2][NX]: s_q, lam_q
+        LT = PHS + 2 * S * NX;              // [NX][NX] double: the master's transpose scratch
+        SL = LT + 2 * NX * NX;              // [S + 1][2][NX]: s_q, lam_q
         ZL = SL + (S + 1) * 2 * NX;         // [N + 1][NU][NXP]
     }
     __host__ __device__ size_t floats(int N) const { return (size_t)ZL + (size_t)(N + 1) * NU * NXP; }
@@ -834,17 +836,14 @@ __global__ __launch_bounds__(64 * W, 1) void k_sqp_rti_rowpar(KParams P, KArgs a
                     }
                 }
                 // C_q C_q' = -Gam_q (= sum of Z'Z over the segment, positive semidefinite), every row but the
-                // last at once, off the master's serial chain. Pivots below 1e-10 of the largest diagonal entry
-                // (fp32 rounding of a rank-deficient sum) drop their column
+                // last at once, off the master's serial chain; non-positive pivots (fp32 rounding of a
+                // rank-deficient sum) drop their column (tools/seg_emu.py --chol-master: any positive drop
+                // threshold costs accuracy on pinned QPs)
                 if (srow && !slast) {
                     double Cr[NX], rdv[NX];
-                    float dg = 0.0f;
 #pragma unroll
-                    for (int c = 0; c < NX; c++) {
-                        Cr[c] = is_x ? -(double)Gam[c] : 0.0;
-                        dg = (is_x && xi == c) ? -Gam[c] : dg;
-                    }
-                    const double thr = 1e-10 * (double)fmaxf(row_max16(dg), 1e-30f);
+                    for (int c = 0; c < NX; c++) Cr[c] = is_x ? -(double)Gam[c] : 0.0;
+                    const double thr = 0.0;
                     rowchol<NX, NU, true>(Cr, rdv, xi, thr);
                     if (is_x) {
                         double* const cp = reinterpret_cast<double*>(seg_lds + SegL.SUM_C) + ((size_t)q * NX + xi) * NX;
@@ -872,8 +871,8 @@ __global__ __launch_bounds__(64 * W, 1) void k_sqp_rti_rowpar(KParams P, KArgs a
             // ---- master (row 0 of wave 0, fp64): the two-point recursion over the segment boundaries,
             //   s_{i+1} = Phi_i' s_i + Gam_i lam_{i+1} + t_i,   lam_i = P_i s_i + pbar_i + Phi_i lam_{i+1},
             // backward lam_i = Phat_i s_i + phat_i with Q_i = Phat_{i+1} (I - Gam_i Phat_{i+1})^-1, formed through the
-            // factor C_i C_i' = -Gam_i as Q_i = Phat - Y Y', Y = Phat C_i R^-T, R R' = K = I + C_i' Phat C_i (K >= I:
-            // Cholesky without pivoting), forward from s_0 = 0. Lane NU + r holds row r of every matrix and element r
+            // factors L L' = Phat_{i+1} and C_i C_i' = -Gam_i as Q_i = Y Y', Y = L R^-T, R R' = K = I + L' C_i C_i' L
+            // (K >= I: Cholesky without pivoting), forward from s_0 = 0. Lane NU + r holds row r of every matrix and element r
             // of every vector (the fused-DPP blocks of team_asm_gen.hpp); segment data come from LDS
             if (tid < 16 && Sg > 1) {
                 const double* const sP = reinterpret_cast<const double*>(seg_lds + SegL.SUM_P);
@@ -881,6 +880,7 @@ __global__ __launch_bounds__(64 * W, 1) void k_sqp_rti_rowpar(KParams P, KArgs a
                 double* const sQ = reinterpret_cast<double*>(seg_lds + SegL.QS);
                 double* const sCv = reinterpret_cast<double*>(seg_lds + SegL.CS);
                 double* const sPh = reinterpret_cast<double*>(seg_lds + SegL.PHS);
+                double* const sLt = reinterpret_cast<double*>(seg_lds + SegL.LT);
                 auto ldrow = [&](int i, int off, double (&v)[NX]) {  // row xi of segment i's fp32 matrix at off
 #pragma unroll
                     for (int c = 0; c < NX; c++) v[c] = (double)seg_lds[off + (i * NX + xi) * NX + c];
@@ -890,35 +890,43 @@ __global__ __launch_bounds__(64 * W, 1) void k_sqp_rti_rowpar(KParams P, KArgs a
                 for (int c = 0; c < NX; c++) Ph[c] = sP[((size_t)(Sg - 1) * NX + xi) * NX + c];
                 ph = (double)seg_lds[SegL.SUM_PB + (Sg - 1) * NX + xi];
                 for (int i = Sg - 2; i >= 0; i--) {
-                    double Cr[NX], Cc[NX], Fr[NX], Gr[NX];
+                    double Cr[NX], Fr[NX], Gr[NX];
 #pragma unroll
-                    for (int c = 0; c < NX; c++) {
-                        Cr[c] = sC[((size_t)i * NX + xi) * NX + c];
-                        Cc[c] = sC[((size_t)i * NX + c) * NX + xi];
-                    }
+                    for (int c = 0; c < NX; c++) Cr[c] = sC[((size_t)i * NX + xi) * NX + c];
                     ldrow(i, SegL.SUM_PHI, Fr);
                     ldrow(i, SegL.SUM_GAM, Gr);
                     const double ti = (double)seg_lds[SegL.SUM_T + i * NX + xi];
-                    double U[NX], K[NX], rdv[NX];
+                    // L L' = Phat (non-positive pivots dropped), L' through the LDS scratch
+                    double Lp[NX], Lt[NX], V[NX], K[NX], rdv[NX];
+#pragma unroll
+                    for (int c = 0; c < NX; c++) Lp[c] = Ph[c];
+                    rowchol<NX, NU, true>(Lp, rdv, xi, 0.0);
+                    if (is_x) {
+#pragma unroll
+                        for (int c = 0; c < NX; c++) sLt[xi * NX + c] = Lp[c];
+                    }
+                    lds_fence();
 #pragma unroll
                     for (int c = 0; c < NX; c++) {
-                        U[c] = 0.0;
+                        Lt[c] = sLt[c * NX + xi];
+                        V[c] = 0.0;
                         K[c] = (xi == c) ? 1.0 : 0.0;
                     }
-                    mst_rowmul<NX, NU>(U, Ph, Cr);  // U = Phat C
-                    mst_rowmul<NX, NU>(K, Cc, U);   // K = I + C' U
+                    mst_rowmul<NX, NU>(V, Lt, Cr);  // V = L' C
+                    mst_rowdot<NX, NU>(K, V, V);    // K = I + V V' = I + L' G L
                     rowchol<NX, NU, false>(K, rdv, xi, 0.5);
-                    // Y = U R^-T (row-wise forward substitution), in place of U
+                    // Y = L R^-T (row-wise forward substitution), in place of Lp; Q = Y Y' (positive semidefinite
+                    // by construction: Phat - Phat C K^-1 C' Phat cancels when G Phat >> 1)
                     sfor<0, NX>([&](auto jc) {
                         constexpr int j = decltype(jc)::value;
-                        const double y = U[j] * rdv[j];
-                        U[j] = y;
-                        if constexpr (j + 1 < NX) mst_trsv<NX, NU, j>(U, K[j], y);
+                        const double y = Lp[j] * rdv[j];
+                        Lp[j] = y;
+                        if constexpr (j + 1 < NX) mst_trsv<NX, NU, j>(Lp, K[j], y);
                     });
                     double Q[NX];
 #pragma unroll
-                    for (int c = 0; c < NX; c++) Q[c] = Ph[c];
-                    mst_rowdot_neg<NX, NU>(Q, U, U);  // Q = Phat - Y Y'
+                    for (int c = 0; c < NX; c++) Q[c] = 0.0;
+                    mst_rowdot<NX, NU>(Q, Lp, Lp);
                     const double cv = mst_vdot<NX, NU>(ti, ph, Gr);  // c_i = t_i + Gam_i phat_{i+1}
                     if (is_x) {
 #pragma unroll

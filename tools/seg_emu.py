@@ -167,6 +167,10 @@ def psd_chol(A, thr, drop=True):
     return np.tril(L)
 
 
+GTHR = 0.0
+SUBTRACT = False  # Q = Phat - (Phat C R^-T)(...)' (cancels when G Phat >> 1) instead of (L R^-T)(L R^-T)'
+
+
 def master_chol(segs, nx):
     """The device master (sqp_rti_rowpar.hip SEG): Q_i = Phat - Y Y', Y = Phat C R^-T, C C' = -Gam_i,
     R R' = I + C' Phat C; forward lam_{i+1} = Q_i (Phi' s_i + c_i) + phat_{i+1}, s_{i+1} = Phi' s_i + Gam lam + t."""
@@ -176,11 +180,18 @@ def master_chol(segs, nx):
     for i in range(S - 2, -1, -1):
         sg = segs[i]
         G = -sg["Gam"]
-        C = psd_chol(G, 1e-10 * max(G.diagonal().max(), 1e-30))
-        U = Ph @ C
-        R = psd_chol(np.eye(nx) + C.T @ U, 0.5, drop=False)
-        Y = np.linalg.solve(R, U.T).T
-        Q = Ph - Y @ Y.T
+        C = psd_chol(G, GTHR * max(G.diagonal().max(), 1e-30))
+        if SUBTRACT:
+            U = Ph @ C
+            R = psd_chol(np.eye(nx) + C.T @ U, 0.5, drop=False)
+            Y = np.linalg.solve(R, U.T).T
+            Q = Ph - Y @ Y.T
+        else:
+            Lp = psd_chol(Ph, 0.0)
+            Vt = Lp.T @ C
+            R = psd_chol(np.eye(nx) + Vt @ Vt.T, 0.5, drop=False)
+            Y = np.linalg.solve(R, Lp.T).T
+            Q = Y @ Y.T
         c = sg["t"] + sg["Gam"] @ ph
         Qs[i], cs[i], phs[i] = Q, c, ph
         if i >= 1:

@@ -1,6 +1,6 @@
 // ubench_master.hip -- unit check of the segmented-Riccati master's fused-DPP blocks (team_asm_gen.hpp mst_*,
 // team_common.hpp rowchol) on one 16-lane row against a host fp64 reference: C = chol(G) of a positive
-// semidefinite G (dropped pivots), Q = Phat (I + G Phat)^-1 through Y = Phat C R^-T (R R' = I + C' Phat C),
+// semidefinite G (dropped pivots), Q = Phat (I + G Phat)^-1 as Y Y', Y = L R^-T (L L' = Phat, R R' = I + L' C C' L),
 // Phat' = Phat + F Q F', the vector blocks c = t + (-G) phat and w = phat + Q c. Prints one JSON line per case.
 // build: make -C nmpc_nav_control_amd/csrc ubench_master   run: build/ubench_master
 #include <hip/hip_runtime.h>
@@ -31,37 +31,44 @@ __global__ void k_master(const double* Ph, const double* G, const double* F, con
         Fr[c] = F[xi * NX + c];
         Gn[c] = -G[xi * NX + c];
     }
-    rowchol<NX, NU, true>(Cr, rdv, xi, thr);
+    rowchol<NX, NU, true>(Cr, rdv, xi, 0.0);
     if (is_x)
         for (int c = 0; c < NX; c++) {
             sC[xi * NX + c] = Cr[c];
             oC[xi * NX + c] = Cr[c];
         }
     __syncthreads();
-    double Cc[NX], U[NX], K[NX];
+    __shared__ double sL[NX * NX];
+    double Lp[NX], Lt[NX], V[NX], K[NX];
+#pragma unroll
+    for (int c = 0; c < NX; c++) Lp[c] = Phr[c];
+    rowchol<NX, NU, true>(Lp, rdv, xi, 0.0);
+    if (is_x)
+        for (int c = 0; c < NX; c++) sL[xi * NX + c] = Lp[c];
+    __syncthreads();
 #pragma unroll
     for (int c = 0; c < NX; c++) {
-        Cc[c] = sC[c * NX + xi];
-        U[c] = 0.0;
+        Lt[c] = sL[c * NX + xi];
+        V[c] = 0.0;
         K[c] = (xi == c) ? 1.0 : 0.0;
     }
-    mst_rowmul<NX, NU>(U, Phr, Cr);
-    mst_rowmul<NX, NU>(K, Cc, U);
+    mst_rowmul<NX, NU>(V, Lt, Cr);
+    mst_rowdot<NX, NU>(K, V, V);
     rowchol<NX, NU, false>(K, rdv, xi, 0.5);
     sfor<0, NX>([&](auto jc) {
         constexpr int j = decltype(jc)::value;
-        const double y = U[j] * rdv[j];
-        U[j] = y;
-        if constexpr (j + 1 < NX) mst_trsv<NX, NU, j>(U, K[j], y);
+        const double y = Lp[j] * rdv[j];
+        Lp[j] = y;
+        if constexpr (j + 1 < NX) mst_trsv<NX, NU, j>(Lp, K[j], y);
     });
     double Q[NX], T[NX], Pn[NX];
 #pragma unroll
     for (int c = 0; c < NX; c++) {
-        Q[c] = Phr[c];
+        Q[c] = 0.0;
         T[c] = 0.0;
         Pn[c] = Phr[c];
     }
-    mst_rowdot_neg<NX, NU>(Q, U, U);
+    mst_rowdot<NX, NU>(Q, Lp, Lp);
     mst_rowdot<NX, NU>(T, Q, Fr);
     mst_rowmul<NX, NU>(Pn, Fr, T);
     const double cv = mst_vdot<NX, NU>(vt[xi], vp[xi], Gn);
