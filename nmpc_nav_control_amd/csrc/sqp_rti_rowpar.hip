@@ -890,11 +890,13 @@ __global__ __launch_bounds__(64 * W, 1) void k_sqp_rti_rowpar(KParams P, KArgs a
                 for (int c = 0; c < NX; c++) Ph[c] = sP[((size_t)(Sg - 1) * NX + xi) * NX + c];
                 ph = (double)seg_lds[SegL.SUM_PB + (Sg - 1) * NX + xi];
                 for (int i = Sg - 2; i >= 0; i--) {
-                    double Cr[NX], Fr[NX], Gr[NX];
+                    double Cr[NX], Cc[NX], Fr[NX];
 #pragma unroll
-                    for (int c = 0; c < NX; c++) Cr[c] = sC[((size_t)i * NX + xi) * NX + c];
+                    for (int c = 0; c < NX; c++) {
+                        Cr[c] = sC[((size_t)i * NX + xi) * NX + c];
+                        Cc[c] = sC[((size_t)i * NX + c) * NX + xi];
+                    }
                     ldrow(i, SegL.SUM_PHI, Fr);
-                    ldrow(i, SegL.SUM_GAM, Gr);
                     const double ti = (double)seg_lds[SegL.SUM_T + i * NX + xi];
                     // L L' = Phat (non-positive pivots dropped), L' through the LDS scratch
                     double Lp[NX], Lt[NX], V[NX], K[NX], rdv[NX];
@@ -927,7 +929,11 @@ __global__ __launch_bounds__(64 * W, 1) void k_sqp_rti_rowpar(KParams P, KArgs a
 #pragma unroll
                     for (int c = 0; c < NX; c++) Q[c] = 0.0;
                     mst_rowdot<NX, NU>(Q, Lp, Lp);
-                    const double cv = mst_vdot<NX, NU>(ti, ph, Gr);  // c_i = t_i + Gam_i phat_{i+1}
+                    // c_i = t_i + Gam_i phat_{i+1} with Gam_i = -C C' (the factor's Gam, as in Q_i: Q_i from C C' with
+                    // the fp32 Gam elsewhere left the boundary equations inconsistent and the IPM stalled on pinned
+                    // robots, tools/seg_case_study.py)
+                    const double cg = mst_vdot<NX, NU>(0.0, ph, Cc);
+                    const double cv = ti - mst_vdot<NX, NU>(0.0, cg, Cr);
                     if (is_x) {
 #pragma unroll
                         for (int c = 0; c < NX; c++) sQ[((size_t)i * NX + xi) * NX + c] = Q[c];
@@ -949,21 +955,23 @@ __global__ __launch_bounds__(64 * W, 1) void k_sqp_rti_rowpar(KParams P, KArgs a
                     }
                 }
                 lds_fence();  // (Q_i, c_i, phat_{i+1} of every lane stored)
-                // forward: s_0 = 0; lam_{i+1} = Q_i (Phi_i' s_i + c_i) + phat_{i+1}; s_{i+1} = Phi_i' s_i + Gam_i lam_{i+1} + t_i
+                // forward: s_0 = 0; lam_{i+1} = Q_i (Phi_i' s_i + c_i) + phat_{i+1}; s_{i+1} = Phi_i' s_i - C C' lam_{i+1} + t_i
                 double sv = 0.0;
                 float* const sl = seg_lds + SegL.SL;
                 for (int i = 0; i <= Sg - 2; i++) {
-                    double Fc[NX], Gr[NX], Qr[NX];
+                    double Fc[NX], Cr[NX], Cc[NX], Qr[NX];
 #pragma unroll
                     for (int l = 0; l < NX; l++) {
                         Fc[l] = (double)seg_lds[SegL.SUM_PHI + (i * NX + l) * NX + xi];
                         Qr[l] = sQ[((size_t)i * NX + xi) * NX + l];
+                        Cr[l] = sC[((size_t)i * NX + xi) * NX + l];
+                        Cc[l] = sC[((size_t)i * NX + l) * NX + xi];
                     }
-                    ldrow(i, SegL.SUM_GAM, Gr);
                     const double fs = mst_vdot<NX, NU>(0.0, sv, Fc);
                     const double v = fs + sCv[i * NX + xi];
                     const double lam = mst_vdot<NX, NU>(sPh[i * NX + xi], v, Qr);
-                    sv = mst_vdot<NX, NU>(fs + (double)seg_lds[SegL.SUM_T + i * NX + xi], lam, Gr);
+                    const double cl = mst_vdot<NX, NU>(0.0, lam, Cc);
+                    sv = fs + (double)seg_lds[SegL.SUM_T + i * NX + xi] - mst_vdot<NX, NU>(0.0, cl, Cr);
                     if (is_x) {
                         sl[(i + 1) * 2 * NX + xi] = (float)sv;
                         sl[(i + 1) * 2 * NX + NX + xi] = (float)lam;

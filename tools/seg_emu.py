@@ -181,6 +181,7 @@ def master_chol(segs, nx):
         sg = segs[i]
         G = -sg["Gam"]
         C = psd_chol(G, GTHR * max(G.diagonal().max(), 1e-30))
+        sg["Gam"] = -(C @ C.T)  # the factor's Gam in c and the forward too (as the device)
         if SUBTRACT:
             U = Ph @ C
             R = psd_chol(np.eye(nx) + C.T @ U, 0.5, drop=False)

@@ -22,8 +22,27 @@ def f32(a, on):
     return a.astype(np.float32).astype(np.float64) if on else a
 
 
-def seg_riccati(emu, sig, ghat, S, sens32=True):
-    """Batched segmented solve of emu's Newton system (segments [qL, (q+1)L), the last one through N)."""
+def psd_chol_b(A, drop=True, thr=0.0):
+    """Batched row-distributed right-looking Cholesky of the device (team_common.hpp rowchol): pivots <= thr drop
+    their column (drop) or give NaN."""
+    L = A.copy()
+    n = A.shape[-1]
+    for j in range(n):
+        p = L[:, j, j].copy()
+        ok = p > thr
+        rd = np.where(ok, 1.0 / np.sqrt(np.where(ok, p, 1.0)), 0.0 if drop else np.nan)
+        L[:, j:, j] *= rd[:, None]
+        L[:, :j, j] = 0.0
+        for jp in range(j + 1, n):
+            L[:, jp:, jp] -= L[:, jp:, j] * L[:, jp, j][:, None]
+    return np.tril(L)
+
+
+def seg_riccati(emu, sig, ghat, S, sens32=True, master="gj"):
+    """Batched segmented solve of emu's Newton system (segments [qL, (q+1)L), the last one through N).
+    master: "gj" (Q = Phat X^-1 by a pivoted solve), "chol" (the device: Q = (L R^-T)(L R^-T)', L L' = Phat,
+    R R' = I + L' C C' L, C C' = -Gam with dropped non-positive pivots; forward with Gam), "cholcc" (the same with
+    C C' in place of Gam everywhere)."""
     Q, N, nx, nu = emu.Q, emu.N, emu.nx, emu.nu
     Bn = emu.B
     D = emu.H + sig
@@ -68,8 +87,18 @@ def seg_riccati(emu, sig, ghat, S, sens32=True):
     eye = np.broadcast_to(np.eye(nx), (Bn, nx, nx))
     for i in range(S - 2, -1, -1):
         sg = segs[i]
-        X = eye - sg["Gam"] @ Ph
-        Qm = np.linalg.solve(X.transpose(0, 2, 1), Ph)  # X^-T Phat (= Phat X^-1, symmetric)
+        if master == "gj":
+            X = eye - sg["Gam"] @ Ph
+            Qm = np.linalg.solve(X.transpose(0, 2, 1), Ph)  # X^-T Phat (= Phat X^-1, symmetric)
+        else:
+            C = psd_chol_b(-sg["Gam"])
+            if master == "cholcc":
+                sg["Gam"] = -(C @ C.transpose(0, 2, 1))
+            Lp = psd_chol_b(Ph)
+            V = Lp.transpose(0, 2, 1) @ C
+            R = psd_chol_b(eye + V @ V.transpose(0, 2, 1), drop=False, thr=0.5)
+            Y = np.linalg.solve(R, Lp.transpose(0, 2, 1)).transpose(0, 2, 1)
+            Qm = Y @ Y.transpose(0, 2, 1)
         c = sg["t"] + np.einsum("bij,bj->bi", sg["Gam"], ph)
         Qs[i], cs[i], phs[i] = Qm, c, ph
         if i >= 1:
