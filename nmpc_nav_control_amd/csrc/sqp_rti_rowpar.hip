@@ -45,19 +45,17 @@ struct RowRec {
 };
 
 // LDS of the segmented phases (SEG, a.seg = S > 0), in floats from its base (8-byte aligned; fp64 parts at even
-// offsets). Per segment q: the entry quantities of its backward sweep -- P (fp64 rows), the factor C_q of -Gam_q
-// (fp64 rows), pbar, Phi, Gam, t; per master step i: Q_i (fp64), c_i, phat_{i+1}; a transpose scratch; the
+// offsets). Per segment q: the entry quantities of its backward sweep -- P (fp64 rows), pbar, Phi, Gam, t; per master step i: Q_i (fp64), c_i, phat_{i+1}; a transpose scratch; the
 // boundary states s_q and
 // costates lam_q; the lam-sensitivity Z of every stage's LR (rows of the NU input lanes).
 template <class M>
 struct SegLayout {
     static constexpr int NX = M::NX, NU = M::NU, NXP = (M::NX + 3) / 4 * 4;
-    int SUM_P, SUM_C, SUM_PB, SUM_PHI, SUM_GAM, SUM_T, QS, CS, PHS, LT, SL, ZL;
+    int SUM_P, SUM_PB, SUM_PHI, SUM_GAM, SUM_T, QS, CS, PHS, LT, SL, ZL;
     __host__ __device__ explicit SegLayout(int S)
     {
         SUM_P = 0;                          // [S][NX][NX] double
-        SUM_C = SUM_P + 2 * S * NX * NX;    // [S][NX][NX] double (lower triangular)
-        SUM_PB = SUM_C + 2 * S * NX * NX;   // [S][NX]
+        SUM_PB = SUM_P + 2 * S * NX * NX;   // [S][NX]
         SUM_PHI = SUM_PB + S * NX;          // [S][NX][NX]
         SUM_GAM = SUM_PHI + S * NX * NX;    // [S][NX][NX]
         SUM_T = SUM_GAM + S * NX * NX;      // [S][NX]
@@ -835,22 +833,6 @@ __global__ __launch_bounds__(64 * W, 1) void k_sqp_rti_rowpar(KParams P, KArgs a
                         seg_lds[SegL.SUM_GAM + (q * NX + xi) * NX + c] = Gam[c];
                     }
                 }
-                // C_q C_q' = -Gam_q (= sum of Z'Z over the segment, positive semidefinite), every row but the
-                // last at once, off the master's serial chain; non-positive pivots (fp32 rounding of a
-                // rank-deficient sum) drop their column (tools/seg_emu.py --chol-master: any positive drop
-                // threshold costs accuracy on pinned QPs)
-                if (srow && !slast) {
-                    double Cr[NX], rdv[NX];
-#pragma unroll
-                    for (int c = 0; c < NX; c++) Cr[c] = is_x ? -(double)Gam[c] : 0.0;
-                    const double thr = 0.0;
-                    rowchol<NX, NU, true>(Cr, rdv, xi, thr);
-                    if (is_x) {
-                        double* const cp = reinterpret_cast<double*>(seg_lds + SegL.SUM_C) + ((size_t)q * NX + xi) * NX;
-#pragma unroll
-                        for (int c = 0; c < NX; c++) cp[c] = Cr[c];
-                    }
-                }
             }
             {
                 float v[6] = {wave_max_rows(row_max16(fail ? 1.0f : 0.0f)), wave_max_rows(row_max16(nanb)), 0.0f,
@@ -871,12 +853,11 @@ __global__ __launch_bounds__(64 * W, 1) void k_sqp_rti_rowpar(KParams P, KArgs a
             // ---- master (row 0 of wave 0, fp64): the two-point recursion over the segment boundaries,
             //   s_{i+1} = Phi_i' s_i + Gam_i lam_{i+1} + t_i,   lam_i = P_i s_i + pbar_i + Phi_i lam_{i+1},
             // backward lam_i = Phat_i s_i + phat_i with Q_i = Phat_{i+1} (I - Gam_i Phat_{i+1})^-1, formed through the
-            // factors L L' = Phat_{i+1} and C_i C_i' = -Gam_i as Q_i = Y Y', Y = L R^-T, R R' = K = I + L' C_i C_i' L
-            // (K >= I: Cholesky without pivoting), forward from s_0 = 0. Lane NU + r holds row r of every matrix and element r
+            // factor L L' = Phat_{i+1} as Q_i = Y Y', Y = L R^-T, R R' = K = I - L' Gam_i L (K >= I: Cholesky without
+            // pivoting; Q_i positive semidefinite by construction), forward from s_0 = 0. Lane NU + r holds row r of every matrix and element r
             // of every vector (the fused-DPP blocks of team_asm_gen.hpp); segment data come from LDS
             if (tid < 16 && Sg > 1) {
                 const double* const sP = reinterpret_cast<const double*>(seg_lds + SegL.SUM_P);
-                const double* const sC = reinterpret_cast<const double*>(seg_lds + SegL.SUM_C);
                 double* const sQ = reinterpret_cast<double*>(seg_lds + SegL.QS);
                 double* const sCv = reinterpret_cast<double*>(seg_lds + SegL.CS);
                 double* const sPh = reinterpret_cast<double*>(seg_lds + SegL.PHS);
@@ -890,19 +871,17 @@ __global__ __launch_bounds__(64 * W, 1) void k_sqp_rti_rowpar(KParams P, KArgs a
                 for (int c = 0; c < NX; c++) Ph[c] = sP[((size_t)(Sg - 1) * NX + xi) * NX + c];
                 ph = (double)seg_lds[SegL.SUM_PB + (Sg - 1) * NX + xi];
                 for (int i = Sg - 2; i >= 0; i--) {
-                    double Cr[NX], Cc[NX], Fr[NX];
-#pragma unroll
-                    for (int c = 0; c < NX; c++) {
-                        Cr[c] = sC[((size_t)i * NX + xi) * NX + c];
-                        Cc[c] = sC[((size_t)i * NX + c) * NX + xi];
-                    }
+                    double Fr[NX], Gr[NX], Gn[NX];
                     ldrow(i, SegL.SUM_PHI, Fr);
+                    ldrow(i, SegL.SUM_GAM, Gr);
+#pragma unroll
+                    for (int c = 0; c < NX; c++) Gn[c] = -Gr[c];
                     const double ti = (double)seg_lds[SegL.SUM_T + i * NX + xi];
-                    // L L' = Phat (non-positive pivots dropped), L' through the LDS scratch
+                    // L L' = Phat (pivots below 1e-13 of their diagonal entry dropped), L' through the LDS scratch
                     double Lp[NX], Lt[NX], V[NX], K[NX], rdv[NX];
 #pragma unroll
                     for (int c = 0; c < NX; c++) Lp[c] = Ph[c];
-                    rowchol<NX, NU, true>(Lp, rdv, xi, 0.0);
+                    rowchol<NX, NU, true>(Lp, rdv, xi, 0.0, 1e-13);
                     if (is_x) {
 #pragma unroll
                         for (int c = 0; c < NX; c++) sLt[xi * NX + c] = Lp[c];
@@ -914,11 +893,12 @@ __global__ __launch_bounds__(64 * W, 1) void k_sqp_rti_rowpar(KParams P, KArgs a
                         V[c] = 0.0;
                         K[c] = (xi == c) ? 1.0 : 0.0;
                     }
-                    mst_rowmul<NX, NU>(V, Lt, Cr);  // V = L' C
-                    mst_rowdot<NX, NU>(K, V, V);    // K = I + V V' = I + L' G L
+                    mst_rowmul<NX, NU>(V, Gn, Lp);  // V = -Gam L
+                    mst_rowmul<NX, NU>(K, Lt, V);   // K = I + L' V = I - L' Gam L
                     rowchol<NX, NU, false>(K, rdv, xi, 0.5);
-                    // Y = L R^-T (row-wise forward substitution), in place of Lp; Q = Y Y' (positive semidefinite
-                    // by construction: Phat - Phat C K^-1 C' Phat cancels when G Phat >> 1)
+                    // Y = L R^-T (row-wise forward substitution), in place of Lp; Q = Y Y' (positive semidefinite by
+                    // construction; the Woodbury form Phat - Phat C K^-1 C' Phat cancels when -Gam Phat >> 1, and a
+                    // factor of -Gam itself, a nearly singular fp32 sum, blew up: tools/seg_case_study.py)
                     sfor<0, NX>([&](auto jc) {
                         constexpr int j = decltype(jc)::value;
                         const double y = Lp[j] * rdv[j];
@@ -929,11 +909,7 @@ __global__ __launch_bounds__(64 * W, 1) void k_sqp_rti_rowpar(KParams P, KArgs a
 #pragma unroll
                     for (int c = 0; c < NX; c++) Q[c] = 0.0;
                     mst_rowdot<NX, NU>(Q, Lp, Lp);
-                    // c_i = t_i + Gam_i phat_{i+1} with Gam_i = -C C' (the factor's Gam, as in Q_i: Q_i from C C' with
-                    // the fp32 Gam elsewhere left the boundary equations inconsistent and the IPM stalled on pinned
-                    // robots, tools/seg_case_study.py)
-                    const double cg = mst_vdot<NX, NU>(0.0, ph, Cc);
-                    const double cv = ti - mst_vdot<NX, NU>(0.0, cg, Cr);
+                    const double cv = mst_vdot<NX, NU>(ti, ph, Gr);  // c_i = t_i + Gam_i phat_{i+1}
                     if (is_x) {
 #pragma unroll
                         for (int c = 0; c < NX; c++) sQ[((size_t)i * NX + xi) * NX + c] = Q[c];
@@ -955,23 +931,21 @@ __global__ __launch_bounds__(64 * W, 1) void k_sqp_rti_rowpar(KParams P, KArgs a
                     }
                 }
                 lds_fence();  // (Q_i, c_i, phat_{i+1} of every lane stored)
-                // forward: s_0 = 0; lam_{i+1} = Q_i (Phi_i' s_i + c_i) + phat_{i+1}; s_{i+1} = Phi_i' s_i - C C' lam_{i+1} + t_i
+                // forward: s_0 = 0; lam_{i+1} = Q_i (Phi_i' s_i + c_i) + phat_{i+1}; s_{i+1} = Phi_i' s_i + Gam_i lam_{i+1} + t_i
                 double sv = 0.0;
                 float* const sl = seg_lds + SegL.SL;
                 for (int i = 0; i <= Sg - 2; i++) {
-                    double Fc[NX], Cr[NX], Cc[NX], Qr[NX];
+                    double Fc[NX], Gr[NX], Qr[NX];
 #pragma unroll
                     for (int l = 0; l < NX; l++) {
                         Fc[l] = (double)seg_lds[SegL.SUM_PHI + (i * NX + l) * NX + xi];
                         Qr[l] = sQ[((size_t)i * NX + xi) * NX + l];
-                        Cr[l] = sC[((size_t)i * NX + xi) * NX + l];
-                        Cc[l] = sC[((size_t)i * NX + l) * NX + xi];
                     }
+                    ldrow(i, SegL.SUM_GAM, Gr);
                     const double fs = mst_vdot<NX, NU>(0.0, sv, Fc);
                     const double v = fs + sCv[i * NX + xi];
                     const double lam = mst_vdot<NX, NU>(sPh[i * NX + xi], v, Qr);
-                    const double cl = mst_vdot<NX, NU>(0.0, lam, Cc);
-                    sv = fs + (double)seg_lds[SegL.SUM_T + i * NX + xi] - mst_vdot<NX, NU>(0.0, cl, Cr);
+                    sv = mst_vdot<NX, NU>(fs + (double)seg_lds[SegL.SUM_T + i * NX + xi], lam, Gr);
                     if (is_x) {
                         sl[(i + 1) * 2 * NX + xi] = (float)sv;
                         sl[(i + 1) * 2 * NX + NX + xi] = (float)lam;

@@ -155,16 +155,23 @@ __device__ __forceinline__ double mst_vdot(double acc, double x, const double (&
 }
 
 // Right-looking Cholesky of the NX x NX matrix held row-wise on the state lanes of a 16-lane row (lane NU + i: row
-// i in lr, xi = i), in place: lane NU + i ends with row i of L. rdv[j] = 1 / L[j][j]. A pivot <= thr is dropped
-// (DROP: its column becomes zero, the factor of a positive semidefinite matrix) or poisons the factor with NaN
-// (!DROP: a breakdown the IPM's NaN test reports); a NaN pivot always propagates.
+// i in lr, xi = i), in place: lane NU + i ends with row i of L. rdv[j] = 1 / L[j][j]. A pivot <= thr, or (rel > 0)
+// <= rel x the column's original diagonal entry, is dropped (DROP: its column becomes zero, the factor of a
+// positive semidefinite matrix; the relative test keeps rounding-level pivots of a nearly singular matrix from
+// scaling their column by 1 / sqrt(noise)) or poisons the factor with NaN (!DROP: a breakdown the IPM's NaN test
+// reports); a NaN pivot always propagates.
 template <int NX, int NU, bool DROP>
-__device__ __forceinline__ void rowchol(double (&lr)[NX], double (&rdv)[NX], int xi, double thr)
+__device__ __forceinline__ void rowchol(double (&lr)[NX], double (&rdv)[NX], int xi, double thr, double rel = 0.0)
 {
+    double d0 = 0.0;
+#pragma unroll
+    for (int c = 0; c < NX; c++) d0 = (xi == c) ? lr[c] : d0;
+    d0 *= rel;
     double piv = bc64<NU>(lr[0]);
     sfor<0, NX>([&](auto jc) {
         constexpr int j = decltype(jc)::value;
-        const double rd = (piv > thr) ? drsq(piv) : ((DROP && piv == piv) ? 0.0 : __builtin_nan(""));
+        const double tj = fmax(thr, bc64<NU + j>(d0));
+        const double rd = (piv > tj) ? drsq(piv) : ((DROP && piv == piv) ? 0.0 : __builtin_nan(""));
         rdv[j] = rd;
         const double lj = (xi >= j) ? lr[j] * rd : 0.0;
         lr[j] = lj;

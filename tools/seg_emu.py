@@ -152,14 +152,15 @@ def master(segs, nx):
     return s, lam, Xs
 
 
-def psd_chol(A, thr, drop=True):
-    """Row-distributed right-looking Cholesky of the device (sqp_rti_rowpar.hip rowchol): pivots <= thr drop their
-    column (drop) or give NaN."""
+def psd_chol(A, thr, drop=True, rel=0.0):
+    """Row-distributed right-looking Cholesky of the device (team_common.hpp rowchol): pivots <= thr or <= rel x the
+    column's original diagonal entry drop their column (drop) or give NaN."""
     n = len(A)
     L = A.copy()
+    d0 = np.diag(A).copy()
     for j in range(n):
         p = L[j, j]
-        rd = 1.0 / np.sqrt(p) if p > thr else (0.0 if drop and p == p else np.nan)
+        rd = 1.0 / np.sqrt(p) if (p > thr and p > rel * d0[j]) else (0.0 if drop and p == p else np.nan)
         L[j:, j] *= rd
         L[:j, j] = 0.0
         for jp in range(j + 1, n):
@@ -167,32 +168,21 @@ def psd_chol(A, thr, drop=True):
     return np.tril(L)
 
 
-GTHR = 0.0
-SUBTRACT = False  # Q = Phat - (Phat C R^-T)(...)' (cancels when G Phat >> 1) instead of (L R^-T)(L R^-T)'
 
 
 def master_chol(segs, nx):
-    """The device master (sqp_rti_rowpar.hip SEG): Q_i = Phat - Y Y', Y = Phat C R^-T, C C' = -Gam_i,
-    R R' = I + C' Phat C; forward lam_{i+1} = Q_i (Phi' s_i + c_i) + phat_{i+1}, s_{i+1} = Phi' s_i + Gam lam + t."""
+    """The device master (sqp_rti_rowpar.hip SEG): Q_i = Y Y', Y = L R^-T, L L' = Phat_{i+1} (relative pivot
+    threshold 1e-13), R R' = I - L' Gam_i L; forward lam_{i+1} = Q_i (Phi' s_i + c_i) + phat_{i+1},
+    s_{i+1} = Phi' s_i + Gam lam + t."""
     S = len(segs)
     Ph, ph = segs[S - 1]["P"], segs[S - 1]["p"]
     Qs, cs, phs = [None] * S, [None] * S, [None] * S
     for i in range(S - 2, -1, -1):
         sg = segs[i]
-        G = -sg["Gam"]
-        C = psd_chol(G, GTHR * max(G.diagonal().max(), 1e-30))
-        sg["Gam"] = -(C @ C.T)  # the factor's Gam in c and the forward too (as the device)
-        if SUBTRACT:
-            U = Ph @ C
-            R = psd_chol(np.eye(nx) + C.T @ U, 0.5, drop=False)
-            Y = np.linalg.solve(R, U.T).T
-            Q = Ph - Y @ Y.T
-        else:
-            Lp = psd_chol(Ph, 0.0)
-            Vt = Lp.T @ C
-            R = psd_chol(np.eye(nx) + Vt @ Vt.T, 0.5, drop=False)
-            Y = np.linalg.solve(R, Lp.T).T
-            Q = Y @ Y.T
+        Lp = psd_chol(Ph, 0.0, rel=1e-13)
+        R = psd_chol(np.eye(nx) - Lp.T @ sg["Gam"] @ Lp, 0.5, drop=False)
+        Y = np.linalg.solve(R, Lp.T).T
+        Q = Y @ Y.T
         c = sg["t"] + sg["Gam"] @ ph
         Qs[i], cs[i], phs[i] = Q, c, ph
         if i >= 1:

@@ -22,14 +22,15 @@ def f32(a, on):
     return a.astype(np.float32).astype(np.float64) if on else a
 
 
-def psd_chol_b(A, drop=True, thr=0.0):
-    """Batched row-distributed right-looking Cholesky of the device (team_common.hpp rowchol): pivots <= thr drop
-    their column (drop) or give NaN."""
+def psd_chol_b(A, drop=True, thr=0.0, rel=0.0):
+    """Batched row-distributed right-looking Cholesky of the device (team_common.hpp rowchol): pivots <= thr (or
+    <= rel x the column's original diagonal entry) drop their column (drop) or give NaN."""
     L = A.copy()
     n = A.shape[-1]
+    d0 = np.diagonal(A, axis1=1, axis2=2).copy()
     for j in range(n):
         p = L[:, j, j].copy()
-        ok = p > thr
+        ok = (p > thr) & (p > rel * d0[:, j])
         rd = np.where(ok, 1.0 / np.sqrt(np.where(ok, p, 1.0)), 0.0 if drop else np.nan)
         L[:, j:, j] *= rd[:, None]
         L[:, :j, j] = 0.0
@@ -42,7 +43,8 @@ def seg_riccati(emu, sig, ghat, S, sens32=True, master="gj"):
     """Batched segmented solve of emu's Newton system (segments [qL, (q+1)L), the last one through N).
     master: "gj" (Q = Phat X^-1 by a pivoted solve), "chol" (the device: Q = (L R^-T)(L R^-T)', L L' = Phat,
     R R' = I + L' C C' L, C C' = -Gam with dropped non-positive pivots; forward with Gam), "cholcc" (the same with
-    C C' in place of Gam everywhere)."""
+    C C' in place of Gam everywhere), "cholg" (Q = (L R^-T)(L R^-T)', R R' = I - L' Gam L: no factor of Gam, whose
+    semidefinite Cholesky blows up on nearly singular fp32 sums)."""
     Q, N, nx, nu = emu.Q, emu.N, emu.nx, emu.nu
     Bn = emu.B
     D = emu.H + sig
@@ -90,6 +92,12 @@ def seg_riccati(emu, sig, ghat, S, sens32=True, master="gj"):
         if master == "gj":
             X = eye - sg["Gam"] @ Ph
             Qm = np.linalg.solve(X.transpose(0, 2, 1), Ph)  # X^-T Phat (= Phat X^-1, symmetric)
+        elif master == "cholg":
+            Lp = psd_chol_b(Ph, rel=1e-13)
+            K = eye + Lp.transpose(0, 2, 1) @ (-sg["Gam"]) @ Lp
+            R = psd_chol_b(K, drop=False, thr=0.5)
+            Y = np.linalg.solve(R, Lp.transpose(0, 2, 1)).transpose(0, 2, 1)
+            Qm = Y @ Y.transpose(0, 2, 1)
         else:
             C = psd_chol_b(-sg["Gam"])
             if master == "cholcc":

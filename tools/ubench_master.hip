@@ -1,6 +1,6 @@
 // ubench_master.hip -- unit check of the segmented-Riccati master's fused-DPP blocks (team_asm_gen.hpp mst_*,
-// team_common.hpp rowchol) on one 16-lane row against a host fp64 reference: C = chol(G) of a positive
-// semidefinite G (dropped pivots), Q = Phat (I + G Phat)^-1 as Y Y', Y = L R^-T (L L' = Phat, R R' = I + L' C C' L),
+// team_common.hpp rowchol) on one 16-lane row against a host fp64 reference: for a positive semidefinite G (= -Gam,
+// full rank, rank 3 and zero), Q = Phat (I + G Phat)^-1 as Y Y', Y = L R^-T (L L' = Phat, R R' = I + L' G L),
 // Phat' = Phat + F Q F', the vector blocks c = t + (-G) phat and w = phat + Q c. Prints one JSON line per case.
 // build: make -C nmpc_nav_control_amd/csrc ubench_master   run: build/ubench_master
 #include <hip/hip_runtime.h>
@@ -17,43 +17,34 @@ using namespace nmpc;
 constexpr int NX = 7, NU = 2;
 
 __global__ void k_master(const double* Ph, const double* G, const double* F, const double* vt, const double* vp,
-                         double thr, double* oC, double* oQ, double* oPn, double* oc, double* ow)
+                         double* oQ, double* oPn, double* oc, double* ow)
 {
-    __shared__ double sC[NX * NX];
+    __shared__ double sL[NX * NX];
     const int r = threadIdx.x & 15;
     const bool is_x = r >= NU && r < NU + NX;
     const int xi = is_x ? r - NU : 0;
-    double Phr[NX], Cr[NX], Fr[NX], Gn[NX], rdv[NX];
+    double Phr[NX], Lp[NX], Fr[NX], Gr[NX], Gn[NX], rdv[NX];
 #pragma unroll
     for (int c = 0; c < NX; c++) {
         Phr[c] = Ph[xi * NX + c];
-        Cr[c] = is_x ? G[xi * NX + c] : 0.0;
+        Lp[c] = Phr[c];
         Fr[c] = F[xi * NX + c];
-        Gn[c] = -G[xi * NX + c];
+        Gr[c] = G[xi * NX + c];  // -Gam
+        Gn[c] = -G[xi * NX + c];  // Gam
     }
-    rowchol<NX, NU, true>(Cr, rdv, xi, 0.0);
-    if (is_x)
-        for (int c = 0; c < NX; c++) {
-            sC[xi * NX + c] = Cr[c];
-            oC[xi * NX + c] = Cr[c];
-        }
-    __syncthreads();
-    __shared__ double sL[NX * NX];
-    double Lp[NX], Lt[NX], V[NX], K[NX];
-#pragma unroll
-    for (int c = 0; c < NX; c++) Lp[c] = Phr[c];
-    rowchol<NX, NU, true>(Lp, rdv, xi, 0.0);
+    rowchol<NX, NU, true>(Lp, rdv, xi, 0.0, 1e-13);
     if (is_x)
         for (int c = 0; c < NX; c++) sL[xi * NX + c] = Lp[c];
     __syncthreads();
+    double Lt[NX], V[NX], K[NX];
 #pragma unroll
     for (int c = 0; c < NX; c++) {
         Lt[c] = sL[c * NX + xi];
         V[c] = 0.0;
         K[c] = (xi == c) ? 1.0 : 0.0;
     }
-    mst_rowmul<NX, NU>(V, Lt, Cr);
-    mst_rowdot<NX, NU>(K, V, V);
+    mst_rowmul<NX, NU>(V, Gr, Lp);
+    mst_rowmul<NX, NU>(K, Lt, V);
     rowchol<NX, NU, false>(K, rdv, xi, 0.5);
     sfor<0, NX>([&](auto jc) {
         constexpr int j = decltype(jc)::value;
@@ -135,8 +126,6 @@ int main()
             }
         for (int i = 0; i < n; i++)
             for (int j = 0; j < i; j++) G[i * n + j] = G[j * n + i];
-        double dmax = 1e-30;
-        for (int i = 0; i < n; i++) dmax = std::fmax(dmax, G[i * n + i]);
         double *dPh, *dG, *dF, *dvt, *dvp, *dout;
         (void)hipMalloc(&dPh, nn * 8);
         (void)hipMalloc(&dG, nn * 8);
@@ -149,23 +138,15 @@ int main()
         (void)hipMemcpy(dF, F.data(), nn * 8, hipMemcpyHostToDevice);
         (void)hipMemcpy(dvt, vt.data(), n * 8, hipMemcpyHostToDevice);
         (void)hipMemcpy(dvp, vp.data(), n * 8, hipMemcpyHostToDevice);
-        hipLaunchKernelGGL(k_master, dim3(1), dim3(64), 0, nullptr, dPh, dG, dF, dvt, dvp, 1e-10 * dmax, dout,
-                           dout + nn, dout + 2 * nn, dout + 3 * nn, dout + 3 * nn + n);
+        hipLaunchKernelGGL(k_master, dim3(1), dim3(64), 0, nullptr, dPh, dG, dF, dvt, dvp, dout + nn, dout + 2 * nn,
+                           dout + 3 * nn, dout + 3 * nn + n);
         std::vector<double> out(3 * nn + 2 * n);
         if (hipMemcpy(out.data(), dout, out.size() * 8, hipMemcpyDeviceToHost) != hipSuccess) {
             std::fprintf(stderr, "hip error\n");
             return 2;
         }
         // reference: Q = Phat (I + G Phat)^-1 = ((I + G Phat)^-T Phat)^T; X' Q' = Phat with X = I + G Phat
-        // (with the device's own factor: G_eff = C C', so that the check isolates the blocks from the
-        // semidefinite projection of an fp32-rounded rank-deficient G; CCt_err reports that projection)
-        std::vector<double> Xt(nn), Qr(Ph), Ge(nn);
-        for (int i = 0; i < n; i++)
-            for (int j = 0; j < n; j++) {
-                double s = 0.0;
-                for (int l = 0; l < n; l++) s += out[i * n + l] * out[j * n + l];
-                Ge[i * n + j] = s;
-            }
+        std::vector<double> Xt(nn), Qr(Ph), Ge(G);
         for (int i = 0; i < n; i++)
             for (int j = 0; j < n; j++) {
                 double s = (i == j) ? 1.0 : 0.0;
@@ -173,7 +154,7 @@ int main()
                 Xt[i * n + j] = s;
             }
         solve(Xt, Qr, n);  // Qr = X^-T Ph = Q^T (= Q)
-        double eq = 0.0, mq = 0.0, ep = 0.0, mp = 0.0, ec = 0.0, ew = 0.0, ecc = 0.0;
+        double eq = 0.0, mq = 0.0, ep = 0.0, mp = 0.0, ec = 0.0, ew = 0.0;
         for (int i = 0; i < n; i++)
             for (int j = 0; j < n; j++) {
                 eq = std::fmax(eq, std::fabs(out[nn + i * n + j] - Qr[j * n + i]));
@@ -184,9 +165,6 @@ int main()
                 const double pn = Ph[i * n + j] + fqf;
                 ep = std::fmax(ep, std::fabs(out[2 * nn + i * n + j] - pn));
                 mp = std::fmax(mp, std::fabs(pn));
-                double cc = 0.0;
-                for (int l = 0; l < n; l++) cc += out[i * n + l] * out[j * n + l];
-                ecc = std::fmax(ecc, std::fabs(cc - G[i * n + j]) / dmax);
             }
         std::vector<double> cref(n);
         for (int i = 0; i < n; i++) {
@@ -200,11 +178,11 @@ int main()
             for (int l = 0; l < n; l++) s += Qr[i * n + l] * cref[l];
             ew = std::fmax(ew, std::fabs(out[3 * nn + n + i] - s) / (1.0 + std::fabs(s)));
         }
-        const bool ok = eq / mq < 1e-9 && ep / mp < 1e-9 && ec < 1e-9 && ew < 1e-6 && ecc < 1e-5;
+        const bool ok = eq / mq < 1e-9 && ep / mp < 1e-9 && ec < 1e-9 && ew < 1e-6 ;
         bad += !ok;
         std::printf("{\"case\": %d, \"rank_G\": %d, \"phat_scale\": %g, \"Q_rel_err\": %.3e, \"Pnext_rel_err\": %.3e, "
-                    "\"CCt_err\": %.3e, \"c_err\": %.3e, \"w_err\": %.3e, \"ok\": %s}\n",
-                    cs, rank, pscale, eq / mq, ep / mp, ecc, ec, ew, ok ? "true" : "false");
+                    "\"c_err\": %.3e, \"w_err\": %.3e, \"ok\": %s}\n",
+                    cs, rank, pscale, eq / mq, ep / mp, ec, ew, ok ? "true" : "false");
         (void)hipFree(dPh);
         (void)hipFree(dG);
         (void)hipFree(dF);
