@@ -27,12 +27,14 @@ struct nmpc_batch {
     int sched = NMPC_SCHED_AUTO;
     int n_simd = 1024;           // SIMDs of the device (4 per CU)
     int split_max = 256;         // team-kernel launches of at most this many robots run one block per robot (split)
-    // launches of at most this many robots (single-direction IPM, not run_path) run k_sqp_rti_rowpar: one wave
-    // per robot with its stage-independent work spread over the wave's 4 rows (latency)
-    int rowpar_max = 256;        // (four waves per robot up to 256 robots; one wave per robot above, A/B only)
+    // launches of at most this many robots (single-direction IPM, not run_path) run k_sqp_rti_rowpar (DESIGN.md
+    // section 4): four waves per robot up to 256 robots; one wave per robot above, and there only with segments
+    // (the serial phases at one wave per robot lose to the team kernel, the segmented ones win up to a robot per
+    // SIMD: diff N = 40 B = 1024 1.15 -> 1.57 M it/s, profiles/r04/ab/seg.txt)
+    int rowpar_max = 1024;
     // horizon segments of the row-parallel kernel (sqp_rti_rowpar.hip SEG): -1 = chosen per launch (seg_count),
     // 0 = the serial phases B / C, S > 0 = S segments when N % S == 0 (NMPC_AMD_SEG overrides)
-    int seg = 0;  // (default -1 once the segmented path is validated on the GPU)
+    int seg = -1;
     int* iter_key = nullptr;     // [capacity] last executed IPM iterations per robot (written by the team kernel)
     int* order = nullptr;        // [capacity] team slot -> robot
     unsigned char* warm = nullptr;  // [capacity] the robot's last solve succeeded: its scratch records hold its
@@ -133,15 +135,16 @@ hipError_t launch_m(nmpc_batch* b, const KArgs& a, int mode, hipStream_t s)
 }
 
 // Segments of the row-parallel kernel's Riccati sweeps for a horizon N on `rows` rows per robot: the divisor S of N
-// (S <= rows, <= kSegMax) that minimises the robot's chain, about N / S stage steps of the segments' sweeps plus
-// S - 1 master steps of ~2 stage steps each; 0 (the serial phases) when no S > 1 divides N
+// (S <= rows, <= kSegMax) that minimises the robot's chain per IPM iteration, N / S stage steps of the segments'
+// sweeps (backward 2.4 k + forward 1.2 k cycles) plus S - 1 master steps (5 k cycles, 1.4 stage steps; diag stamps,
+// profiles/r04/stamps/); 0 (the serial phases) when no S > 1 divides N. N = 80 -> 8, N = 40 -> 5 (4 on one wave)
 inline int seg_count(int N, int rows)
 {
     int best = 0;
     double cost = (double)N;
     for (int S = 2; S <= rows && S <= kSegMax; S++) {
         if (N % S) continue;
-        const double c = (double)N / S + 2.0 * (S - 1);
+        const double c = (double)N / S + 1.4 * (S - 1);
         if (c < cost) {
             cost = c;
             best = S;
@@ -158,6 +161,7 @@ bool rowpar_ok(const nmpc_batch* b, KArgs& a, int mode)
     int S = b->seg >= 0 ? b->seg : seg_count(b->prm.N, rows);
     if (S > rows || S > kSegMax || (S > 0 && b->prm.N % S)) S = 0;
     if (S > 0 && rowpar_lds_bytes<M>(b->prm.N, mode, S) > 65536) S = 0;
+    if (a.B > 256 && S == 0 && b->seg < 0) return false;  // one wave per robot only with segments (auto)
     a.seg = S;
     return rowpar_lds_bytes<M>(b->prm.N, mode, S) <= 65536;
 }

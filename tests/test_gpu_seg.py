@@ -110,10 +110,12 @@ def test_hybrid_launch_matches_plain(built, monkeypatch, model):
     nx, nu = o.nx, o.nu
     monkeypatch.setenv("NMPC_AMD_HYBRID", "8")
     monkeypatch.setenv("NMPC_AMD_SPLIT_MAX", "0")
+    monkeypatch.setenv("NMPC_AMD_ROWPAR_MAX", "0")  # the team kernel (600 robots would run the segmented kernel)
     hy = BatchSolver(model, N, B, params=default_params(model, N))
     monkeypatch.delenv("NMPC_AMD_HYBRID")
     pl = BatchSolver(model, N, B, params=default_params(model, N))
     monkeypatch.delenv("NMPC_AMD_SPLIT_MAX")
+    monkeypatch.delenv("NMPC_AMD_ROWPAR_MAX")
     x0 = t(np.stack([r[0] for r in rec]).T)
     yref = t(np.stack([r[1] for r in rec]).transpose(1, 2, 0))
     We = t(np.stack([r[2] for r in rec]).T)

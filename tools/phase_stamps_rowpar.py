@@ -33,15 +33,15 @@ buf = (ctypes.c_ulonglong * (256 * W))()
 L = lib()
 L.nmpc_debug_stamps_rowpar.argtypes = [ctypes.c_void_p]
 assert L.nmpc_debug_stamps_rowpar(buf) == 0
-st = np.frombuffer(buf, dtype=np.uint64).reshape(256, W).astype(np.int64)[:B]
-it = f.qp_iter.cpu().numpy()
+st = np.frombuffer(buf, dtype=np.uint64).reshape(256, W).astype(np.int64)[:min(B, 256)]  # robots 0..255 stamped
+it = f.qp_iter.cpu().numpy()[:min(B, 256)]
 print("kernel ms", ev0.elapsed_time(ev1), "qp_iter", it.tolist())
 # serial kernel: A, B (Riccati), C (forward), D; segmented (NMPC_AMD_SEG > 0): A, B (segment sweeps), M (master),
 # C+D (segment forward + step); the segmented kernel decides to stop before its phase B
 seg = int(os.environ.get("NMPC_AMD_SEG", "0")) > 0
 names = ["A", "Bseg", "M", "CD"] if seg else ["A", "B", "C", "D"]
 ph = {n: [] for n in names}
-for b in range(B):
+for b in range(min(B, 256)):
     for i in range(int(it[b]) + 1):
         base = 3 + 4 * i
         prev = st[b, 2] if i == 0 else st[b, base - 1]
