@@ -142,7 +142,7 @@ def roofline(fleets, node, kernel_ms, steps, step_s=None):
                                         "every issued instruction, idle team lanes and the lockstep waves' extra "
                                         "iterations included"}
                                if pmc and pmc.get("executed_flops_fp64_per_launch") else None),
-            "traffic_source": src, "kernel": f"k_sqp_rti_{fleets[0].solver.kernel}" +
+            "traffic_source": src, "kernel": _kernel_label(fleets[0]) +
             (f" x{len(fleets)} concurrent streams" if len(fleets) > 1 else ""),
             "kernel_ms_mean": round(t_launch * 1e3, 4),
             "timing": ("HIP events per launch on its stream; achieved = the step's flops / (timed region / steps), "
@@ -153,6 +153,18 @@ def roofline(fleets, node, kernel_ms, steps, step_s=None):
             "note": "VALU-bound, latency-limited: <=15x15 per-robot blocks, no GEMM-shaped work (no MFMA); "
                     "traffic = 2*FETCH_SIZE + WRITE_SIZE (L2<->fabric incl. Infinity-Cache hits) per step (the sum "
                     "over the step's launches: one per model and stream group)"}
+
+
+def _kernel_label(fleet):
+    """The solve kernel a fleet's launches take (nmpc_batch_plan): the team kernel, or the row-parallel one with its
+    waves per robot and horizon segments."""
+    plan = getattr(fleet.solver, "plan", None)
+    if plan is None:
+        return f"k_sqp_rti_{getattr(fleet.solver, 'kernel', 'team')}"
+    name, waves, segs = plan(fleet.B)
+    if name == "team":
+        return "k_sqp_rti_team"
+    return f"k_sqp_rti_rowpar ({waves} wave(s) per robot, " + (f"{segs} horizon segments)" if segs else "serial phases)")
 
 
 def hbm_block(pmc, src, traffic, cbytes, t_k, groups=1):

@@ -194,6 +194,11 @@ int nmpc_batch_warm_state(nmpc_batch* b, unsigned char** warm, float** scratch, 
  * the parameters. Each output may be NULL. */
 int nmpc_batch_warm_rule(const nmpc_batch* b, int* warm, int* warm_iter_max, int* iter_max);
 
+/* The kernel a solve / run launch of B robots takes on this handle (the single-direction IPM; run_path launches
+ * always take the team kernel): kernel 0 = k_sqp_rti_team (four robots per wave), 1 = k_sqp_rti_rowpar
+ * (waves_per_robot waves per robot, `segments` horizon segments, 0 = the serial phases). Each output may be NULL. */
+int nmpc_batch_plan(const nmpc_batch* b, int B, int* kernel, int* waves_per_robot, int* segments);
+
 /* Bench / test harness: closed-loop plant step and path-reference regeneration for B robots
  * (see DESIGN.md "Synthetic closed loop"). All device pointers, [field][B]:
  *   path [6][B] = {x0, y0, th0, kappa, speed, length} circular-arc paths; goal-pose robots have length < 0

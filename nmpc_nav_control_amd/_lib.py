@@ -75,7 +75,7 @@ class SolverCapsule(ctypes.Structure):
 BATCH_SYMBOLS = [
     "nmpc_model_dims", "nmpc_model_params_default", "nmpc_model_params_set_limits", "nmpc_batch_create",
     "nmpc_batch_destroy", "nmpc_batch_set_params", "nmpc_batch_get_params", "nmpc_batch_init_iterate",
-    "nmpc_batch_solve", "nmpc_batch_solve_iterate", "nmpc_batch_run", "nmpc_batch_run_path", "nmpc_batch_state", "nmpc_batch_warm_state", "nmpc_batch_warm_rule", "nmpc_batch_forget_warm", "nmpc_batch_set_kernel", "nmpc_batch_set_schedule",
+    "nmpc_batch_solve", "nmpc_batch_solve_iterate", "nmpc_batch_run", "nmpc_batch_run_path", "nmpc_batch_state", "nmpc_batch_warm_state", "nmpc_batch_warm_rule", "nmpc_batch_plan", "nmpc_batch_forget_warm", "nmpc_batch_set_kernel", "nmpc_batch_set_schedule",
     "nmpc_fleet_sim_step", "nmpc_fleet_sim_step_renew", "nmpc_fleet_hash",
     "nmpc_last_error", "nmpc_version", "nmpc_path_discretize", "nmpc_codegen_default", "nmpc_capsule_new",
     "nmpc_capsule_delete", "nmpc_capsule_create", "nmpc_capsule_reset", "nmpc_capsule_update_params",
@@ -127,6 +127,7 @@ def lib():
     L.nmpc_batch_forget_warm.argtypes = [vp, i, vp, vp]
     L.nmpc_batch_warm_state.argtypes = [vp, ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.POINTER(ctypes.c_size_t)]
     L.nmpc_batch_warm_rule.argtypes = [vp, c_int_p, c_int_p, c_int_p]
+    L.nmpc_batch_plan.argtypes = [vp, ctypes.c_int, c_int_p, c_int_p, c_int_p]
     L.nmpc_fleet_sim_step.argtypes = [vp, i, vp, vp, vp, vp, vp, vp, vp, vp, vp, i, vp]
     L.nmpc_fleet_sim_step_renew.argtypes = [vp, i, vp, vp, vp, vp, vp, vp, vp, vp, vp, ctypes.POINTER(FleetRenew), vp]
     L.nmpc_fleet_hash.argtypes = [ctypes.c_uint, ctypes.c_uint, ctypes.c_uint]

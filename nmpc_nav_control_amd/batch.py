@@ -68,6 +68,14 @@ class BatchSolver:
         check(lib().nmpc_batch_set_kernel(self._h, KERNELS[kernel]), "nmpc_batch_set_kernel")
         self.kernel = kernel
 
+    def plan(self, B):
+        """The kernel a solve / run launch of B robots takes (nmpc_batch_plan): (name, waves per robot, segments),
+        name 'team' (k_sqp_rti_team) or 'rowpar' (k_sqp_rti_rowpar; segments 0 = its serial phases)."""
+        k, w, sg = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        check(lib().nmpc_batch_plan(self._h, int(B), ctypes.byref(k), ctypes.byref(w), ctypes.byref(sg)),
+              "nmpc_batch_plan")
+        return ("rowpar" if k.value else "team"), w.value, sg.value
+
     def set_schedule(self, mode):
         """Team placement of the team kernel: 'auto' (default), 'off', 'sorted' or 'interleaved'
         (include/nmpc_amd/nmpc_batch.h; no effect on any result)."""

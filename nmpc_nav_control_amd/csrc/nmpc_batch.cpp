@@ -671,6 +671,24 @@ int nmpc_batch_forget_warm(nmpc_batch* b, int B, const unsigned char* mask, void
     return hip_err(hipGetLastError(), "forget_warm launch");
 }
 
+int nmpc_batch_plan(const nmpc_batch* b, int B, int* kernel, int* waves_per_robot, int* segments)
+{
+    if (!b) return set_err(NMPC_ERR_ARG, "batch is NULL");
+    if (B < 0 || B > b->capacity) return set_err(NMPC_ERR_ARG, "B out of range");
+    KArgs a{};
+    a.B = B;
+    bool rp;
+    switch (b->prm.model) {
+    case NMPC_MODEL_DIFF2AMR: rp = rowpar_ok<Diff2>(b, a, kModeSolve); break;
+    case NMPC_MODEL_OMNI4AMR: rp = rowpar_ok<Omni4>(b, a, kModeSolve); break;
+    default: rp = rowpar_ok<Tric3>(b, a, kModeSolve); break;
+    }
+    if (kernel) *kernel = rp ? 1 : 0;
+    if (waves_per_robot) *waves_per_robot = rp ? (B <= 256 ? 4 : 1) : 0;
+    if (segments) *segments = rp ? a.seg : 0;
+    return NMPC_OK;
+}
+
 int nmpc_batch_warm_rule(const nmpc_batch* b, int* warm, int* warm_iter_max, int* iter_max)
 {
     if (!b) return set_err(NMPC_ERR_ARG, "batch is NULL");

@@ -192,6 +192,7 @@ def test_null_handle_is_an_argument_error_everywhere(built):
         "nmpc_batch_forget_warm": lambda: L.nmpc_batch_forget_warm(None, 1, None, None),
         "nmpc_batch_warm_state": lambda: L.nmpc_batch_warm_state(None, None, None, None),
         "nmpc_batch_warm_rule": lambda: L.nmpc_batch_warm_rule(None, None, None, None),
+        "nmpc_batch_plan": lambda: L.nmpc_batch_plan(None, 1, None, None, None),
         "nmpc_fleet_sim_step": lambda: L.nmpc_fleet_sim_step(None, 1, *([None] * 9), 0, None),
     }
     for name, call in calls.items():

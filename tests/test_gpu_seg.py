@@ -138,3 +138,17 @@ def test_hybrid_launch_matches_plain(built, monkeypatch, model):
         if tick == 0:
             assert float(np.abs(a["u0"].cpu().numpy().T - u0_o).max()) <= TOL
             assert int((b["qp_iter"] >= 8).sum()) > 0  # the next ticks split the batch
+
+
+def test_plan_defaults(built):
+    """nmpc_batch_plan: the kernel each launch size takes by default -- one capsule (N = 80) on four waves with 8
+    horizon segments, up to 1024 robots (N = 40) the segmented kernel on one wave each (4 segments), larger batches
+    the team kernel."""
+    h1 = BatchSolver("diff", 80, 1, params=default_params("diff", 80))
+    assert h1.plan(1) == ("rowpar", 4, 8)
+    h = BatchSolver("diff", 40, 4096, params=default_params("diff", 40))
+    assert h.plan(256) == ("rowpar", 4, 5)
+    assert h.plan(1024) == ("rowpar", 1, 4)
+    assert h.plan(1025)[0] == "team" and h.plan(4096)[0] == "team"
+    ht = BatchSolver("tric", 60, 64, params=default_params("tric", 60))
+    assert ht.plan(64) == ("rowpar", 4, 6)
