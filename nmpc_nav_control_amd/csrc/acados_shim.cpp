@@ -143,6 +143,10 @@ void codegen_defaults(nmpc_capsule_impl* c, const nmpc_codegen_desc& d)
     // a capsule is one robot whose latency is its own IPM count, so its warm start floors the multipliers for the
     // mean count (kappa 0.01; the batch default for diff, 0.2, is tuned for the slowest robot of a fleet)
     c->prm.qp_warm_kappa = 0.01;
+    // acados' default, which the reference's OCP keeps (scripts/diff/generate_c_code.py:68-74 sets no
+    // qp_warm_start): HPIPM starts every QP cold. ocp_nlp_solver_opts_set(.., "qp_warm_start", 1) opts in to the
+    // capsule's multiplier warm start (INTEGRATION.md "Capsule semantics")
+    c->prm.qp_warm_start = 0;
     // HPIPM has no infeasibility exit: a hard QP runs to qp_iter_max and acados' RTI accepts the result
     // (SURVEY Appendix B.6), so the drop-in never turns a stiff but feasible QP into the wrapper's exception
     c->prm.qp_infeas_lambda = 0.0;

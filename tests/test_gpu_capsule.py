@@ -118,10 +118,11 @@ def _set_tick(c, x0, yref):
 
 
 def test_capsule_warm_start_and_reset(built):
-    """A capsule solved tick after tick starts its IPM from its own previous multipliers (qp_warm_start): a fresh
+    """A capsule with qp_warm_start = 1, solved tick after tick, starts its IPM from its own previous multipliers: a fresh
     capsule given the same inputs and iterate starts cold, in the same launch, and reaches the same QP solution.
     After reset the next solve is cold again: bit-identical to a fresh capsule's solve from a zero iterate."""
     a = make("diff")[0]
+    a.solver_opts_set("qp_warm_start", 1)  # (the capsule default is acados' cold start)
     o = Oracle("diff", N)
     x0 = np.array([0.05, -0.02, 2.9, 0.1, 0.05, 0.0, 0.0])
     yref = np.zeros((N + 1, a.ny))

@@ -9,9 +9,10 @@
  * The robot follows a circle of radius 0.5 m in closed loop on a kinematic plant. No Python anywhere: this is
  * the latency a C++ ROS node linked against libacados_ocp_solver_diff2amr.so sees.
  * Prints one JSON line: wall ms per tick (mean, p50, p99), the solver's own time_tot, IPM iterations.
- * usage: build/capsule_latency [ticks=300] [cold]
- *   cold: ocp_nlp_solver_opts_set(.., "qp_warm_start", 0) -- HPIPM's cold start every tick, the reference's
- *         generated default (scripts/diff/generate_c_code.py:68-74); default: the capsule's warm start
+ * usage: build/capsule_latency [ticks=300] [cold|warm]
+ *   cold (default): HPIPM's cold start every tick, acados' default and the reference's generated OCP's
+ *         (scripts/diff/generate_c_code.py:68-74 sets no qp_warm_start), also the capsule's default
+ *   warm: ocp_nlp_solver_opts_set(.., "qp_warm_start", 1) -- the capsule's multiplier warm start
  */
 #include <string.h>
 #include <math.h>
@@ -43,15 +44,15 @@ static int cmp(const void* a, const void* b)
 int main(int argc, char** argv)
 {
     const int ticks = argc > 1 ? atoi(argv[1]) : 300;
-    const int warm = !(argc > 2 && !strcmp(argv[2], "cold"));
+    const int warm = argc > 2 && !strcmp(argv[2], "warm");
     const double dt = 1.0 / 40.0, b = 0.270;  /* control period, wheel separation (NMPCNavControlDiff) */
     const double W[NY] = {10, 10, 5, 0, 0, 0, 0, 1, 1};
     diff2amr_solver_capsule* c = diff2amr_acados_create_capsule();
     if (diff2amr_acados_create(c) != 0) { fprintf(stderr, "create failed\n"); return 1; }
     const int N = c->nlp_dims->N;
-    if (!warm) {
-        int zero = 0;
-        ocp_nlp_solver_opts_set(c->nlp_config, c->nlp_opts, "qp_warm_start", &zero);
+    {
+        int ws = warm;
+        ocp_nlp_solver_opts_set(c->nlp_config, c->nlp_opts, "qp_warm_start", &ws);
     }
     /* constructor: stage weights (NMPCNavControlDiff.cpp:62-73) */
     double Wm[NY * NY] = {0}, We[NYN * NYN] = {0};

@@ -11,6 +11,6 @@ timeout -k 10 420 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout
 tail -2 $OUT/${TAG}_tests.log
 timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/${TAG}_smoke.log 2>&1; ok $? smoke
 timeout -k 10 300 python bench.py "$@" > $OUT/${TAG}_bench.json 2> $OUT/${TAG}_bench.err; ok $? bench
-timeout -k 10 60 build/capsule_latency 300 > $OUT/${TAG}_cap_warm.json 2> $OUT/${TAG}_cap_warm.err; ok $? cap_warm
+timeout -k 10 60 build/capsule_latency 300 warm > $OUT/${TAG}_cap_warm.json 2> $OUT/${TAG}_cap_warm.err; ok $? cap_warm
 timeout -k 10 60 build/capsule_latency 300 cold > $OUT/${TAG}_cap_cold.json 2> $OUT/${TAG}_cap_cold.err; ok $? cap_cold
 bash tools/mall_calibration.sh $TAG; ok $? mall
