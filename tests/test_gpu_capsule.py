@@ -131,6 +131,7 @@ def test_capsule_warm_start_and_reset(built):
         for k, p in enumerate(path(tick, N + 1)):
             yref[k, :3] = [p.x, p.y, np.unwrap([x0[2], p.theta])[1]]
         cold = make("diff")[0]
+        cold.solver_opts_set("qp_warm_start", 1)  # same options as a, so both share one launch; fresh, so cold
         xs, us = a.iterate()
         for k in range(N + 1):
             cold.out_set(k, "x", xs[k])

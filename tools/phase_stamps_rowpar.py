@@ -38,7 +38,9 @@ it = f.qp_iter.cpu().numpy()[:min(B, 256)]
 print("kernel ms", ev0.elapsed_time(ev1), "qp_iter", it.tolist())
 # serial kernel: A, B (Riccati), C (forward), D; segmented (NMPC_AMD_SEG > 0): A, B (segment sweeps), M (master),
 # C+D (segment forward + step); the segmented kernel decides to stop before its phase B
-seg = int(os.environ.get("NMPC_AMD_SEG", "0")) > 0
+plan = f.solver.plan(B)  # (kernel, waves per robot, segments) of this launch
+print("plan", plan)
+seg = plan[2] > 0
 names = ["A", "Bseg", "M", "CD"] if seg else ["A", "B", "C", "D"]
 ph = {n: [] for n in names}
 for b in range(min(B, 256)):
