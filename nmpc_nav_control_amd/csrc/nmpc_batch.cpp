@@ -32,6 +32,7 @@ struct nmpc_batch {
     // (the serial phases at one wave per robot lose to the team kernel, the segmented ones win up to a robot per
     // SIMD: diff N = 40 B = 1024 1.15 -> 1.57 M it/s, profiles/r04/ab/seg.txt)
     int rowpar_max = 1024;
+    int rowpar_w = 1;  // waves per robot above 256 robots (1, or 2 for A/B: NMPC_AMD_ROWPAR_W)
     // horizon segments of the row-parallel kernel (sqp_rti_rowpar.hip SEG): -1 = chosen per launch (seg_count),
     // 0 = the serial phases B / C, S > 0 = S segments when N % S == 0 (NMPC_AMD_SEG overrides)
     int seg = -1;
@@ -157,7 +158,7 @@ template <class M>
 bool rowpar_ok(const nmpc_batch* b, KArgs& a, int mode)
 {
     if (b->kp.ipm != NMPC_IPM_SINGLE || a.segs || a.B > b->rowpar_max) return false;
-    const int rows = a.B <= 256 ? 16 : 4;  // four waves per robot up to 256 robots, one wave above
+    const int rows = a.B <= 256 ? 16 : 4 * b->rowpar_w;  // four waves per robot up to 256 robots, rowpar_w above
     int S = b->seg >= 0 ? b->seg : seg_count(b->prm.N, rows);
     if (S > rows || S > kSegMax || (S > 0 && b->prm.N % S)) S = 0;
     if (S > 0 && rowpar_lds_bytes<M>(b->prm.N, mode, S) > 65536) S = 0;
@@ -176,7 +177,7 @@ hipError_t schedule(nmpc_batch* b, KArgs& a, int mode, hipStream_t s)
     case NMPC_MODEL_OMNI4AMR: a.rowpar = rowpar_ok<Omni4>(b, a, mode); break;
     default: a.rowpar = rowpar_ok<Tric3>(b, a, mode); break;
     }
-    if (a.rowpar) a.rowpar = (a.B <= 256) ? 4 : 1;  // waves per robot
+    if (a.rowpar) a.rowpar = (a.B <= 256) ? 4 : b->rowpar_w;  // waves per robot
     if (a.rowpar) return hipSuccess;  // one robot per wave: nothing to place
     a.dense = ((a.B + 3) / 4 > b->n_simd) ? 1 : 0;  // 4 teams per wave
     // small batches leave most of the chip idle: one wave per robot, whose spare rows integrate P0's stages
@@ -415,6 +416,7 @@ int nmpc_batch_create(const nmpc_model_params* prm, int capacity, nmpc_batch** o
     if (const char* v = std::getenv("NMPC_AMD_SPLIT_MAX")) b->split_max = std::atoi(v);  // A/B: 0 = never split
     if (const char* v = std::getenv("NMPC_AMD_ROWPAR_MAX")) b->rowpar_max = std::atoi(v);  // A/B: 0 = never
     if (const char* v = std::getenv("NMPC_AMD_SEG")) b->seg = std::atoi(v);  // A/B: 0 = serial, S = S segments
+    if (const char* v = std::getenv("NMPC_AMD_ROWPAR_W")) b->rowpar_w = std::atoi(v) == 2 ? 2 : 1;  // A/B
     if (const char* v = std::getenv("NMPC_AMD_HYBRID")) b->hybrid_h = std::atoi(v);  // A/B: 0 = off
     if (const char* v = std::getenv("NMPC_AMD_HYBRID_CAP")) b->hybrid_cap = std::atoi(v);
     const int N = prm->N;
@@ -684,7 +686,7 @@ int nmpc_batch_plan(const nmpc_batch* b, int B, int* kernel, int* waves_per_robo
     default: rp = rowpar_ok<Tric3>(b, a, kModeSolve); break;
     }
     if (kernel) *kernel = rp ? 1 : 0;
-    if (waves_per_robot) *waves_per_robot = rp ? (B <= 256 ? 4 : 1) : 0;
+    if (waves_per_robot) *waves_per_robot = rp ? (B <= 256 ? 4 : b->rowpar_w) : 0;
     if (segments) *segments = rp ? a.seg : 0;
     return NMPC_OK;
 }

@@ -1305,12 +1305,15 @@ hipError_t launch_sqp_rti_rowpar(const KParams& P, const KArgs& a, int mode, hip
     const size_t lds = rowpar_lds_bytes<M>(P.N, mode, a.seg);
     if (lds > 65536 || P.ipm != 1 || a.segs) return hipErrorInvalidValue;
     // segments: N % S == 0, at most kSegMax and at most one per row of the block
-    if (a.seg < 0 || a.seg > kSegMax || a.seg > 4 * (a.rowpar >= 4 ? 4 : 1) || (a.seg > 0 && P.N % a.seg != 0))
+    const int W = a.rowpar >= 4 ? 4 : (a.rowpar == 2 ? 2 : 1);
+    if (a.seg < 0 || a.seg > kSegMax || a.seg > 4 * W || (a.seg > 0 && P.N % a.seg != 0))
         return hipErrorInvalidValue;
     const int grid = (a.hyb_role == 2) ? (a.B < a.hyb_cap ? a.B : a.hyb_cap) : a.B;
-    if (a.rowpar >= 4)  // four waves per robot (one per SIMD of its CU)
+    if (W == 4)  // four waves per robot (one per SIMD of its CU)
         if (a.seg > 0) hipLaunchKernelGGL((k_sqp_rti_rowpar<M, 4, true>), dim3(grid), dim3(256), lds, stream, P, a, mode);
         else hipLaunchKernelGGL((k_sqp_rti_rowpar<M, 4, false>), dim3(grid), dim3(256), lds, stream, P, a, mode);
+    else if (W == 2 && a.seg > 0)  // (A/B: NMPC_AMD_ROWPAR_W=2 above 256 robots)
+        hipLaunchKernelGGL((k_sqp_rti_rowpar<M, 2, true>), dim3(grid), dim3(128), lds, stream, P, a, mode);
     else if (a.seg > 0)
         hipLaunchKernelGGL((k_sqp_rti_rowpar<M, 1, true>), dim3(grid), dim3(64), lds, stream, P, a, mode);
     else
