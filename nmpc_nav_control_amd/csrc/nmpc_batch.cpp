@@ -28,11 +28,12 @@ struct nmpc_batch {
     int n_simd = 1024;           // SIMDs of the device (4 per CU)
     int split_max = 256;         // team-kernel launches of at most this many robots run one block per robot (split)
     // launches of at most this many robots (single-direction IPM, not run_path) run k_sqp_rti_rowpar (DESIGN.md
-    // section 4): four waves per robot up to 256 robots; one wave per robot above, and there only with segments
-    // (the serial phases at one wave per robot lose to the team kernel, the segmented ones win up to a robot per
-    // SIMD: diff N = 40 B = 1024 1.15 -> 1.57 M it/s, profiles/r04/ab/seg.txt)
+    // section 4): four waves per robot up to 256 robots; above, rowpar_w waves per robot and there only with
+    // segments, all on the first wave's four rows (the second wave takes half of the stage-parallel phases; segments
+    // on both waves of a SIMD's two resident waves contend: diff N = 40 B = 1024 1.15 M it/s on the team kernel ->
+    // 1.57 M on one wave per robot -> 1.65 M on two, 1.52 M with 5 segments over both; profiles/r04/ab/seg.txt)
     int rowpar_max = 1024;
-    int rowpar_w = 1;  // waves per robot above 256 robots (1, or 2 for A/B: NMPC_AMD_ROWPAR_W)
+    int rowpar_w = 2;  // (NMPC_AMD_ROWPAR_W=1 for A/B)
     // horizon segments of the row-parallel kernel (sqp_rti_rowpar.hip SEG): -1 = chosen per launch (seg_count),
     // 0 = the serial phases B / C, S > 0 = S segments when N % S == 0 (NMPC_AMD_SEG overrides)
     int seg = -1;
@@ -158,7 +159,7 @@ template <class M>
 bool rowpar_ok(const nmpc_batch* b, KArgs& a, int mode)
 {
     if (b->kp.ipm != NMPC_IPM_SINGLE || a.segs || a.B > b->rowpar_max) return false;
-    const int rows = a.B <= 256 ? 16 : 4 * b->rowpar_w;  // four waves per robot up to 256 robots, rowpar_w above
+    const int rows = a.B <= 256 ? 16 : 4;  // segments: any row up to 256 robots, the first wave's rows above
     int S = b->seg >= 0 ? b->seg : seg_count(b->prm.N, rows);
     if (S > rows || S > kSegMax || (S > 0 && b->prm.N % S)) S = 0;
     if (S > 0 && rowpar_lds_bytes<M>(b->prm.N, mode, S) > 65536) S = 0;
@@ -416,7 +417,7 @@ int nmpc_batch_create(const nmpc_model_params* prm, int capacity, nmpc_batch** o
     if (const char* v = std::getenv("NMPC_AMD_SPLIT_MAX")) b->split_max = std::atoi(v);  // A/B: 0 = never split
     if (const char* v = std::getenv("NMPC_AMD_ROWPAR_MAX")) b->rowpar_max = std::atoi(v);  // A/B: 0 = never
     if (const char* v = std::getenv("NMPC_AMD_SEG")) b->seg = std::atoi(v);  // A/B: 0 = serial, S = S segments
-    if (const char* v = std::getenv("NMPC_AMD_ROWPAR_W")) b->rowpar_w = std::atoi(v) == 2 ? 2 : 1;  // A/B
+    if (const char* v = std::getenv("NMPC_AMD_ROWPAR_W")) b->rowpar_w = std::atoi(v) == 1 ? 1 : 2;  // A/B
     if (const char* v = std::getenv("NMPC_AMD_HYBRID")) b->hybrid_h = std::atoi(v);  // A/B: 0 = off
     if (const char* v = std::getenv("NMPC_AMD_HYBRID_CAP")) b->hybrid_cap = std::atoi(v);
     const int N = prm->N;

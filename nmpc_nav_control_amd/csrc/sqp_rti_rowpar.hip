@@ -1312,7 +1312,7 @@ hipError_t launch_sqp_rti_rowpar(const KParams& P, const KArgs& a, int mode, hip
     if (W == 4)  // four waves per robot (one per SIMD of its CU)
         if (a.seg > 0) hipLaunchKernelGGL((k_sqp_rti_rowpar<M, 4, true>), dim3(grid), dim3(256), lds, stream, P, a, mode);
         else hipLaunchKernelGGL((k_sqp_rti_rowpar<M, 4, false>), dim3(grid), dim3(256), lds, stream, P, a, mode);
-    else if (W == 2 && a.seg > 0)  // (A/B: NMPC_AMD_ROWPAR_W=2 above 256 robots)
+    else if (W == 2 && a.seg > 0)  // two waves per robot above 256 robots (the default there)
         hipLaunchKernelGGL((k_sqp_rti_rowpar<M, 2, true>), dim3(grid), dim3(128), lds, stream, P, a, mode);
     else if (a.seg > 0)
         hipLaunchKernelGGL((k_sqp_rti_rowpar<M, 1, true>), dim3(grid), dim3(64), lds, stream, P, a, mode);

@@ -91,8 +91,8 @@ def test_seg_matches_serial_and_oracle(built, monkeypatch, model, N, seg):
 
 @pytest.mark.parametrize("model", ["diff", "tric"])
 def test_seg_one_wave_per_robot(built, monkeypatch, model):
-    """Batches above 256 robots run one wave (4 rows, up to 4 segments) per robot when the row-parallel kernel is
-    allowed there (NMPC_AMD_ROWPAR_MAX): 300 robots at N = 40, 4 segments against the serial phases."""
+    """Batches above 256 robots run two waves (segments on the first wave's 4 rows) per robot: 300 robots at N = 40,
+    4 segments against the serial phases (one wave per robot)."""
     out, u0_o = run_pair(monkeypatch, model, 40, 300, 4, ticks=2, cap=300, rowpar_max=1024)
     for tick, (sg, se) in enumerate(out):
         assert (sg["status"] == 0).all() and (se["status"] == 0).all(), tick
@@ -142,13 +142,13 @@ def test_hybrid_launch_matches_plain(built, monkeypatch, model):
 
 def test_plan_defaults(built):
     """nmpc_batch_plan: the kernel each launch size takes by default -- one capsule (N = 80) on four waves with 8
-    horizon segments, up to 1024 robots (N = 40) the segmented kernel on one wave each (4 segments), larger batches
-    the team kernel."""
+    horizon segments, up to 1024 robots (N = 40) the segmented kernel on two waves each (4 segments, all on the
+    first wave), larger batches the team kernel."""
     h1 = BatchSolver("diff", 80, 1, params=default_params("diff", 80))
     assert h1.plan(1) == ("rowpar", 4, 8)
     h = BatchSolver("diff", 40, 4096, params=default_params("diff", 40))
     assert h.plan(256) == ("rowpar", 4, 5)
-    assert h.plan(1024) == ("rowpar", 1, 4)
+    assert h.plan(1024) == ("rowpar", 2, 4)
     assert h.plan(1025)[0] == "team" and h.plan(4096)[0] == "team"
     ht = BatchSolver("tric", 60, 64, params=default_params("tric", 60))
     assert ht.plan(64) == ("rowpar", 4, 6)
