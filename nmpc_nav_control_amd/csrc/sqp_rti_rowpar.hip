@@ -766,10 +766,13 @@ __global__ __launch_bounds__(64 * W, 1) void k_sqp_rti_rowpar(KParams P, KArgs a
                     pv = is_x ? y : 0.0f;
                     // lam sensitivities: column c of Y = G' Phi_{k+1}, Z = L^-1 Y_u (uniform over the row), and
                     // Phi_k = Y_x - LM Z; the value's lam terms Gam -= Z'Z, t -= Z' LR
-                    float zc[NU][NX];
+                    float zc[NU][NX], Yc[NX];
+#pragma unroll
+                    for (int c = 0; c < NX; c++) Yc[c] = 0.0f;
+                    rowmul_f32<NX, NU>(Yc, Gc, Phi);  // Y = G' Phi, every column in one fused-DPP block
                     sfor<0, NX>([&](auto cc) {
                         constexpr int c = decltype(cc)::value;
-                        float yc = dot_x<NX, NU>(0.0f, Phi[c], Gc);
+                        float yc = Yc[c];
                         sfor<0, NU>([&](auto jc) {
                             constexpr int j2 = decltype(jc)::value;
                             const float z = bc<j2>(yc * rLm[j2]);
