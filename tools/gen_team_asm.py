@@ -109,6 +109,20 @@ def mst_rowmul(n, off):
     return "\n".join(out)
 
 
+def mst_rowmul_lt(n, off):
+    # acc[c] += bcast_{off+l}(b[c]) * a[l] for l >= c only: row r of A B with B lower triangular (b[c] = 0 on lane
+    # off + l for c > l), or the lower triangle of A B where row r of A vanishes left of r (the master's L' V)
+    lines = ["s_nop 1"]
+    for l in range(n):
+        for c in range(l + 1):
+            lines.append(f"v_fmac_f64_dpp %{c}, %{n + c}, %{2 * n + l} row_newbcast:{off + l}{M}")
+    outs = ", ".join(f'"+v"(acc[{c}])' for c in range(n))
+    ins = ", ".join([f'"v"(b[{c}])' for c in range(n)] + [f'"v"(a[{l}])' for l in range(n)])
+    body = "\\n\\t".join(lines)
+    return (f"__device__ __forceinline__ void mst_rowmul_lt_{n}_{off}(double (&acc)[{n}], const double (&a)[{n}],"
+            f" const double (&b)[{n}])\n{{\n    asm(\"{body}\"\n        : {outs}\n        : {ins});\n}}\n")
+
+
 def rowmul_f32(n, off):
     # fp32 acc[c] += bcast_{off+l}(b[c]) * a[l] (the segments' lam sensitivities Y = G' Phi, all columns in one block)
     lines = ["s_nop 1"]
@@ -201,7 +215,7 @@ def main():
         nv = nx + nu
         parts += [pg_block(nx, nu), mrow_pg_block(nx, nu), chol_update(nx, nu),
                   dot_f32(nx, nu, f"dot_x_{nx}_{nu}"), dot_f32(nv, 0, f"dot_v_{nx}_{nu}"),
-                  mst_rowmul(nx, nu), rowmul_f32(nx, nu), mst_rowdot(nx, nu), mst_chol(nx, nu), mst_trsv(nx, nu), mst_vdot(nx, nu)]
+                  mst_rowmul(nx, nu), mst_rowmul_lt(nx, nu), rowmul_f32(nx, nu), mst_rowdot(nx, nu), mst_chol(nx, nu), mst_trsv(nx, nu), mst_vdot(nx, nu)]
     parts += ["}  // namespace nmpc", ""]
     with open(OUT, "w") as fh:
         fh.write("\n".join(parts))

@@ -43,8 +43,8 @@ __global__ void k_master(const double* Ph, const double* G, const double* F, con
         V[c] = 0.0;
         K[c] = (xi == c) ? 1.0 : 0.0;
     }
-    mst_rowmul<NX, NU>(V, Gr, Lp);
-    mst_rowmul<NX, NU>(K, Lt, V);
+    mst_rowmul_lt<NX, NU>(V, Gr, Lp);  // as the kernel: L lower triangular, K's lower triangle only
+    mst_rowmul_lt<NX, NU>(K, Lt, V);
     rowchol<NX, NU, false>(K, rdv, xi, 0.5);
     sfor<0, NX>([&](auto jc) {
         constexpr int j = decltype(jc)::value;
@@ -52,16 +52,16 @@ __global__ void k_master(const double* Ph, const double* G, const double* F, con
         Lp[j] = y;
         if constexpr (j + 1 < NX) mst_trsv<NX, NU, j>(Lp, K[j], y);
     });
-    double Q[NX], T[NX], Pn[NX];
+    double Q[NX], Wr[NX], Pn[NX];
 #pragma unroll
     for (int c = 0; c < NX; c++) {
         Q[c] = 0.0;
-        T[c] = 0.0;
+        Wr[c] = 0.0;
         Pn[c] = Phr[c];
     }
-    mst_rowdot<NX, NU>(Q, Lp, Lp);
-    mst_rowdot<NX, NU>(T, Q, Fr);
-    mst_rowmul<NX, NU>(Pn, Fr, T);
+    mst_rowdot<NX, NU>(Q, Lp, Lp);  // Q = Y Y'
+    mst_rowmul<NX, NU>(Wr, Fr, Lp);  // W = F Y
+    mst_rowdot<NX, NU>(Pn, Wr, Wr);  // Phat' = Phat + W W' (= Phat + F Q F')
     const double cv = mst_vdot<NX, NU>(vt[xi], vp[xi], Gn);
     const double w = mst_vdot<NX, NU>(vp[xi], cv, Q);
     if (is_x) {
