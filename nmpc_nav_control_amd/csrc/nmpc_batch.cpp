@@ -164,6 +164,10 @@ bool rowpar_ok(const nmpc_batch* b, KArgs& a, int mode)
     if (S > rows || S > kSegMax || (S > 0 && b->prm.N % S)) S = 0;
     if (S > 0 && rowpar_lds_bytes<M>(b->prm.N, mode, S) > 65536) S = 0;
     if (a.B > 256 && S == 0 && b->seg < 0) return false;  // one wave per robot only with segments (auto)
+    // above 256 robots two robots' waves share a SIMD, which needs <= 256 registers per lane: diff and tric's
+    // segmented kernels take 246-250, omni4's (11 x 11 master blocks) 357 (tools/reg_usage.py), so omni4 keeps the
+    // team kernel there
+    if (a.B > 256 && M::NU == 4 && b->rowpar_max <= 1024) return false;
     a.seg = S;
     return rowpar_lds_bytes<M>(b->prm.N, mode, S) <= 65536;
 }

@@ -766,13 +766,12 @@ __global__ __launch_bounds__(64 * W, 1) void k_sqp_rti_rowpar(KParams P, KArgs a
                     pv = is_x ? y : 0.0f;
                     // lam sensitivities: column c of Y = G' Phi_{k+1}, Z = L^-1 Y_u (uniform over the row), and
                     // Phi_k = Y_x - LM Z; the value's lam terms Gam -= Z'Z, t -= Z' LR
-                    float zc[NU][NX], Yc[NX];
-#pragma unroll
-                    for (int c = 0; c < NX; c++) Yc[c] = 0.0f;
-                    rowmul_f32<NX, NU>(Yc, Gc, Phi);  // Y = G' Phi, every column in one fused-DPP block
+                    // (column by column: the fused all-column block held 7 more accumulators live and pushed the
+                    // kernel past 256 registers, one wave per SIMD: diff1024 1.65 -> 1.11 M it/s)
+                    float zc[NU][NX];
                     sfor<0, NX>([&](auto cc) {
                         constexpr int c = decltype(cc)::value;
-                        float yc = Yc[c];
+                        float yc = dot_x<NX, NU>(0.0f, Phi[c], Gc);
                         sfor<0, NU>([&](auto jc) {
                             constexpr int j2 = decltype(jc)::value;
                             const float z = bc<j2>(yc * rLm[j2]);
@@ -861,21 +860,13 @@ __global__ __launch_bounds__(64 * W, 1) void k_sqp_rti_rowpar(KParams P, KArgs a
             // of every vector (the fused-DPP blocks of team_asm_gen.hpp); segment data come from LDS
             if (tid < 16 && Sg > 1) {
                 const double* const sP = reinterpret_cast<const double*>(seg_lds + SegL.SUM_P);
-                double* const sY = reinterpret_cast<double*>(seg_lds + SegL.QS);  // Y_i rows (Q_i = Y_i Y_i')
+                double* const sQ = reinterpret_cast<double*>(seg_lds + SegL.QS);
                 double* const sCv = reinterpret_cast<double*>(seg_lds + SegL.CS);
                 double* const sPh = reinterpret_cast<double*>(seg_lds + SegL.PHS);
                 double* const sLt = reinterpret_cast<double*>(seg_lds + SegL.LT);
                 auto ldrow = [&](int i, int off, double (&v)[NX]) {  // row xi of segment i's fp32 matrix at off
 #pragma unroll
                     for (int c = 0; c < NX; c++) v[c] = (double)seg_lds[off + (i * NX + xi) * NX + c];
-                };
-                // Q_i v = Y_i (Y_i' v) for a lane-distributed v: column xi of Y_i from LDS, then row xi
-                auto qmul = [&](int i, double v, const double (&Yr)[NX]) -> double {
-                    double Yc[NX];
-#pragma unroll
-                    for (int r2 = 0; r2 < NX; r2++) Yc[r2] = sY[((size_t)i * NX + r2) * NX + xi];
-                    const double u = mst_vdot<NX, NU>(0.0, v, Yc);
-                    return mst_vdot<NX, NU>(0.0, u, Yr);
                 };
                 double Ph[NX], ph;
 #pragma unroll
@@ -916,43 +907,46 @@ __global__ __launch_bounds__(64 * W, 1) void k_sqp_rti_rowpar(KParams P, KArgs a
                         Lp[j] = y;
                         if constexpr (j + 1 < NX) mst_trsv<NX, NU, j>(Lp, K[j], y);
                     });
+                    double Q[NX];
+#pragma unroll
+                    for (int c = 0; c < NX; c++) Q[c] = 0.0;
+                    mst_rowdot<NX, NU>(Q, Lp, Lp);
                     const double cv = mst_vdot<NX, NU>(ti, ph, Gr);  // c_i = t_i + Gam_i phat_{i+1}
                     if (is_x) {
 #pragma unroll
-                        for (int c = 0; c < NX; c++) sY[((size_t)i * NX + xi) * NX + c] = Lp[c];
+                        for (int c = 0; c < NX; c++) sQ[((size_t)i * NX + xi) * NX + c] = Q[c];
                         sCv[i * NX + xi] = cv;
                         sPh[i * NX + xi] = ph;
                     }
                     if (i >= 1) {
-                        // Phat_i = P_i + (Phi_i Y)(Phi_i Y)',  phat_i = pbar_i + Phi_i (Q_i c_i + phat_{i+1})
-                        double Wr[NX];
+                        // Phat_i = P_i + Phi_i Q_i Phi_i',  phat_i = pbar_i + Phi_i (Q_i c_i + phat_{i+1})
+                        double T[NX];
 #pragma unroll
                         for (int c = 0; c < NX; c++) {
-                            Wr[c] = 0.0;
+                            T[c] = 0.0;
                             Ph[c] = sP[((size_t)i * NX + xi) * NX + c];
                         }
-                        mst_rowmul<NX, NU>(Wr, Fr, Lp);  // W = Phi Y
-                        mst_rowdot<NX, NU>(Ph, Wr, Wr);  // Phat_i = P_i + W W'
-                        lds_fence();  // (Y_i rows stored)
-                        const double w = ph + qmul(i, cv, Lp);
+                        mst_rowdot<NX, NU>(T, Q, Fr);  // T = Q Phi'
+                        mst_rowmul<NX, NU>(Ph, Fr, T);  // Phat_i = P_i + Phi T
+                        const double w = mst_vdot<NX, NU>(ph, cv, Q);
                         ph = mst_vdot<NX, NU>((double)seg_lds[SegL.SUM_PB + i * NX + xi], w, Fr);
                     }
                 }
-                lds_fence();  // (Y_i, c_i, phat_{i+1} of every lane stored)
+                lds_fence();  // (Q_i, c_i, phat_{i+1} of every lane stored)
                 // forward: s_0 = 0; lam_{i+1} = Q_i (Phi_i' s_i + c_i) + phat_{i+1}; s_{i+1} = Phi_i' s_i + Gam_i lam_{i+1} + t_i
                 double sv = 0.0;
                 float* const sl = seg_lds + SegL.SL;
                 for (int i = 0; i <= Sg - 2; i++) {
-                    double Fc[NX], Gr[NX], Yr[NX];
+                    double Fc[NX], Gr[NX], Qr[NX];
 #pragma unroll
                     for (int l = 0; l < NX; l++) {
                         Fc[l] = (double)seg_lds[SegL.SUM_PHI + (i * NX + l) * NX + xi];
-                        Yr[l] = sY[((size_t)i * NX + xi) * NX + l];
+                        Qr[l] = sQ[((size_t)i * NX + xi) * NX + l];
                     }
                     ldrow(i, SegL.SUM_GAM, Gr);
                     const double fs = mst_vdot<NX, NU>(0.0, sv, Fc);
                     const double v = fs + sCv[i * NX + xi];
-                    const double lam = sPh[i * NX + xi] + qmul(i, v, Yr);
+                    const double lam = mst_vdot<NX, NU>(sPh[i * NX + xi], v, Qr);
                     sv = mst_vdot<NX, NU>(fs + (double)seg_lds[SegL.SUM_T + i * NX + xi], lam, Gr);
                     if (is_x) {
                         sl[(i + 1) * 2 * NX + xi] = (float)sv;

@@ -130,12 +130,6 @@ __device__ __forceinline__ void mst_rowmul_lt(double (&acc)[NX], const double (&
     else mst_rowmul_lt_11_4(acc, a, b);
 }
 template <int NX, int NU>
-__device__ __forceinline__ void rowmul_f32(float (&acc)[NX], const float (&a)[NX], const float (&b)[NX])
-{
-    if constexpr (NX == 7 && NU == 2) rowmul_f32_7_2(acc, a, b);
-    else rowmul_f32_11_4(acc, a, b);
-}
-template <int NX, int NU>
 __device__ __forceinline__ void mst_rowdot(double (&acc)[NX], const double (&a)[NX], const double (&b)[NX])
 {
     if constexpr (NX == 7 && NU == 2) mst_rowdot_7_2(acc, a, b);

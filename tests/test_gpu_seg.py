@@ -152,3 +152,5 @@ def test_plan_defaults(built):
     assert h.plan(1025)[0] == "team" and h.plan(4096)[0] == "team"
     ht = BatchSolver("tric", 60, 64, params=default_params("tric", 60))
     assert ht.plan(64) == ("rowpar", 4, 6)
+    ho = BatchSolver("omni4", 40, 512, params=default_params("omni4", 40))
+    assert ho.plan(256)[0] == "rowpar" and ho.plan(300)[0] == "team"  # 357 registers: one wave per SIMD

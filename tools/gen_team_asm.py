@@ -123,19 +123,6 @@ def mst_rowmul_lt(n, off):
             f" const double (&b)[{n}])\n{{\n    asm(\"{body}\"\n        : {outs}\n        : {ins});\n}}\n")
 
 
-def rowmul_f32(n, off):
-    # fp32 acc[c] += bcast_{off+l}(b[c]) * a[l] (the segments' lam sensitivities Y = G' Phi, all columns in one block)
-    lines = ["s_nop 1"]
-    for l in range(n):
-        for c in range(n):
-            lines.append(f"v_fmac_f32_dpp %{c}, %{n + c}, %{2 * n + l} row_newbcast:{off + l}{M}")
-    outs = ", ".join(f'"+v"(acc[{c}])' for c in range(n))
-    ins = ", ".join([f'"v"(b[{c}])' for c in range(n)] + [f'"v"(a[{l}])' for l in range(n)])
-    body = "\\n\\t".join(lines)
-    return (f"__device__ __forceinline__ void rowmul_f32_{n}_{off}(float (&acc)[{n}], const float (&a)[{n}],"
-            f" const float (&b)[{n}])\n{{\n    asm(\"{body}\"\n        : {outs}\n        : {ins});\n}}\n")
-
-
 def mst_rowdot(n, off):
     # acc[c] (+|-)= bcast_{off+c}(b[m]) * a[m]: row r of A B' (lane off+c holds row c of B); operands acc, b, a
     out = []
@@ -215,7 +202,7 @@ def main():
         nv = nx + nu
         parts += [pg_block(nx, nu), mrow_pg_block(nx, nu), chol_update(nx, nu),
                   dot_f32(nx, nu, f"dot_x_{nx}_{nu}"), dot_f32(nv, 0, f"dot_v_{nx}_{nu}"),
-                  mst_rowmul(nx, nu), mst_rowmul_lt(nx, nu), rowmul_f32(nx, nu), mst_rowdot(nx, nu), mst_chol(nx, nu), mst_trsv(nx, nu), mst_vdot(nx, nu)]
+                  mst_rowmul(nx, nu), mst_rowmul_lt(nx, nu), mst_rowdot(nx, nu), mst_chol(nx, nu), mst_trsv(nx, nu), mst_vdot(nx, nu)]
     parts += ["}  // namespace nmpc", ""]
     with open(OUT, "w") as fh:
         fh.write("\n".join(parts))
