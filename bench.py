@@ -182,17 +182,17 @@ def hbm_block(pmc, src, traffic, cbytes, t_k, groups=1):
                     "pmc_over_compulsory": round(traffic / cbytes, 1) if cbytes else None, "pmc_source": src,
                     "includes_mall_hits": True})
     if pmc and pmc.get("ea_rdreq"):
-        # the L2's memory-side requests, sized by tools/ubench_mall.hip (read requests 128 B, write requests 64 B:
-        # 8.00 read requests per KiB streamed, profiles/<round>/pmc/mall_calibration.json): a second, independent
-        # count of the same L2<->fabric bytes. The _DRAM-tagged share is 1.0 for an Infinity-Cache-resident table
-        # as well, so it cannot separate MALL hits from DRAM reads on gfx950
+        # the L2's memory-side read requests, sized by tools/ubench_mall.hip (128 B each: 8.00 per KiB streamed,
+        # profiles/<round>/pmc/mall_calibration.json): a second, independent count of the read bytes beside
+        # 2 x FETCH_SIZE. Write requests are counted, not sized (partial-sector stores make them smaller than the
+        # 64 B of the calibration's full-line fill). The _DRAM-tagged share is 1.0 for an Infinity-Cache-resident
+        # table as well, so it cannot separate MALL hits from DRAM reads on gfx950
         g = groups if groups else 1
         rd, rdd = pmc["ea_rdreq"], pmc.get("ea_rdreq_dram")
         wr, wrd = pmc.get("ea_wrreq"), pmc.get("ea_wrreq_dram")
-        ea = g * (rd * 128 + (wr or 0) * 64)
-        out["ea_bytes_per_step"] = ea
-        out["ea_GBs"] = round(ea / t_k / 1e9, 1)
-        out["ea_frac"] = round(ea / t_k / 1e9 / HBM_PEAK_GBS, 4)
+        out["ea_read_bytes_per_step"] = g * rd * 128
+        out["ea_read_GBs"] = round(g * rd * 128 / t_k / 1e9, 1)
+        out["ea_write_requests_per_step"] = g * wr if wr is not None else None
         out["dram_destined_share"] = {"read": round(rdd / rd, 4) if rdd is not None else None,
                                       "write": round(wrd / wr, 4) if wr and wrd is not None else None}
         cal, csrc = _profile_json("pmc/mall_calibration.json")
