@@ -366,6 +366,8 @@ def main():
     gather = args.gather or (args.config == "mixed" and world > 1)
     # weak scaling: the global fleet holds B x world robots of each model; this rank owns the contiguous
     # shard [rank*B, (rank+1)*B) of it (sharding.shard_range), no collective on the solve path
+    if args.groups is None and os.environ.get("NMPC_BENCH_GROUPS"):  # A/B runs (tools/ab_env.py variants)
+        args.groups = int(os.environ["NMPC_BENCH_GROUPS"])
     groups = cfg.get("groups", 1) if args.groups is None else args.groups
     node = FleetNode(models, cfg["N"], DEFAULT_SEED + cfg["idx"], dev, rank=rank, world=world, gather=gather,
                      groups=groups, decoupled=False if args.joined else None, renew=not args.no_renew,
