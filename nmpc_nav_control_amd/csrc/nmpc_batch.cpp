@@ -47,6 +47,7 @@ struct nmpc_batch {
     // concurrently with the team kernel on the caller's stream for the rest (DESIGN.md "Hybrid launch")
     int hybrid_h = 0, hybrid_cap = 1024;
     int* hyb_n = nullptr;        // [1] robots taken by the segmented part (device)
+    int rec_layout = -1;         // record layout of the last launch (schedule(): 1 = the team kernel's split planes)
     hipStream_t aux = nullptr;
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
 };
@@ -172,6 +173,8 @@ bool rowpar_ok(const nmpc_batch* b, KArgs& a, int mode)
     return rowpar_lds_bytes<M>(b->prm.N, mode, S) <= 65536;
 }
 
+__global__ void k_forget_warm(unsigned char* warm, const unsigned char* mask, int B);
+
 // Team placement before a team-kernel launch (schedule.hip); fills a.order / a.iter_key
 hipError_t schedule(nmpc_batch* b, KArgs& a, int mode, hipStream_t s)
 {
@@ -183,12 +186,24 @@ hipError_t schedule(nmpc_batch* b, KArgs& a, int mode, hipStream_t s)
     default: a.rowpar = rowpar_ok<Tric3>(b, a, mode); break;
     }
     if (a.rowpar) a.rowpar = (a.B <= 256) ? 4 : b->rowpar_w;  // waves per robot
+    // the two kernels keep the records of the 9-slot single-direction models in different layouts (the team
+    // kernel's split core / bound planes, TeamRec::SPLIT): when a handle switches kernel the multipliers in its
+    // records are unreadable to the other one, so every robot's next solve starts cold
+    const int rec_layout = (!a.rowpar && b->prm.model != NMPC_MODEL_OMNI4AMR && b->kp.ipm == NMPC_IPM_SINGLE) ? 1 : 0;
+    if (b->rec_layout >= 0 && b->rec_layout != rec_layout) {
+        hipLaunchKernelGGL(k_forget_warm, dim3((b->capacity + 255) / 256), dim3(256), 0, s, b->warm,
+                           (const unsigned char*)nullptr, b->capacity);
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    b->rec_layout = rec_layout;
     if (a.rowpar) return hipSuccess;  // one robot per wave: nothing to place
     a.dense = ((a.B + 3) / 4 > b->n_simd) ? 1 : 0;  // 4 teams per wave
     // small batches leave most of the chip idle: one wave per robot, whose spare rows integrate P0's stages
     a.split = (!a.dense && a.B <= b->split_max) ? 1 : 0;
     if (a.split) return hipSuccess;  // one robot per wave: nothing to place
-    if (b->hybrid_h > 0 && b->kp.ipm == NMPC_IPM_SINGLE && !a.segs && b->hyb_n) {
+    // (the hybrid launch mixes the kernels in one tick: only where they share the record layout, omni4)
+    if (b->hybrid_h > 0 && b->kp.ipm == NMPC_IPM_SINGLE && !a.segs && b->hyb_n && rec_layout == 0) {
         a.hyb_role = 1;  // launch() adds the segmented part on the aux stream
         a.hyb_n = b->hyb_n;
         a.order = b->order;

@@ -90,6 +90,9 @@ constexpr int kStampItsC = 0;
 // Mehrotra's predictor-corrector (P1 + F0 + C1 + F1 sweeps)
 // zeros: the source of a cold robot's warm-start multiplier loads (load_l in P0)
 __device__ float g_zero4[4];
+// split records (TeamRec::SPLIT): the bound pair of a slot without a bound -- TL TU LL LU | LB UB -- as P0 writes
+// it for bounded slots outside their stage range (kFar slacks and bounds, zero multipliers)
+__device__ __attribute__((aligned(16))) float g_rec_sentinel[8] = {kFar, kFar, 0.0f, 0.0f, -kFar, kFar, 0.0f, 0.0f};
 
 // MODE is a template parameter: kModeSolve, kModeRun, or kModeRunPath (run mode with the in-kernel path march,
 // a.segs set). As runtime arguments their branches inside P0's stage loop (reference unwrap, yref or pose-reference
@@ -146,6 +149,15 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a)
     // a record nobody reads (slot 15 of the robot's stage-N block: the idle slot of every model), the target of
     // stores that lanes without work issue unconditionally
     float* const tdummy = a.scratch + (size_t)inst * (N + 1) * KS + (size_t)N * KS + 15 * rec_lane<RSS, QM>();
+    // split records (R::SPLIT, TeamRec): this lane's core and bound plane entries of stage 0 (stage k: + k CS,
+    // + k kb) in the robot's record region; slots without a bound (and idle slots) read the sentinel pair with
+    // stride 0; the dummy pair is tdummy (past the planes)
+    constexpr bool SPL = R::SPLIT;
+    float* const pc0 = a.scratch + (size_t)inst * (N + 1) * KS + (lv ? r : 0) * R::CW;
+    float* const pb0 = has_b ? a.scratch + (size_t)inst * (N + 1) * KS + (size_t)(N + 1) * R::CS +
+                                   (is_u ? r : NU + (cx >= 0 ? cx : 0)) * R::CW
+                             : g_rec_sentinel;
+    const int kb = has_b ? R::BS : 0;
     // this lane's DZ in the dense plane after the records: dzbase + k * 16 (every lane its own float)
     float* const dzbase = a.scratch + (size_t)a.sstride * (N + 1) * KS + (size_t)inst * (N + 1) * 16 + r;
     // IPM warm start: the bound multipliers of the robot's previous successful solve are still in its records
@@ -259,7 +271,8 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a)
                 const int kt = kk < len_a ? kk : (len_a > 0 ? len_a - 1 : 0);
                 v.tq = a.traj[((size_t)kt * 3 + r) * Bn + inst];
             }
-            v.l = warm ? *reinterpret_cast<const float2*>(tbase + (size_t)kk * KS + rec_off<RS, QM>(R::LL))
+            v.l = warm ? *reinterpret_cast<const float2*>(SPL ? pb0 + (size_t)kk * kb + 2
+                                                              : tbase + (size_t)kk * KS + rec_off<RS, QM>(R::LL))
                        : make_float2(0.0f, 0.0f);
         };
         In cur, nxt;
@@ -348,7 +361,9 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a)
     // used under the team's warm flag is issued under that lane mask, and the compiler's waits for every later load
     // of the loop then drain the whole memory counter)
     auto load_l = [&](int k) -> float2 {
-        const float* const src = warm ? tbase + (size_t)(k <= N ? k : N) * KS + rec_off<RS, QM>(R::LL) : g_zero4;
+        const int kk = k <= N ? k : N;
+        const float* const src = warm ? (SPL ? pb0 + (size_t)kk * kb + 2 : tbase + (size_t)kk * KS + rec_off<RS, QM>(R::LL))
+                                      : g_zero4;
         return *reinterpret_cast<const float2*>(src);
     };
     // One stage of the serial pass: reference (run mode: unwrap + pad), cost gradient, bounds / slacks /
@@ -430,6 +445,9 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a)
         else if (lv) rec_store_range<0, RSS, RS, QM>(tbase + (size_t)k * KS, rec);
 #else
         // 9-slot teams: the idle lanes all store into the team's dummy record (one record's bytes, not seven)
+        else if constexpr (SPL)
+            split_store<R, 0, R::GR + 1, RS>(lv ? pc0 + (size_t)k * R::CS : tdummy,
+                                             (lv && has_b) ? pb0 + (size_t)k * kb : tdummy + R::CW, rec);
         else rec_store_range<0, RSS, RS, QM>(lv ? tbase + (size_t)k * KS : tdummy, rec);
 #endif
         if constexpr (kDzPlane) dzbase[(size_t)k * 16] = 0.0f;  // P1 of iteration 0 applies a zero step
@@ -584,25 +602,26 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a)
     // converged teams) re-read one fixed record instead; past k1 the pointer stays on k1.
     // P1's loads of one stage: its record fields and (DZ plane) the lane's DZ; dz points at the plane entry of
     // the stage whose record p points at (p - tbase = k KS <=> dz - dzbase = 16 k)
-    auto p1_load = [&](const float* p, float (&v)[RS]) {
-        rec_load_range<R::P1L0, R::P1L1, RS, QM>(p, v);
-        if constexpr (kDzPlane) v[R::DZ] = dzbase[(p - tbase) / KS * 16];
+    auto p1_load = [&](int kk, float (&v)[RS]) {
+        if constexpr (SPL) split_load<R, R::P1L0, R::P1L1, RS>(pc0 + (size_t)kk * R::CS, pb0 + (size_t)kk * kb, v);
+        else rec_load_range<R::P1L0, R::P1L1, RS, QM>(tbase + (size_t)kk * KS, v);
+        if constexpr (kDzPlane) v[R::DZ] = dzbase[(size_t)kk * 16];
     };
     auto sweep = [&](int k0, int k1, int dir, bool ld, auto&& body) {  // 2 buffers (compute-heavy P1)
-        const ptrdiff_t step = ld ? (ptrdiff_t)KS * dir : 0;
-        const float* p = tbase + (size_t)k0 * KS;
+        const int sd = ld ? dir : 0;  // stage step of this lane's loads (0: a lane that does not sweep)
+        int kp = k0;
         float ra[RS], rb[RS];
-        p1_load(p, ra);
+        p1_load(kp, ra);
         for (int k = k0;; k += 2 * dir) {
-            const float* p1 = (k == k1) ? p : p + step;
-            p1_load(p1, rb);
+            const int kp1 = (k == k1) ? kp : kp + sd;
+            p1_load(kp1, rb);
             body(k, ra);
             if (k == k1) break;
-            const float* p2 = (k + dir == k1) ? p1 : p1 + step;
-            p1_load(p2, ra);
+            const int kp2 = (k + dir == k1) ? kp1 : kp1 + sd;
+            p1_load(kp2, ra);
             body(k + dir, rb);
             if (k + dir == k1) break;
-            p = p2;
+            kp = kp2;
         }
     };
     // D buffers: buf[i] holds stage k + i*dir while the loop is at k; after body(k + i*dir) it is refilled with
@@ -610,21 +629,22 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a)
     auto sweepd = [&](auto dc, auto f0c, auto fc, int k0, int k1, int dir, bool ld, auto&& body) {
         constexpr int D = decltype(dc)::value;
         constexpr int F0 = decltype(f0c)::value, F = decltype(fc)::value;  // floats [F0, F) this sweep reads
-        const ptrdiff_t step = ld ? (ptrdiff_t)KS * dir : 0;
+        const int sd = ld ? dir : 0;
         float buf[D][RS];
-        const float* p = tbase + (size_t)k0 * KS;
+        int kp = k0;
         int kl = k0;
         // P1 with P1_D > 2 buffers also takes DZ from the plane (the light sweeps read only the prefix)
-        auto load = [&](const float* pp, float (&v)[RS]) {
-            rec_load_range<F0, F, RS, QM>(pp, v);
-            if constexpr (kDzPlane && F == R::P1L1) v[R::DZ] = dzbase[(pp - tbase) / KS * 16];
+        auto load = [&](int kk, float (&v)[RS]) {
+            if constexpr (SPL) split_load<R, F0, F, RS>(pc0 + (size_t)kk * R::CS, pb0 + (size_t)kk * kb, v);
+            else rec_load_range<F0, F, RS, QM>(tbase + (size_t)kk * KS, v);
+            if constexpr (kDzPlane && F == R::P1L1) v[R::DZ] = dzbase[(size_t)kk * 16];
         };
-        load(p, buf[0]);
+        load(kp, buf[0]);
         sfor<1, D>([&](auto ic) {
             constexpr int i = decltype(ic)::value;
-            p = (kl == k1) ? p : p + step;
+            kp = (kl == k1) ? kp : kp + sd;
             kl = (kl == k1) ? kl : kl + dir;
-            load(p, buf[i]);
+            load(kp, buf[i]);
         });
         for (int k = k0;; k += D * dir) {
             bool stop = false;
@@ -636,9 +656,9 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a)
                     stop = true;
                     return;
                 }
-                p = (kl == k1) ? p : p + step;
+                kp = (kl == k1) ? kp : kp + sd;
                 kl = (kl == k1) ? kl : kl + dir;
-                load(p, buf[i]);
+                load(kp, buf[i]);
             });
             if (stop) break;
         }
@@ -794,7 +814,11 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a)
             // s_waitcnt vmcnt(0) at the loop header of the ping-pong sweep (it waited for the stores just issued
             // and for the prefetch); unconditional, every wait in the loop is counted (tools/isa_waits.py)
             float* const pk = act ? tbase + (size_t)k * KS : tdummy;
-            if constexpr (MS) {
+            if constexpr (SPL) {
+                // core quad (LR LM Z) of the sweeping lanes; the bound quad only where a bound lives
+                split_store<R, 0, R::TL, RS>(act ? pc0 + (size_t)k * R::CS : tdummy, tdummy + R::CW, rc);
+                split_store<R, R::TL, R::TL + 4, RS>(tdummy, (act && bnd) ? pb0 + (size_t)k * kb : tdummy + R::CW, rc);
+            } else if constexpr (MS) {
                 // slack / multiplier quad only where a bound lives (elsewhere it holds the constant sentinel)
                 rec_store_range<R::TL, R::TL + 4, RS, QM>(bnd ? pk : tdummy, rc);
                 if constexpr (R::TL > 0) rec_store_range<0, R::TL, RS, QM>(pk, rc);
@@ -912,7 +936,7 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a)
                             if (r == j) my_lr = lrj;
                             y -= Lmj * lrj;
                         });
-                        if (ld && is_u) tbase[(size_t)k * KS + rec_off<RS, QM>(R::LR)] = my_lr;
+                        if (ld && is_u) (SPL ? pc0[(size_t)k * R::CS] : tbase[(size_t)k * KS + rec_off<RS, QM>(R::LR)]) = my_lr;
                         rc[R::LR] = my_lr;
                         pvc = is_x ? y : 0.0f;
                     }
@@ -993,8 +1017,8 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a)
                    // the compiler's wait after the sweep a full drain
                     const bool st = ld && valid;
                     if (corr && kDzPlane) *(st ? dzbase + (size_t)k * 16 : tdummy) = dz;
-                    else *(st ? tbase + (size_t)k * KS + (!corr ? rec_off<RS, QM>(R::DZA) : rec_off<RS, QM>(R::DZ))
-                              : tdummy) = dz;
+                    else *((st && !SPL) ? tbase + (size_t)k * KS + (!corr ? rec_off<RS, QM>(R::DZA) : rec_off<RS, QM>(R::DZ))
+                              : tdummy) = dz;  // (split records: single-direction only, DZ in the plane)
                 }
                 if (k < N) dxs = dyn(rc, valid ? dz : 0.0f);
             });
@@ -1047,7 +1071,7 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a)
 #pragma unroll
             for (int j = 0; j < EC; j++) {
                 const int kk = (k0 + j) <= N ? k0 + j : N;
-                zs[j] = tbase[(size_t)kk * KS + rec_off<RS, QM>(R::Z)];
+                zs[j] = SPL ? pc0[(size_t)kk * R::CS + R::Z] : tbase[(size_t)kk * KS + rec_off<RS, QM>(R::Z)];
                 vs[j] = *entry(k0 + j);
             }
 #pragma unroll

@@ -15,6 +15,8 @@ constexpr bool kDzPlane = true;
 constexpr bool kDzPlane = false;  // A/B: the round-2 layout, DZ a field of the lane record
 #endif
 
+constexpr bool rec_quad_major_v(int nv) { return nv > 12; }
+
 template <class M, bool SD = false>
 struct TeamRec {
     static constexpr int NX = M::NX, NU = M::NU, NV = NX + NU, NGV = M::NGV;
@@ -64,6 +66,24 @@ struct TeamRec {
     static_assert(NV <= 16, "a team holds at most 16 variables");
     static_assert(TL % 4 == 0, "bound quad aligned");
     static_assert(RSS <= RS && (kDzPlane || DZ < RSS) && (L2 || (RU < RSS && DZA < RSS)), "stored fields");
+    // Split records (team kernel, single-direction layout of the 9-slot models; NMPC_REC_FULL: the round-3 stage
+    // blocks for A/B): per robot a core plane [stage][NV slots][8] = LR LM[2] Z | GV[NGV] GR (pad) and a bound
+    // plane [stage][NBND bounded slots][8] = TL TU LL LU | LB UB (pad), in the robot's old record region. A slot
+    // without a bound keeps no bound fields in memory: its loads read the sentinel quad pair (kFar slacks and
+    // bounds, zero multipliers) and its stores go to the robot's dummy pair. A sweep's stage then touches
+    // 9 x 32 B of core plane (2.25 lines, stages contiguous) + 128 B of bound plane instead of 5 lines of 64-B
+    // records (DESIGN.md section 3 "Record stride").
+#ifndef NMPC_REC_FULL
+    static constexpr bool SPLIT = L2 && !rec_quad_major_v(NV);
+#else
+    static constexpr bool SPLIT = false;
+#endif
+    static constexpr int NBND = NU + M::NBX;
+    static constexpr int CW = 8;                 // floats per slot in either plane
+    static constexpr int CS = NV * CW;           // core floats per stage
+    static constexpr int BS = NBND * CW;         // bound floats per stage
+    static_assert(!SPLIT || (TL == 4 && LB == 8 && GV == 10 && GR == GV + NGV && NGV <= 3), "split record map");
+    static_assert(!SPLIT || (CS + BS) <= 16 * RSS, "split planes fit the robot's record region");
 };
 
 namespace {
@@ -308,6 +328,65 @@ __device__ __forceinline__ void rec_store_range(float* p, const float (&v)[RS])
         else if constexpr (L == 2) *reinterpret_cast<float2*>(pq) = make_float2(v[a], v[a + 1]);
         else pq[0] = v[a];
     });
+}
+
+// Split records (TeamRec::SPLIT): image fields [lo, hi) <-> memory floats [m0, m0 + hi - lo) of one plane, one access
+// per memory quad piece
+template <int LO, int HI, int M0, int RS, bool ST>
+__device__ __forceinline__ void split_piece(float* mb, float (&v)[RS])
+{
+    if constexpr (LO < HI) {
+        constexpr int ME = M0 + (HI - LO);
+        sfor<M0 / 4, (ME + 3) / 4>([&](auto qc) {
+            constexpr int q = decltype(qc)::value;
+            constexpr int a = (M0 > 4 * q) ? M0 : 4 * q, b = (ME < 4 * q + 4) ? ME : 4 * q + 4, L = b - a;
+            constexpr int f = LO + (a - M0);
+            float* pq = mb + a;
+            if constexpr (ST) {
+                if constexpr (L == 4) *reinterpret_cast<float4*>(pq) = make_float4(v[f], v[f + 1], v[f + 2], v[f + 3]);
+                else if constexpr (L == 2 && a % 2 == 0) *reinterpret_cast<float2*>(pq) = make_float2(v[f], v[f + 1]);
+                else {
+#pragma unroll
+                    for (int i = 0; i < L; i++) pq[i] = v[f + i];
+                }
+            } else {
+                if constexpr (L == 4) {
+                    const float4 t = *reinterpret_cast<const float4*>(pq);
+                    v[f] = t.x; v[f + 1] = t.y; v[f + 2] = t.z; v[f + 3] = t.w;
+                } else if constexpr (L == 2 && a % 2 == 0) {
+                    const float2 t = *reinterpret_cast<const float2*>(pq);
+                    v[f] = t.x; v[f + 1] = t.y;
+                } else {
+#pragma unroll
+                    for (int i = 0; i < L; i++) v[f + i] = pq[i];
+                }
+            }
+        });
+    }
+}
+template <int A, int B>
+constexpr int cmax() { return A > B ? A : B; }
+template <int A, int B>
+constexpr int cmin() { return A < B ? A : B; }
+// image [F0, F1) of a split record: core plane entry pc (LR LM Z at 0..3, GV.. GR at 4..), bound plane entry pb
+// (TL TU LL LU at 0..3, LB UB at 4..5)
+template <class R, int F0, int F1, int RS, bool ST>
+__device__ __forceinline__ void split_access(float* pc, float* pb, float (&v)[RS])
+{
+    split_piece<cmax<F0, 0>(), cmin<F1, 4>(), cmax<F0, 0>(), RS, ST>(pc, v);
+    split_piece<cmax<F0, 4>(), cmin<F1, 8>(), cmax<F0, 4>() - 4, RS, ST>(pb, v);
+    split_piece<cmax<F0, 8>(), cmin<F1, 10>(), cmax<F0, 8>() - 4, RS, ST>(pb, v);
+    split_piece<cmax<F0, R::GV>(), cmin<F1, R::GR + 1>(), cmax<F0, R::GV>() - R::GV + 4, RS, ST>(pc, v);
+}
+template <class R, int F0, int F1, int RS>
+__device__ __forceinline__ void split_load(const float* pc, const float* pb, float (&v)[RS])
+{
+    split_access<R, F0, F1, RS, false>(const_cast<float*>(pc), const_cast<float*>(pb), v);
+}
+template <class R, int F0, int F1, int RS>
+__device__ __forceinline__ void split_store(float* pc, float* pb, const float (&v)[RS])
+{
+    split_access<R, F0, F1, RS, true>(pc, pb, const_cast<float (&)[RS]>(v));
 }
 
 template <int RS, bool QM>
