@@ -186,10 +186,10 @@ hipError_t schedule(nmpc_batch* b, KArgs& a, int mode, hipStream_t s)
     default: a.rowpar = rowpar_ok<Tric3>(b, a, mode); break;
     }
     if (a.rowpar) a.rowpar = (a.B <= 256) ? 4 : b->rowpar_w;  // waves per robot
-    // the two kernels keep the records of the 9-slot single-direction models in different layouts (the team
-    // kernel's split core / bound planes, TeamRec::SPLIT): when a handle switches kernel the multipliers in its
-    // records are unreadable to the other one, so every robot's next solve starts cold
-    const int rec_layout = (!a.rowpar && b->prm.model != NMPC_MODEL_OMNI4AMR && b->kp.ipm == NMPC_IPM_SINGLE) ? 1 : 0;
+    // the two kernels keep tric's single-direction records in different layouts (the team kernel's split core /
+    // bound planes, TeamRec::SPLIT): when a handle switches kernel the multipliers in its records are unreadable
+    // to the other one, so every robot's next solve starts cold
+    const int rec_layout = (!a.rowpar && b->prm.model == NMPC_MODEL_TRIC3AMR && b->kp.ipm == NMPC_IPM_SINGLE) ? 1 : 0;
     if (b->rec_layout >= 0 && b->rec_layout != rec_layout) {
         hipLaunchKernelGGL(k_forget_warm, dim3((b->capacity + 255) / 256), dim3(256), 0, s, b->warm,
                            (const unsigned char*)nullptr, b->capacity);
@@ -202,7 +202,7 @@ hipError_t schedule(nmpc_batch* b, KArgs& a, int mode, hipStream_t s)
     // small batches leave most of the chip idle: one wave per robot, whose spare rows integrate P0's stages
     a.split = (!a.dense && a.B <= b->split_max) ? 1 : 0;
     if (a.split) return hipSuccess;  // one robot per wave: nothing to place
-    // (the hybrid launch mixes the kernels in one tick: only where they share the record layout, omni4)
+    // (the hybrid launch mixes the kernels in one tick: only where they share the record layout, diff and omni4)
     if (b->hybrid_h > 0 && b->kp.ipm == NMPC_IPM_SINGLE && !a.segs && b->hyb_n && rec_layout == 0) {
         a.hyb_role = 1;  // launch() adds the segmented part on the aux stream
         a.hyb_n = b->hyb_n;

@@ -66,15 +66,17 @@ struct TeamRec {
     static_assert(NV <= 16, "a team holds at most 16 variables");
     static_assert(TL % 4 == 0, "bound quad aligned");
     static_assert(RSS <= RS && (kDzPlane || DZ < RSS) && (L2 || (RU < RSS && DZA < RSS)), "stored fields");
-    // Split records (team kernel, single-direction layout of the 9-slot models; NMPC_REC_FULL: the round-3 stage
-    // blocks for A/B): per robot a core plane [stage][NV slots][8] = LR LM[2] Z | GV[NGV] GR (pad) and a bound
+    // Split records (team kernel, single-direction layout of tric; NMPC_REC_FULL: the 64-B stage blocks for A/B): per robot a core plane [stage][NV slots][8] = LR LM[2] Z | GV[NGV] GR (pad) and a bound
     // plane [stage][NBND bounded slots][8] = TL TU LL LU | LB UB (pad), in the robot's old record region. A slot
     // without a bound keeps no bound fields in memory: its loads read the sentinel quad pair (kFar slacks and
     // bounds, zero multipliers) and its stores go to the robot's dummy pair. A sweep's stage then touches
     // 9 x 32 B of core plane (2.25 lines, stages contiguous) + 128 B of bound plane instead of 5 lines of 64-B
     // records (DESIGN.md section 3 "Record stride").
+    // Taken where it wins (same-box A/B, profiles/r04/ab/split.txt): tric 3.60 -> 4.92 M it/s, mixed 4.76 -> 5.76 M
+    // (the working set drops under the Infinity Cache); diff loses 1 % (issue-bound: more load instructions and
+    // registers for 35 % less traffic), so diff keeps the 64-B records
 #ifndef NMPC_REC_FULL
-    static constexpr bool SPLIT = L2 && !rec_quad_major_v(NV);
+    static constexpr bool SPLIT = L2 && !rec_quad_major_v(NV) && M::ID == kTric;
 #else
     static constexpr bool SPLIT = false;
 #endif
