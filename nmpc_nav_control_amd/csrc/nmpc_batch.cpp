@@ -8,6 +8,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
+#include <mutex>
 #include <string>
 
 #include "nmpc_kernels.hpp"
@@ -48,6 +50,9 @@ struct nmpc_batch {
     int hybrid_h = 0, hybrid_cap = 1024;
     int* hyb_n = nullptr;        // [1] robots taken by the segmented part (device)
     int rec_layout = -1;         // record layout of the last launch (schedule(): 1 = the team kernel's split planes)
+    int rec_split = -1;          // diff's team-kernel record layout: -1 auto (rec_split_auto), 0 wide, 1 split
+    int dev = 0;                 // the handle's device
+    size_t rec_bytes = 0;        // its records' footprint in the registry below
     hipStream_t aux = nullptr;
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
 };
@@ -175,6 +180,28 @@ bool rowpar_ok(const nmpc_batch* b, KArgs& a, int mode)
 
 __global__ void k_forget_warm(unsigned char* warm, const unsigned char* mask, int B);
 
+// Live handles' record footprints per device (touched bytes of one sweep over their capacity, 64-B record layout):
+// diff's team kernel takes the split record planes when the device's resident records exceed 3/4 of the 256 MB
+// Infinity Cache. Alone on the device the metric fleet (4096 robots, 107 MB) keeps the wide records, 1.2 % faster
+// there (issue-bound); beside omni4 and tric (mixed: 272 MB) the split planes win 10 % (profiles/r04/ab/split.txt)
+std::mutex g_rec_mu;
+std::map<int, size_t> g_rec_bytes;
+constexpr size_t kRecSplitBytes = (size_t)192 << 20;
+
+size_t rec_footprint(const nmpc_batch* b)
+{
+    const size_t slots = b->prm.model == NMPC_MODEL_OMNI4AMR ? 16 : 9;  // omni4: quad-major, 16 slots of 80 B
+    const size_t rec = b->prm.model == NMPC_MODEL_DIFF2AMR ? 64 : 80;
+    return (size_t)b->capacity * (size_t)(b->prm.N + 1) * (slots * rec + 64);
+}
+
+bool rec_split_auto(const nmpc_batch* b)
+{
+    std::lock_guard<std::mutex> lk(g_rec_mu);
+    const auto it = g_rec_bytes.find(b->dev);
+    return it != g_rec_bytes.end() && it->second > kRecSplitBytes;
+}
+
 // Team placement before a team-kernel launch (schedule.hip); fills a.order / a.iter_key
 hipError_t schedule(nmpc_batch* b, KArgs& a, int mode, hipStream_t s)
 {
@@ -189,7 +216,12 @@ hipError_t schedule(nmpc_batch* b, KArgs& a, int mode, hipStream_t s)
     // the two kernels keep tric's single-direction records in different layouts (the team kernel's split core /
     // bound planes, TeamRec::SPLIT): when a handle switches kernel the multipliers in its records are unreadable
     // to the other one, so every robot's next solve starts cold
-    const int rec_layout = (!a.rowpar && b->prm.model == NMPC_MODEL_TRIC3AMR && b->kp.ipm == NMPC_IPM_SINGLE) ? 1 : 0;
+    a.rec_split = 0;
+    if (!a.rowpar && b->kp.ipm == NMPC_IPM_SINGLE) {
+        if (b->prm.model == NMPC_MODEL_TRIC3AMR) a.rec_split = 1;
+        else if (b->prm.model == NMPC_MODEL_DIFF2AMR) a.rec_split = b->rec_split >= 0 ? b->rec_split : rec_split_auto(b);
+    }
+    const int rec_layout = a.rec_split;
     if (b->rec_layout >= 0 && b->rec_layout != rec_layout) {
         hipLaunchKernelGGL(k_forget_warm, dim3((b->capacity + 255) / 256), dim3(256), 0, s, b->warm,
                            (const unsigned char*)nullptr, b->capacity);
@@ -438,6 +470,7 @@ int nmpc_batch_create(const nmpc_model_params* prm, int capacity, nmpc_batch** o
     if (const char* v = std::getenv("NMPC_AMD_SEG")) b->seg = std::atoi(v);  // A/B: 0 = serial, S = S segments
     if (const char* v = std::getenv("NMPC_AMD_ROWPAR_W")) b->rowpar_w = std::atoi(v) == 1 ? 1 : 2;  // A/B
     if (const char* v = std::getenv("NMPC_AMD_HYBRID")) b->hybrid_h = std::atoi(v);  // A/B: 0 = off
+    if (const char* v = std::getenv("NMPC_AMD_REC_SPLIT")) b->rec_split = std::atoi(v);  // A/B: -1 auto, 0, 1
     if (const char* v = std::getenv("NMPC_AMD_HYBRID_CAP")) b->hybrid_cap = std::atoi(v);
     const int N = prm->N;
     const size_t S = (size_t)capacity;
@@ -466,6 +499,12 @@ int nmpc_batch_create(const nmpc_model_params* prm, int capacity, nmpc_batch** o
         nmpc_batch_destroy(b);
         return rc;
     }
+    b->dev = dev;
+    b->rec_bytes = rec_footprint(b);
+    {
+        std::lock_guard<std::mutex> lk(g_rec_mu);
+        g_rec_bytes[dev] += b->rec_bytes;
+    }
     *out = b;
     return NMPC_OK;
 }
@@ -473,6 +512,10 @@ int nmpc_batch_create(const nmpc_model_params* prm, int capacity, nmpc_batch** o
 int nmpc_batch_destroy(nmpc_batch* b)
 {
     if (!b) return NMPC_OK;
+    if (b->rec_bytes) {
+        std::lock_guard<std::mutex> lk(g_rec_mu);
+        g_rec_bytes[b->dev] -= b->rec_bytes;
+    }
     (void)hipFree(b->xbar);
     (void)hipFree(b->ubar);
     (void)hipFree(b->carried);

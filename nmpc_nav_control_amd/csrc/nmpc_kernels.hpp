@@ -58,6 +58,7 @@ struct KArgs {
                           // multipliers), or nullptr (cold start, nothing written)
     int dense;      // the launch has more waves than the device has SIMDs (selects the team kernel variant)
     int rowpar;     // 0: team kernel; W > 0: k_sqp_rti_rowpar with W waves per robot
+    int rec_split;  // team kernel, diff: split core / bound record planes (TeamRec::SPLIT_OK; tric always)
     int split;      // one 256-lane block per robot: P0's integrations spread over its 16 rows (4 waves, stage k on
                     // row k mod 16, joined by a block barrier); small batches
     int seg;        // k_sqp_rti_rowpar: horizon segments S (N % S == 0) whose Riccati sweeps run in parallel on S rows,

@@ -99,7 +99,7 @@ __device__ __attribute__((aligned(16))) float g_rec_sentinel[8] = {kFar, kFar, 0
 // loads, and a pose load from either LDS or global memory, i.e. a flat load) made the compiler's waits drain the
 // whole memory counter, the stage's record stores and the prefetched rows included
 constexpr int kModeRunPath = 2;
-template <class M, bool MS, bool SD, int MODE>
+template <class M, bool MS, bool SD, int MODE, bool SP>
 __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a)
 {
     constexpr int mode = MODE == kModeRunPath ? kModeRun : MODE;
@@ -152,7 +152,7 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a)
     // split records (R::SPLIT, TeamRec): this lane's core and bound plane entries of stage 0 (stage k: + k CS,
     // + k kb) in the robot's record region; slots without a bound (and idle slots) read the sentinel pair with
     // stride 0; the dummy pair is tdummy (past the planes)
-    constexpr bool SPL = R::SPLIT;
+    constexpr bool SPL = R::SPLIT_OK && SP;  // split record planes (TeamRec::SPLIT, KArgs::rec_split)
     float* const pc0 = a.scratch + (size_t)inst * (N + 1) * KS + (lv ? r : 0) * R::CW;
     float* const pb0 = has_b ? a.scratch + (size_t)inst * (N + 1) * KS + (size_t)(N + 1) * R::CS +
                                    (is_u ? r : NU + (cx >= 0 ? cx : 0)) * R::CW
@@ -1158,11 +1158,20 @@ hipError_t launch_sqp_rti_team(const KParams& P, const KArgs& a, int mode, hipSt
     auto go = [&](auto kern) { hipLaunchKernelGGL(kern, dim3(grid), dim3(block), lds, stream, P, as); };
     // compile-time mode (the kernel's MODE parameter)
     const int km = mode != kModeRun ? kModeSolve : (a.segs ? kModeRunPath : kModeRun);
+    auto pick2 = [&](auto msc, auto sdc, auto spc) {
+        constexpr bool ms = decltype(msc)::value, sd = decltype(sdc)::value, sp = decltype(spc)::value;
+        if (km == kModeRunPath) go(k_sqp_rti_team<M, ms, sd, kModeRunPath, sp>);
+        else if (km == kModeRun) go(k_sqp_rti_team<M, ms, sd, kModeRun, sp>);
+        else go(k_sqp_rti_team<M, ms, sd, kModeSolve, sp>);
+    };
+    // record layout: tric always split, diff per launch (a.rec_split), omni4 and Mehrotra never
     auto pick = [&](auto msc, auto sdc) {
-        constexpr bool ms = decltype(msc)::value, sd = decltype(sdc)::value;
-        if (km == kModeRunPath) go(k_sqp_rti_team<M, ms, sd, kModeRunPath>);
-        else if (km == kModeRun) go(k_sqp_rti_team<M, ms, sd, kModeRun>);
-        else go(k_sqp_rti_team<M, ms, sd, kModeSolve>);
+        using R = TeamRec<M, decltype(sdc)::value>;
+        if constexpr (R::SPLIT) pick2(msc, sdc, std::true_type{});
+        else if constexpr (R::SPLIT_OK) {
+            if (a.rec_split) pick2(msc, sdc, std::true_type{});
+            else pick2(msc, sdc, std::false_type{});
+        } else pick2(msc, sdc, std::false_type{});
     };
     using T = std::true_type;
     using F = std::false_type;

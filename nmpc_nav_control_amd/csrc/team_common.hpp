@@ -75,17 +75,22 @@ struct TeamRec {
     // Taken where it wins (same-box A/B, profiles/r04/ab/split.txt): tric 3.60 -> 4.92 M it/s, mixed 4.76 -> 5.76 M
     // (the working set drops under the Infinity Cache); diff loses 1 % (issue-bound: more load instructions and
     // registers for 35 % less traffic), so diff keeps the 64-B records
+    // SPLIT_OK: the layout exists for the model (diff, tric); SPLIT: tric always takes it. For diff the host picks
+    // per launch (KArgs::rec_split): wide records alone on the device (the metric: -1.2 % with split planes), split
+    // planes beside other resident fleets (mixed: 5.25 -> 5.76 M it/s; nmpc_batch.cpp rec_split_auto)
 #ifndef NMPC_REC_FULL
-    static constexpr bool SPLIT = L2 && !rec_quad_major_v(NV) && M::ID == kTric;
+    static constexpr bool SPLIT_OK = L2 && !rec_quad_major_v(NV);
+    static constexpr bool SPLIT = SPLIT_OK && M::ID == kTric;
 #else
+    static constexpr bool SPLIT_OK = false;
     static constexpr bool SPLIT = false;
 #endif
     static constexpr int NBND = NU + M::NBX;
     static constexpr int CW = 8;                 // floats per slot in either plane
     static constexpr int CS = NV * CW;           // core floats per stage
     static constexpr int BS = NBND * CW;         // bound floats per stage
-    static_assert(!SPLIT || (TL == 4 && LB == 8 && GV == 10 && GR == GV + NGV && NGV <= 3), "split record map");
-    static_assert(!SPLIT || (CS + BS) <= 16 * RSS, "split planes fit the robot's record region");
+    static_assert(!SPLIT_OK || (TL == 4 && LB == 8 && GV == 10 && GR == GV + NGV && NGV <= 3), "split record map");
+    static_assert(!SPLIT_OK || (CS + BS) <= 16 * RSS, "split planes fit the robot's record region");
 };
 
 namespace {
