@@ -4,10 +4,12 @@
 # profiles/<round>/pmc/ (which bench.py reads), then microbenchmarks, capsule latency, a bench line per config and
 # the rocprofv3 kernel trace of the headline bench. Stops at the first failing step. Collect with
 # python tools/collect_round.py <tag> <round> <commit>.
-# usage: gpurun --timeout 1200 -- 'bash tools/final_profile.sh <tag> <round> [configs]'
+# usage: gpurun --timeout 1200 -- 'NMPC_SOURCE_COMMIT=<sha> bash tools/final_profile.sh <tag> <round> [configs]'
+#   (the snapshot on the box has no .git; the sha goes into the PMC summaries the bench lines cite)
 TAG=${1:-fin}; RND=${2:-r04}; shift 2
 CONFIGS=${@:-metric diff1024 omni4 tric mixed}
 OUT=$GRAFT_REPO_ROOT/gpurun_out
+export NMPC_SOURCE_COMMIT=${NMPC_SOURCE_COMMIT:-unknown}
 cd $GRAFT_REPO_ROOT
 mkdir -p $OUT
 ok() { local rc=$1; if [ $rc -ne 0 ]; then echo "STOP rc=$rc at $2"; exit $rc; fi; }

@@ -6,7 +6,8 @@ usage: python tools/pmc_summary.py gpurun_out/<tag> <config key, e.g. diff_N40_B
                                    [--commit <sha>] [--write]
   --last K   average only the last K dispatches of each kernel (the stationary tail of the bench's closed loop;
              default: all dispatches)
-  --commit   the commit the GPU run was made from (recorded as source_commit; default: this checkout's HEAD)
+  --commit   the commit the GPU run was made from (recorded as source_commit; default: this checkout's HEAD,
+             else $NMPC_SOURCE_COMMIT)
 
 Figures per launch of the solve kernel (for a mixed fleet: the sum over its per-model launches of one step):
   l2_fabric_bytes_per_launch = 2 x FETCH_SIZE + WRITE_SIZE (KB -> bytes). MI355X_MICROARCH.md "HBM": on gfx950
@@ -126,6 +127,8 @@ def main():
                                     text=True).stdout.strip()
         except OSError:
             commit = None
+    # the GPU box's snapshot has no .git: tools/final_profile.sh passes the commit in NMPC_SOURCE_COMMIT
+    commit = commit or os.environ.get("NMPC_SOURCE_COMMIT") or None
     rec = {"kernels": solve, "config": key, "l2_fabric_bytes_per_launch": 2 * fetch * 1024 + write * 1024,
            "fetch_size_kb": fetch, "write_size_kb": write,
            "tcc_hit_rate": hit / (hit + miss) if hit + miss > 0 else None,
