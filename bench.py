@@ -156,15 +156,17 @@ def roofline(fleets, node, kernel_ms, steps, step_s=None):
 
 
 def _kernel_label(fleet):
-    """The solve kernel a fleet's launches take (nmpc_batch_plan): the team kernel, or the row-parallel one with its
-    waves per robot and horizon segments."""
-    plan = getattr(fleet.solver, "plan", None)
+    """The solve kernel a fleet's run launches take (nmpc_batch_plan_ex, run mode): the team kernel with its record
+    layout, or the row-parallel one with its waves per robot and horizon segments."""
+    plan = getattr(fleet.solver, "plan_ex", None)
     if plan is None:
         return f"k_sqp_rti_{getattr(fleet.solver, 'kernel', 'team')}"
-    name, waves, segs = plan(fleet.B)
-    if name == "team":
-        return "k_sqp_rti_team"
-    return f"k_sqp_rti_rowpar ({waves} wave(s) per robot, " + (f"{segs} horizon segments)" if segs else "serial phases)")
+    p = plan(fleet.B, "run")
+    if p["kernel"] == "team":
+        return f"k_sqp_rti_team ({p['record_layout']} records)"
+    segs = p["segments"]
+    return (f"k_sqp_rti_rowpar ({p['waves_per_robot']} wave(s) per robot, " +
+            (f"{segs} horizon segments)" if segs else "serial phases)"))
 
 
 def hbm_block(pmc, src, traffic, cbytes, t_k, groups=1):
@@ -221,7 +223,7 @@ def cpu_baseline(fleets, sample, ticks, nthreads):
     time_1, solves_1 = 0.0, 0
     for f in fleets:
         S = f.B if sample <= 0 else min(sample, f.B)
-        o = Oracle(f.model, f.N)
+        o = Oracle(f.model, f.N, rule="batched")
         for _ in range(ticks):
             torch.cuda.synchronize()
             sn = f.snapshot()

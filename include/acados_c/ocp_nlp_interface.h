@@ -50,9 +50,11 @@ void ocp_nlp_out_set(ocp_nlp_config* config, ocp_nlp_dims* dims, ocp_nlp_out* ou
  *         "status" (int). */
 void ocp_nlp_get(ocp_nlp_solver* solver, const char* field, void* return_value_);
 /* Solver options (acados: ocp_nlp_solver_opts_set(config, capsule->nlp_opts, field, value)). Fields:
- *   "qp_warm_start" (int): 0 = HPIPM's cold start every solve (the reference's generated default,
- *                   scripts/diff/generate_c_code.py:68-74); 1 or 2 = warm-started bound
- *                   multipliers from the capsule's previous solve (this library's default for capsules);
+ *   "qp_warm_start" (int): 0 = HPIPM's cold start every solve (the reference's generated default and this
+ *                   library's capsule default, scripts/diff/generate_c_code.py:68-74);
+ *                   1 = acados' primal-only warm start, which starts cold here (the IPM has no separate primal
+ *                   start: its primal point is always the dynamics-feasible initial iterate); 2 = primal and dual:
+ *                   bound multipliers warm-started from the capsule's previous solve;
  *   "qp_iter_max"   (int >= 1): IPM iteration cap (50). Unknown fields are logged and ignored. */
 void ocp_nlp_solver_opts_set(ocp_nlp_config* config, void* opts_, const char* field, void* value);
 /* Dimension query: "x", "u", "y_ref" per stage (int). */

@@ -182,11 +182,32 @@ int nmpc_batch_state(nmpc_batch* b, float** xbar, float** ubar, float** carried,
  * instances between slots (a slot's multipliers belong to whatever instance solved there last). mask: device. */
 int nmpc_batch_forget_warm(nmpc_batch* b, int B, const unsigned char* mask, void* stream);
 
-/* Device pointers of the IPM warm-start state (qp_warm_start): warm [capacity] per-robot flags (1: the robot's
- * last solve succeeded) and the scratch records [scratch_bytes] that hold each robot's multipliers. With
- * nmpc_batch_state this is everything a solve reads from the handle, e.g. to checkpoint a fleet or to replay a
- * tick bit for bit. */
+/* Device pointers of the IPM warm-start state (qp_warm_start): warm [capacity] per-robot flags and the scratch
+ * records [scratch_bytes] that hold each robot's multipliers. A flag is 0 (the next solve starts cold) or the tag of
+ * the record layout its multipliers were stored in (NMPC_WARM_TAG_*): a solve reads them only when its launch uses
+ * the same layout, so a robot whose launches change kernel or layout (e.g. a handle whose batch crosses the
+ * row-parallel kernel's limit) starts cold on its own, and no other robot is touched. With nmpc_batch_state this
+ * is everything a solve reads from the handle, e.g. to checkpoint a fleet or to replay a tick bit for bit. */
+#define NMPC_WARM_TAG_WIDE 1     /* single-direction field order, one record per lane (team / row-parallel) */
+#define NMPC_WARM_TAG_SPLIT 2    /* the team kernel's split core / bound planes */
+#define NMPC_WARM_TAG_MEHROTRA 3 /* the Mehrotra rule's field order (NMPC_IPM_MEHROTRA) */
 int nmpc_batch_warm_state(nmpc_batch* b, unsigned char** warm, float** scratch, size_t* scratch_bytes);
+
+/* Record layout of the team kernel's single-direction scratch records, a per-handle choice fixed at create time
+ * and changed only by this call (never by other handles):
+ *   NMPC_REC_WIDE   one 64-B record per lane and stage (diff's default alone on a device: the metric fleet's
+ *                   107 MB fit the Infinity Cache, and the issue-bound kernel is 1.2 % faster with it);
+ *   NMPC_REC_SPLIT  core and bound planes (tric always; diff beside other resident fleets: the mixed fleet's
+ *                   272 MB drop under the 256 MB Infinity Cache, 5.25 -> 5.70 M it/s);
+ *   NMPC_REC_AUTO   the model's choice from this handle alone: tric SPLIT, omni4 WIDE, diff SPLIT when its own
+ *                   records (capacity x (N+1) x 640 B) exceed 192 MB, else WIDE.
+ * diff accepts all three; tric only SPLIT / AUTO and omni4 only WIDE / AUTO (NMPC_ERR_UNSUPPORTED otherwise). The
+ * environment variable NMPC_AMD_REC_SPLIT (0 / 1) overrides the create-time choice (A/B runs). Changing the layout
+ * leaves every robot's warm flag in place: each robot starts its next IPM cold because its tag no longer matches. */
+#define NMPC_REC_AUTO (-1)
+#define NMPC_REC_WIDE 0
+#define NMPC_REC_SPLIT 1
+int nmpc_batch_set_record_layout(nmpc_batch* b, int layout);
 
 /* The warm-start rule the solve kernels apply (the parameters after the NMPC_AMD_WARM / NMPC_AMD_WARM_ITER_MAX
  * overrides): a robot's flag is set after a solve iff warm && status == 0 && iterations < iter_max &&
@@ -194,9 +215,24 @@ int nmpc_batch_warm_state(nmpc_batch* b, unsigned char** warm, float** scratch, 
  * the parameters. Each output may be NULL. */
 int nmpc_batch_warm_rule(const nmpc_batch* b, int* warm, int* warm_iter_max, int* iter_max);
 
-/* The kernel a solve / run launch of B robots takes on this handle (the single-direction IPM; run_path launches
- * always take the team kernel): kernel 0 = k_sqp_rti_team (four robots per wave), 1 = k_sqp_rti_rowpar
- * (waves_per_robot waves per robot, `segments` horizon segments, 0 = the serial phases). Each output may be NULL. */
+/* The launch a call of B robots makes on this handle (nmpc_batch_plan_ex; nmpc_batch_plan: a solve launch):
+ *   kernel          0 = k_sqp_rti_team (four robots per wave), 1 = k_sqp_rti_rowpar;
+ *   waves_per_robot the row-parallel kernel's waves per robot (0 for the team kernel);
+ *   segments        its horizon segments (0 = the serial phases, or the team kernel);
+ *   record_layout   NMPC_REC_WIDE / NMPC_REC_SPLIT: the scratch record layout of the launch;
+ *   warm_tag        the NMPC_WARM_TAG_* the launch reads and writes (nmpc_batch_warm_state);
+ *   record_bytes    this handle's records touched per sweep over its capacity (the NMPC_REC_AUTO measure).
+ * mode: NMPC_PLAN_SOLVE (nmpc_batch_solve / _solve_iterate), NMPC_PLAN_RUN (nmpc_batch_run: run mode keeps the
+ * reference poses in LDS, which can push a long horizon off the row-parallel kernel) or NMPC_PLAN_RUN_PATH
+ * (nmpc_batch_run_path: always the team kernel). */
+#define NMPC_PLAN_SOLVE 0
+#define NMPC_PLAN_RUN 1
+#define NMPC_PLAN_RUN_PATH 2
+typedef struct nmpc_launch_plan {
+    int kernel, waves_per_robot, segments, record_layout, warm_tag;
+    size_t record_bytes;
+} nmpc_launch_plan;
+int nmpc_batch_plan_ex(const nmpc_batch* b, int B, int mode, nmpc_launch_plan* plan);
 int nmpc_batch_plan(const nmpc_batch* b, int B, int* kernel, int* waves_per_robot, int* segments);
 
 /* Bench / test harness: closed-loop plant step and path-reference regeneration for B robots

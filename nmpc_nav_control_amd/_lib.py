@@ -50,6 +50,12 @@ class FleetRenew(ctypes.Structure):
                 ("ev", c_void_p), ("ttl", c_void_p), ("reset", c_void_p), ("stats", c_void_p)]
 
 
+class LaunchPlan(ctypes.Structure):
+    """Mirror of nmpc_launch_plan (include/nmpc_amd/nmpc_batch.h)."""
+    _fields_ = [("kernel", ctypes.c_int), ("waves_per_robot", ctypes.c_int), ("segments", ctypes.c_int),
+                ("record_layout", ctypes.c_int), ("warm_tag", ctypes.c_int), ("record_bytes", ctypes.c_size_t)]
+
+
 class CodegenDesc(ctypes.Structure):
     """Mirror of nmpc_codegen_desc (include/nmpc_amd/nmpc_capsule.h)."""
     _fields_ = [("model", ctypes.c_int), ("N", ctypes.c_int), ("tf", ctypes.c_double),
@@ -75,13 +81,16 @@ class SolverCapsule(ctypes.Structure):
 BATCH_SYMBOLS = [
     "nmpc_model_dims", "nmpc_model_params_default", "nmpc_model_params_set_limits", "nmpc_batch_create",
     "nmpc_batch_destroy", "nmpc_batch_set_params", "nmpc_batch_get_params", "nmpc_batch_init_iterate",
-    "nmpc_batch_solve", "nmpc_batch_solve_iterate", "nmpc_batch_run", "nmpc_batch_run_path", "nmpc_batch_state", "nmpc_batch_warm_state", "nmpc_batch_warm_rule", "nmpc_batch_plan", "nmpc_batch_forget_warm", "nmpc_batch_set_kernel", "nmpc_batch_set_schedule",
+    "nmpc_batch_solve", "nmpc_batch_solve_iterate", "nmpc_batch_run", "nmpc_batch_run_path", "nmpc_batch_state", "nmpc_batch_warm_state", "nmpc_batch_warm_rule", "nmpc_batch_plan", "nmpc_batch_plan_ex", "nmpc_batch_set_record_layout", "nmpc_batch_forget_warm", "nmpc_batch_set_kernel", "nmpc_batch_set_schedule",
     "nmpc_fleet_sim_step", "nmpc_fleet_sim_step_renew", "nmpc_fleet_hash",
     "nmpc_last_error", "nmpc_version", "nmpc_path_discretize", "nmpc_codegen_default", "nmpc_capsule_new",
     "nmpc_capsule_delete", "nmpc_capsule_create", "nmpc_capsule_reset", "nmpc_capsule_update_params",
     "nmpc_capsule_solve", "nmpc_capsule_batch_solve", "nmpc_capsule_free", "nmpc_capsule_print_stats",
 ]
 KERNELS = {"team": 0}
+REC_LAYOUTS = {"auto": -1, "wide": 0, "split": 1}
+PLAN_MODES = {"solve": 0, "run": 1, "run_path": 2}
+WARM_TAGS = {1: "wide", 2: "split", 3: "mehrotra"}
 SCHEDULES = {"off": 0, "auto": 1, "sorted": 2, "interleaved": 3, "spread": 4}
 NLP_SYMBOLS = ["ocp_nlp_constraints_model_set", "ocp_nlp_cost_model_set", "ocp_nlp_out_get", "ocp_nlp_out_set",
                "ocp_nlp_get", "ocp_nlp_solver_opts_set", "ocp_nlp_dims_get_from_attr"]
@@ -128,6 +137,8 @@ def lib():
     L.nmpc_batch_warm_state.argtypes = [vp, ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.POINTER(ctypes.c_size_t)]
     L.nmpc_batch_warm_rule.argtypes = [vp, c_int_p, c_int_p, c_int_p]
     L.nmpc_batch_plan.argtypes = [vp, ctypes.c_int, c_int_p, c_int_p, c_int_p]
+    L.nmpc_batch_plan_ex.argtypes = [vp, i, i, ctypes.POINTER(LaunchPlan)]
+    L.nmpc_batch_set_record_layout.argtypes = [vp, i]
     L.nmpc_fleet_sim_step.argtypes = [vp, i, vp, vp, vp, vp, vp, vp, vp, vp, vp, i, vp]
     L.nmpc_fleet_sim_step_renew.argtypes = [vp, i, vp, vp, vp, vp, vp, vp, vp, vp, vp, ctypes.POINTER(FleetRenew), vp]
     L.nmpc_fleet_hash.argtypes = [ctypes.c_uint, ctypes.c_uint, ctypes.c_uint]

@@ -8,7 +8,8 @@ import ctypes
 
 import torch
 
-from ._lib import KERNELS, MODEL_IDS, SCHEDULES, FleetRenew, FleetStats, ModelParams, check, default_params, lib, model_dims
+from ._lib import (KERNELS, MODEL_IDS, PLAN_MODES, REC_LAYOUTS, SCHEDULES, FleetRenew, FleetStats, LaunchPlan,
+                   ModelParams, check, default_params, lib, model_dims)
 
 
 def _ptr(t, dtype=None, shape=None, name="argument"):
@@ -45,7 +46,7 @@ class BatchSolver:
 
     fused_stats = True  # fleet_sim_step_renew accumulates the solve statistics in its own launch (nmpc_fleet_stats)
 
-    def __init__(self, model, N, capacity, params=None, device="cuda", kernel=None):
+    def __init__(self, model, N, capacity, params=None, device="cuda", kernel=None, record_layout=None):
         self.model = model
         self.N = int(N)
         self.capacity = int(capacity)
@@ -62,6 +63,24 @@ class BatchSolver:
         self.kernel = "team"
         if kernel is not None:
             self.set_kernel(kernel)
+        if record_layout is not None:
+            self.set_record_layout(record_layout)
+
+    def set_record_layout(self, layout):
+        """The team kernel's scratch record layout of this handle: 'auto' (the model's choice from this handle
+        alone, fixed at create), 'wide' or 'split' (nmpc_batch_set_record_layout; diff has both, tric only split,
+        omni4 only wide). Robots whose multipliers sit in the other layout start their next IPM cold."""
+        check(lib().nmpc_batch_set_record_layout(self._h, REC_LAYOUTS[layout]), "nmpc_batch_set_record_layout")
+
+    def plan_ex(self, B, mode="solve"):
+        """The launch a call of B robots makes (nmpc_batch_plan_ex): dict with kernel ('team' / 'rowpar'),
+        waves_per_robot, segments, record_layout ('wide' / 'split'), warm_tag and record_bytes. mode: 'solve',
+        'run' or 'run_path'."""
+        p = LaunchPlan()
+        check(lib().nmpc_batch_plan_ex(self._h, int(B), PLAN_MODES[mode], ctypes.byref(p)), "nmpc_batch_plan_ex")
+        return dict(kernel="rowpar" if p.kernel else "team", waves_per_robot=p.waves_per_robot, segments=p.segments,
+                    record_layout="split" if p.record_layout else "wide", warm_tag=p.warm_tag,
+                    record_bytes=p.record_bytes)
 
     def set_kernel(self, kernel):
         """'team' (16-lane team per robot): the only kernel."""

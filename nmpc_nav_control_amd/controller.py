@@ -164,7 +164,8 @@ class NMPCNavControl:
 
     def solver_opts_set(self, field, value):
         """ocp_nlp_solver_opts_set(config, capsule->nlp_opts, field, &value) for the int fields "qp_warm_start"
-        (0: HPIPM's cold start every solve, the reference's generated default) and "qp_iter_max"."""
+        (0: HPIPM's cold start every solve, the reference's generated default; 1, acados' primal-only warm start,
+        starts cold too; 2: the capsule's multiplier warm start) and "qp_iter_max"."""
         v = ctypes.c_int(int(value))
         self._L.ocp_nlp_solver_opts_set(self._cfg, self._capsule.contents.nlp_opts, field.encode(), ctypes.byref(v))
 

@@ -55,6 +55,7 @@ struct nmpc_capsule_impl {
     // while the capsule still owns that slot, its last solve succeeded and no reset/create came in between
     std::uint64_t uid = 0;
     bool warm_ok = false;
+    unsigned char warm_tag = 0;  // the record layout tag of the launch that left them (NMPC_WARM_TAG_*)
     ocp_nlp_config config;
     ocp_nlp_dims dims;
     ocp_nlp_in in;
@@ -90,9 +91,12 @@ struct Blocks {  // float offsets of the arrays inside the I/O block for n capsu
     }
 };
 // Slot q of an engine keeps the scratch records (and so the bound multipliers) of the capsule that last solved
-// in it. owner[q] names that capsule; dev_warm[q] mirrors the handle's device warm flag of slot q (1 after a
-// successful solve, which is what the kernel leaves; 2 = unknown), so the flags only travel to the device when a
-// slot changes hands or a capsule was reset.
+// in it. owner[q] names that capsule; dev_warm[q] mirrors the handle's device warm flag of slot q (the launch's
+// NMPC_WARM_TAG_* after a successful solve, which is what the kernel leaves; kWarmUnknown = unknown), so the flags
+// only travel to the device when a slot changes hands or a capsule was reset. A capsule keeps the tag of the launch
+// that stored its multipliers: if its next launch takes another kernel or layout (e.g. the group grows past the
+// row-parallel kernel's limit), the kernel sees the mismatch and starts that capsule cold.
+constexpr unsigned char kWarmUnknown = 0xff;
 struct Engine {
     nmpc_batch* batch = nullptr;
     int cap = 0;
@@ -380,7 +384,7 @@ void solve_group(std::vector<nmpc_capsule_impl*>& cs, std::vector<Packed>& ps, c
         }
         for (int q = 0; q < (int)e.owner.size() && q < n; q++) {
             e.owner[q] = 0;
-            e.dev_warm[q] = 2;
+            e.dev_warm[q] = kWarmUnknown;
         }
     };
     {
@@ -415,7 +419,7 @@ void solve_group(std::vector<nmpc_capsule_impl*>& cs, std::vector<Packed>& ps, c
     bool flags_differ = false;
     for (int q = 0; q < n; q++) {
         const nmpc_capsule_impl* c = cs[idx[q]];
-        e.hwarm[q] = (e.owner[q] == c->uid && c->warm_ok) ? 1 : 0;
+        e.hwarm[q] = (e.owner[q] == c->uid && c->warm_ok) ? c->warm_tag : 0;
         flags_differ |= e.hwarm[q] != e.dev_warm[q];
     }
     {
@@ -450,6 +454,8 @@ void solve_group(std::vector<nmpc_capsule_impl*>& cs, std::vector<Packed>& ps, c
                      std::chrono::duration<double>(t1 - tb).count() * 1e3, tq * 1e3);
     int rule_warm = 0, rule_wmax = 0, rule_imax = 0;
     nmpc_batch_warm_rule(e.batch, &rule_warm, &rule_wmax, &rule_imax);
+    nmpc_launch_plan plan{};
+    nmpc_batch_plan_ex(e.batch, n, NMPC_PLAN_SOLVE, &plan);  // the tag this launch left in the flags
     std::vector<double*> xbs(n), ubs(n);  // failed solves keep their iterate (nullptr: skipped)
     for (int q = 0; q < n; q++) {
         nmpc_capsule_impl* c = cs[idx[q]];
@@ -468,8 +474,9 @@ void solve_group(std::vector<nmpc_capsule_impl*>& cs, std::vector<Packed>& ps, c
         // dev_warm mirrors the device flags exactly: warm && status == 0 && converged before the cap
         const bool conv = rule_warm && hst[q] == 0 && hit[q] < rule_imax && hit[q] <= rule_wmax;
         c->warm_ok = conv;
+        c->warm_tag = (unsigned char)plan.warm_tag;
         e.owner[q] = c->uid;
-        e.dev_warm[q] = conv ? 1 : 0;
+        e.dev_warm[q] = conv ? (unsigned char)plan.warm_tag : 0;
         xbs[q] = hst[q] == 0 ? c->xbar.data() : nullptr;
         ubs[q] = hst[q] == 0 ? c->ubar.data() : nullptr;
     }
@@ -635,8 +642,11 @@ void ocp_nlp_solver_opts_set(ocp_nlp_config* config, void* opts_, const char* fi
     if (!c || !field || !value) return;
     const int v = *static_cast<const int*>(value);
     if (!std::strcmp(field, "qp_warm_start")) {
-        c->prm.qp_warm_start = v ? 1 : 0;
-        if (!v) c->warm_ok = false;
+        // acados / HPIPM: 0 cold, 1 warm-start the primal QP variables, 2 primal and dual. The delta-form IPM here
+        // always starts its primal point from the dynamics-feasible initial iterate (there is no separate primal
+        // warm start), so 0 and 1 both start cold and only 2 warm-starts the bound multipliers
+        c->prm.qp_warm_start = (v == 2) ? 1 : 0;
+        if (v != 2) c->warm_ok = false;
     } else if (!std::strcmp(field, "qp_iter_max") && v >= 1) {
         c->prm.qp_iter_max = v;
     } else {

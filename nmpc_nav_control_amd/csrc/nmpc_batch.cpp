@@ -8,8 +8,6 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
-#include <map>
-#include <mutex>
 #include <string>
 
 #include "nmpc_kernels.hpp"
@@ -44,17 +42,19 @@ struct nmpc_batch {
     unsigned char* warm = nullptr;  // [capacity] the robot's last solve succeeded: its scratch records hold its
                                     // multipliers (IPM warm start)
     int* sorted = nullptr;       // [capacity] sort scratch
-    // hybrid launch (A/B, NMPC_AMD_HYBRID=H): in a team-kernel launch the robots whose last IPM count was >= H (at
-    // most hybrid_cap of them, the hardest first) run the segmented row-parallel kernel (one wave each) on aux,
-    // concurrently with the team kernel on the caller's stream for the rest (DESIGN.md "Hybrid launch")
+    // the team kernel's single-direction record layout (NMPC_REC_WIDE / NMPC_REC_SPLIT), fixed per handle: resolved
+    // at create time from this handle alone and changed only by nmpc_batch_set_record_layout
+    int rec_split = 0;
+#ifdef NMPC_HYBRID
+    // hybrid launch (A/B build only, -DNMPC_HYBRID, NMPC_AMD_HYBRID=H): in a team-kernel launch the robots whose last
+    // IPM count was >= H (at most hybrid_cap of them, the hardest first) run the segmented row-parallel kernel (one
+    // wave each) on aux, concurrently with the team kernel on the caller's stream for the rest (measured and not
+    // adopted: metric 4.16 -> 3.84 M it/s at H = 12, DESIGN.md "Hybrid launch")
     int hybrid_h = 0, hybrid_cap = 1024;
     int* hyb_n = nullptr;        // [1] robots taken by the segmented part (device)
-    int rec_layout = -1;         // record layout of the last launch (schedule(): 1 = the team kernel's split planes)
-    int rec_split = -1;          // diff's team-kernel record layout: -1 auto (rec_split_auto), 0 wide, 1 split
-    int dev = 0;                 // the handle's device
-    size_t rec_bytes = 0;        // its records' footprint in the registry below
     hipStream_t aux = nullptr;
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+#endif
 };
 
 namespace {
@@ -178,31 +178,40 @@ bool rowpar_ok(const nmpc_batch* b, KArgs& a, int mode)
     return rowpar_lds_bytes<M>(b->prm.N, mode, S) <= 65536;
 }
 
-__global__ void k_forget_warm(unsigned char* warm, const unsigned char* mask, int B);
-
-// Live handles' record footprints per device (touched bytes of one sweep over their capacity, 64-B record layout):
-// diff's team kernel takes the split record planes when the device's resident records exceed 3/4 of the 256 MB
-// Infinity Cache. Alone on the device the metric fleet (4096 robots, 107 MB) keeps the wide records, 1.2 % faster
-// there (issue-bound); beside omni4 and tric (mixed: 272 MB) the split planes win 10 % (profiles/r04/ab/split.txt)
-std::mutex g_rec_mu;
-std::map<int, size_t> g_rec_bytes;
+// Records one sweep of the team kernel touches over the handle's capacity in the wide layout (9 or 16 slots of
+// 64 / 80 B per stage, plus the 64-B DZ plane entry): the measure of NMPC_REC_AUTO. diff takes the split planes when
+// its own records exceed 3/4 of the 256 MB Infinity Cache. Alone on the device the metric fleet (4096 robots,
+// 107 MB) keeps the wide records, 1.2 % faster there (issue-bound); a fleet beside other models (the mixed config)
+// is set to SPLIT by its caller (fleet.py), where the split planes win 7 % (profiles/r04/ab/split.txt). The choice
+// depends on this handle only, so no other handle can change it.
 constexpr size_t kRecSplitBytes = (size_t)192 << 20;
 
 size_t rec_footprint(const nmpc_batch* b)
 {
     const size_t slots = b->prm.model == NMPC_MODEL_OMNI4AMR ? 16 : 9;  // omni4: quad-major, 16 slots of 80 B
-    const size_t rec = b->prm.model == NMPC_MODEL_DIFF2AMR ? 64 : 80;
+    const size_t rec = b->prm.model == NMPC_MODEL_OMNI4AMR ? 80 : 64;
     return (size_t)b->capacity * (size_t)(b->prm.N + 1) * (slots * rec + 64);
 }
 
-bool rec_split_auto(const nmpc_batch* b)
+int rec_layout_auto(const nmpc_batch* b)
 {
-    std::lock_guard<std::mutex> lk(g_rec_mu);
-    const auto it = g_rec_bytes.find(b->dev);
-    return it != g_rec_bytes.end() && it->second > kRecSplitBytes;
+    switch (b->prm.model) {
+    case NMPC_MODEL_TRIC3AMR: return NMPC_REC_SPLIT;
+    case NMPC_MODEL_OMNI4AMR: return NMPC_REC_WIDE;
+    default: return rec_footprint(b) > kRecSplitBytes ? NMPC_REC_SPLIT : NMPC_REC_WIDE;
+    }
 }
 
-// Team placement before a team-kernel launch (schedule.hip); fills a.order / a.iter_key
+// the warm-flag tag of a launch (NMPC_WARM_TAG_*): its multipliers' record layout and field order
+int warm_tag_of(const nmpc_batch* b, const KArgs& a)
+{
+    if (b->kp.ipm != NMPC_IPM_SINGLE) return NMPC_WARM_TAG_MEHROTRA;
+    return a.rec_split ? NMPC_WARM_TAG_SPLIT : NMPC_WARM_TAG_WIDE;
+}
+
+// Kernel choice, record layout and (team kernel) placement before a launch (schedule.hip); fills a.order /
+// a.iter_key. Every robot's warm flag carries the tag of the layout its multipliers sit in, so a launch whose
+// layout differs from a robot's last one starts that robot cold and leaves the others alone
 hipError_t schedule(nmpc_batch* b, KArgs& a, int mode, hipStream_t s)
 {
     a.iter_key = b->iter_key;
@@ -213,34 +222,23 @@ hipError_t schedule(nmpc_batch* b, KArgs& a, int mode, hipStream_t s)
     default: a.rowpar = rowpar_ok<Tric3>(b, a, mode); break;
     }
     if (a.rowpar) a.rowpar = (a.B <= 256) ? 4 : b->rowpar_w;  // waves per robot
-    // the two kernels keep tric's single-direction records in different layouts (the team kernel's split core /
-    // bound planes, TeamRec::SPLIT): when a handle switches kernel the multipliers in its records are unreadable
-    // to the other one, so every robot's next solve starts cold
-    a.rec_split = 0;
-    if (!a.rowpar && b->kp.ipm == NMPC_IPM_SINGLE) {
-        if (b->prm.model == NMPC_MODEL_TRIC3AMR) a.rec_split = 1;
-        else if (b->prm.model == NMPC_MODEL_DIFF2AMR) a.rec_split = b->rec_split >= 0 ? b->rec_split : rec_split_auto(b);
-    }
-    const int rec_layout = a.rec_split;
-    if (b->rec_layout >= 0 && b->rec_layout != rec_layout) {
-        hipLaunchKernelGGL(k_forget_warm, dim3((b->capacity + 255) / 256), dim3(256), 0, s, b->warm,
-                           (const unsigned char*)nullptr, b->capacity);
-        const hipError_t e = hipGetLastError();
-        if (e != hipSuccess) return e;
-    }
-    b->rec_layout = rec_layout;
+    // the row-parallel kernel keeps the wide single-direction records; the team kernel the handle's layout
+    a.rec_split = (!a.rowpar && b->kp.ipm == NMPC_IPM_SINGLE) ? b->rec_split : 0;
+    a.warm_tag = warm_tag_of(b, a);
     if (a.rowpar) return hipSuccess;  // one robot per wave: nothing to place
     a.dense = ((a.B + 3) / 4 > b->n_simd) ? 1 : 0;  // 4 teams per wave
     // small batches leave most of the chip idle: one wave per robot, whose spare rows integrate P0's stages
     a.split = (!a.dense && a.B <= b->split_max) ? 1 : 0;
     if (a.split) return hipSuccess;  // one robot per wave: nothing to place
-    // (the hybrid launch mixes the kernels in one tick: only where they share the record layout, diff and omni4)
-    if (b->hybrid_h > 0 && b->kp.ipm == NMPC_IPM_SINGLE && !a.segs && b->hyb_n && rec_layout == 0) {
+#ifdef NMPC_HYBRID
+    // (the hybrid launch mixes the kernels in one tick: only where they share the record layout)
+    if (b->hybrid_h > 0 && b->kp.ipm == NMPC_IPM_SINGLE && !a.segs && b->hyb_n && a.rec_split == 0) {
         a.hyb_role = 1;  // launch() adds the segmented part on the aux stream
         a.hyb_n = b->hyb_n;
         a.order = b->order;
         return launch_hybrid_order(b->iter_key, a.B, b->hybrid_h, b->hybrid_cap, b->order, b->hyb_n, s);
     }
+#endif
     int layout = b->sched;
     if (layout == NMPC_SCHED_AUTO) layout = a.dense ? NMPC_SCHED_SORTED : NMPC_SCHED_OFF;
     if (layout == NMPC_SCHED_OFF) return hipSuccess;
@@ -248,6 +246,7 @@ hipError_t schedule(nmpc_batch* b, KArgs& a, int mode, hipStream_t s)
     return launch_team_order(b->iter_key, a.B, layout, b->sorted, b->order, s);
 }
 
+#ifdef NMPC_HYBRID
 template <class M>
 hipError_t launch_hybrid(nmpc_batch* b, KArgs& a, int mode, hipStream_t s)
 {
@@ -273,11 +272,13 @@ hipError_t launch_hybrid(nmpc_batch* b, KArgs& a, int mode, hipStream_t s)
     if ((e = hipEventRecord(b->ev_join, b->aux)) != hipSuccess) return e;
     return hipStreamWaitEvent(s, b->ev_join, 0);
 }
+#endif
 
 hipError_t launch(nmpc_batch* b, KArgs& a, int mode, hipStream_t s)
 {
     const hipError_t e = schedule(b, a, mode, s);
     if (e != hipSuccess) return e;
+#ifdef NMPC_HYBRID
     if (a.hyb_role == 1) {
         switch (b->prm.model) {
         case NMPC_MODEL_DIFF2AMR: return launch_hybrid<Diff2>(b, a, mode, s);
@@ -285,6 +286,7 @@ hipError_t launch(nmpc_batch* b, KArgs& a, int mode, hipStream_t s)
         default: return launch_hybrid<Tric3>(b, a, mode, s);
         }
     }
+#endif
     switch (b->prm.model) {
     case NMPC_MODEL_DIFF2AMR: return launch_m<Diff2>(b, a, mode, s);
     case NMPC_MODEL_OMNI4AMR: return launch_m<Omni4>(b, a, mode, s);
@@ -348,7 +350,11 @@ int check_params(const nmpc_model_params* prm)
 extern "C" {
 
 const char* nmpc_last_error(void) { return g_err.c_str(); }
-const char* nmpc_version(void) { return "nmpc_amd 0.3 (team-per-instance DPP SQP-RTI, gfx950)"; }
+#ifdef NMPC_HYBRID
+const char* nmpc_version(void) { return "nmpc_amd 0.4 (team-per-instance DPP SQP-RTI, gfx950; A/B: hybrid launch)"; }
+#else
+const char* nmpc_version(void) { return "nmpc_amd 0.4 (team-per-instance DPP SQP-RTI, gfx950)"; }
+#endif
 
 int nmpc_model_dims(int model, int* nx, int* nu, int* ny, int* nbx, int* nbu, int* np)
 {
@@ -469,9 +475,10 @@ int nmpc_batch_create(const nmpc_model_params* prm, int capacity, nmpc_batch** o
     if (const char* v = std::getenv("NMPC_AMD_ROWPAR_MAX")) b->rowpar_max = std::atoi(v);  // A/B: 0 = never
     if (const char* v = std::getenv("NMPC_AMD_SEG")) b->seg = std::atoi(v);  // A/B: 0 = serial, S = S segments
     if (const char* v = std::getenv("NMPC_AMD_ROWPAR_W")) b->rowpar_w = std::atoi(v) == 1 ? 1 : 2;  // A/B
+#ifdef NMPC_HYBRID
     if (const char* v = std::getenv("NMPC_AMD_HYBRID")) b->hybrid_h = std::atoi(v);  // A/B: 0 = off
-    if (const char* v = std::getenv("NMPC_AMD_REC_SPLIT")) b->rec_split = std::atoi(v);  // A/B: -1 auto, 0, 1
     if (const char* v = std::getenv("NMPC_AMD_HYBRID_CAP")) b->hybrid_cap = std::atoi(v);
+#endif
     const int N = prm->N;
     const size_t S = (size_t)capacity;
     hipError_t e;
@@ -480,8 +487,13 @@ int nmpc_batch_create(const nmpc_model_params* prm, int capacity, nmpc_batch** o
     if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&props, dev) == hipSuccess &&
         props.multiProcessorCount > 0)
         b->n_simd = 4 * props.multiProcessorCount;
-    if ((e = hipMalloc(&b->hyb_n, sizeof(int))) != hipSuccess || (e = hipMemset(b->hyb_n, 0, sizeof(int))) != hipSuccess ||
-        (e = hipMalloc(&b->iter_key, sizeof(int) * S)) != hipSuccess ||
+#ifdef NMPC_HYBRID
+    if ((e = hipMalloc(&b->hyb_n, sizeof(int))) != hipSuccess || (e = hipMemset(b->hyb_n, 0, sizeof(int))) != hipSuccess) {
+        nmpc_batch_destroy(b);
+        return hip_err(e, "hipMalloc");
+    }
+#endif
+    if ((e = hipMalloc(&b->iter_key, sizeof(int) * S)) != hipSuccess ||
         (e = hipMalloc(&b->order, sizeof(int) * S)) != hipSuccess ||
         (e = hipMalloc(&b->sorted, sizeof(int) * S)) != hipSuccess ||
         (e = hipMemset(b->iter_key, 0, sizeof(int) * S)) != hipSuccess ||
@@ -499,12 +511,10 @@ int nmpc_batch_create(const nmpc_model_params* prm, int capacity, nmpc_batch** o
         nmpc_batch_destroy(b);
         return rc;
     }
-    b->dev = dev;
-    b->rec_bytes = rec_footprint(b);
-    {
-        std::lock_guard<std::mutex> lk(g_rec_mu);
-        g_rec_bytes[dev] += b->rec_bytes;
-    }
+    // the record layout: this handle's own choice (NMPC_REC_AUTO), fixed until nmpc_batch_set_record_layout
+    b->rec_split = rec_layout_auto(b);
+    if (const char* v = std::getenv("NMPC_AMD_REC_SPLIT"))  // A/B runs: 0 wide, 1 split (where the model has it)
+        if (prm->model == NMPC_MODEL_DIFF2AMR) b->rec_split = std::atoi(v) ? NMPC_REC_SPLIT : NMPC_REC_WIDE;
     *out = b;
     return NMPC_OK;
 }
@@ -512,10 +522,6 @@ int nmpc_batch_create(const nmpc_model_params* prm, int capacity, nmpc_batch** o
 int nmpc_batch_destroy(nmpc_batch* b)
 {
     if (!b) return NMPC_OK;
-    if (b->rec_bytes) {
-        std::lock_guard<std::mutex> lk(g_rec_mu);
-        g_rec_bytes[b->dev] -= b->rec_bytes;
-    }
     (void)hipFree(b->xbar);
     (void)hipFree(b->ubar);
     (void)hipFree(b->carried);
@@ -524,10 +530,12 @@ int nmpc_batch_destroy(nmpc_batch* b)
     (void)hipFree(b->order);
     (void)hipFree(b->sorted);
     (void)hipFree(b->warm);
+#ifdef NMPC_HYBRID
     (void)hipFree(b->hyb_n);
     if (b->ev_fork) (void)hipEventDestroy(b->ev_fork);
     if (b->ev_join) (void)hipEventDestroy(b->ev_join);
     if (b->aux) (void)hipStreamDestroy(b->aux);
+#endif
     delete b;
     return NMPC_OK;
 }
@@ -736,21 +744,56 @@ int nmpc_batch_forget_warm(nmpc_batch* b, int B, const unsigned char* mask, void
     return hip_err(hipGetLastError(), "forget_warm launch");
 }
 
-int nmpc_batch_plan(const nmpc_batch* b, int B, int* kernel, int* waves_per_robot, int* segments)
+int nmpc_batch_set_record_layout(nmpc_batch* b, int layout)
 {
     if (!b) return set_err(NMPC_ERR_ARG, "batch is NULL");
+    if (layout != NMPC_REC_AUTO && layout != NMPC_REC_WIDE && layout != NMPC_REC_SPLIT)
+        return set_err(NMPC_ERR_ARG, "layout must be NMPC_REC_AUTO, NMPC_REC_WIDE or NMPC_REC_SPLIT");
+    const int want = layout == NMPC_REC_AUTO ? rec_layout_auto(b) : layout;
+    if ((b->prm.model == NMPC_MODEL_TRIC3AMR && want != NMPC_REC_SPLIT) ||
+        (b->prm.model == NMPC_MODEL_OMNI4AMR && want != NMPC_REC_WIDE))
+        return set_err(NMPC_ERR_UNSUPPORTED, "this model's team kernel has one record layout (tric split, omni4 wide)");
+    b->rec_split = want;  // robots warm-started in the other layout start cold at their next solve (warm tags)
+    return NMPC_OK;
+}
+
+int nmpc_batch_plan_ex(const nmpc_batch* b, int B, int mode, nmpc_launch_plan* plan)
+{
+    if (!b || !plan) return set_err(NMPC_ERR_ARG, "NULL argument");
     if (B < 0 || B > b->capacity) return set_err(NMPC_ERR_ARG, "B out of range");
+    if (mode != NMPC_PLAN_SOLVE && mode != NMPC_PLAN_RUN && mode != NMPC_PLAN_RUN_PATH)
+        return set_err(NMPC_ERR_ARG, "mode must be NMPC_PLAN_SOLVE, NMPC_PLAN_RUN or NMPC_PLAN_RUN_PATH");
     KArgs a{};
     a.B = B;
+    // run_path launches carry the path segments (a.segs), which keep them on the team kernel
+    static const nmpc_path_segment kSeg{};
+    if (mode == NMPC_PLAN_RUN_PATH) a.segs = &kSeg;
+    const int km = mode == NMPC_PLAN_SOLVE ? kModeSolve : kModeRun;
     bool rp;
     switch (b->prm.model) {
-    case NMPC_MODEL_DIFF2AMR: rp = rowpar_ok<Diff2>(b, a, kModeSolve); break;
-    case NMPC_MODEL_OMNI4AMR: rp = rowpar_ok<Omni4>(b, a, kModeSolve); break;
-    default: rp = rowpar_ok<Tric3>(b, a, kModeSolve); break;
+    case NMPC_MODEL_DIFF2AMR: rp = rowpar_ok<Diff2>(b, a, km); break;
+    case NMPC_MODEL_OMNI4AMR: rp = rowpar_ok<Omni4>(b, a, km); break;
+    default: rp = rowpar_ok<Tric3>(b, a, km); break;
     }
-    if (kernel) *kernel = rp ? 1 : 0;
-    if (waves_per_robot) *waves_per_robot = rp ? (B <= 256 ? 4 : b->rowpar_w) : 0;
-    if (segments) *segments = rp ? a.seg : 0;
+    a.rowpar = rp ? 1 : 0;
+    a.rec_split = (!rp && b->kp.ipm == NMPC_IPM_SINGLE) ? b->rec_split : 0;
+    plan->kernel = rp ? 1 : 0;
+    plan->waves_per_robot = rp ? (B <= 256 ? 4 : b->rowpar_w) : 0;
+    plan->segments = rp ? a.seg : 0;
+    plan->record_layout = a.rec_split ? NMPC_REC_SPLIT : NMPC_REC_WIDE;
+    plan->warm_tag = warm_tag_of(b, a);
+    plan->record_bytes = rec_footprint(b);
+    return NMPC_OK;
+}
+
+int nmpc_batch_plan(const nmpc_batch* b, int B, int* kernel, int* waves_per_robot, int* segments)
+{
+    nmpc_launch_plan p;
+    const int rc = nmpc_batch_plan_ex(b, B, NMPC_PLAN_SOLVE, &p);
+    if (rc) return rc;
+    if (kernel) *kernel = p.kernel;
+    if (waves_per_robot) *waves_per_robot = p.waves_per_robot;
+    if (segments) *segments = p.segments;
     return NMPC_OK;
 }
 

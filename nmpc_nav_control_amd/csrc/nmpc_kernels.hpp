@@ -54,8 +54,9 @@ struct KArgs {
     // team placement (schedule.hip): team slot -> instance, or nullptr (slot i = instance i)
     const int* order;
     int* iter_key;  // [stride] resident: executed IPM iterations of the last solve, or nullptr
-    unsigned char* warm;  // [stride] resident: 1 if the robot's last solve succeeded (its records hold its
-                          // multipliers), or nullptr (cold start, nothing written)
+    unsigned char* warm;  // [stride] resident: the robot's last solve succeeded and its records hold its multipliers
+                          // in the layout tagged (NMPC_WARM_TAG_*), 0 otherwise; nullptr: cold start, nothing written
+    int warm_tag;   // this launch's record layout tag: a robot starts warm only if warm[inst] == warm_tag
     int dense;      // the launch has more waves than the device has SIMDs (selects the team kernel variant)
     int rowpar;     // 0: team kernel; W > 0: k_sqp_rti_rowpar with W waves per robot
     int rec_split;  // team kernel, diff: split core / bound record planes (TeamRec::SPLIT_OK; tric always)
@@ -63,9 +64,9 @@ struct KArgs {
                     // row k mod 16, joined by a block barrier); small batches
     int seg;        // k_sqp_rti_rowpar: horizon segments S (N % S == 0) whose Riccati sweeps run in parallel on S rows,
                     // joined by a master recursion over the segment boundaries; 0: the serial phases B / C
-    // hybrid launch (nmpc_batch.cpp): the robots of the first hyb_n[0] ranks of `order` (the hardest by last tick's
-    // IPM count) run the segmented row-parallel kernel on a second stream (role 2, at most hyb_cap blocks), the
-    // rest the team kernel (role 1, team slot t -> order[hyb_n[0] + t]); role 0: a plain launch
+    // hybrid launch (A/B build -DNMPC_HYBRID only, nmpc_batch.cpp): the robots of the first hyb_n[0] ranks of `order`
+    // (the hardest by last tick's IPM count) run the segmented row-parallel kernel on a second stream (role 2, at most
+    // hyb_cap blocks), the rest the team kernel (role 1, team slot t -> order[hyb_n[0] + t]); role 0: a plain launch
     const int* hyb_n;
     int hyb_role, hyb_cap;
 };
@@ -85,8 +86,10 @@ hipError_t launch_fleet_sim(const KParams& P, int B, int stride, float* path, fl
                             float* steer, const float* u0, const int* status, const float* carried, float* traj,
                             int* traj_len, int advance, const nmpc_fleet_renew* renew, hipStream_t stream);
 hipError_t launch_team_order(const int* key, int B, int layout, int* sorted, int* order, hipStream_t stream);
+#ifdef NMPC_HYBRID
 // sorted order (hardest first) plus nhard[0] = min(#robots with key >= H, cap): the hybrid launch's split
 hipError_t launch_hybrid_order(const int* key, int B, int H, int cap, int* order, int* nhard, hipStream_t stream);
+#endif
 hipError_t launch_path_discretize(int B, const nmpc_path_segment* segs, int seg_stride, const int* nseg,
                                   const double* nearest_u, double period, int num_poses, int holo, float* traj,
                                   double* traj64, hipStream_t stream);

@@ -112,6 +112,7 @@ hipError_t launch_team_order(const int* key, int B, int layout, int* sorted, int
     return hipGetLastError();
 }
 
+#ifdef NMPC_HYBRID
 hipError_t launch_hybrid_order(const int* key, int B, int H, int cap, int* order, int* nhard, hipStream_t stream)
 {
     if (B <= 0) return hipSuccess;
@@ -119,5 +120,6 @@ hipError_t launch_hybrid_order(const int* key, int B, int H, int cap, int* order
                        order, H, cap, nhard);
     return hipGetLastError();
 }
+#endif
 
 }  // namespace nmpc

@@ -156,9 +156,13 @@ __global__ __launch_bounds__(64 * W, 1) void k_sqp_rti_rowpar(KParams P, KArgs a
     constexpr int NX = M::NX, NU = M::NU, NV = R::NV, NGV = R::NGV, RS = R::RS, RSS = R::RSS;
     constexpr bool QM = rec_quad_major<NV>();
     constexpr int ROWS = 4 * W;
-    // hybrid launch (role 2): block i takes the robot of rank i of the order, for the first hyb_n[0] ranks
+#ifdef NMPC_HYBRID
+    // hybrid launch (A/B build, role 2): block i takes the robot of rank i of the order, for the first hyb_n[0] ranks
     if (a.hyb_role == 2 && (int)blockIdx.x >= a.hyb_n[0]) return;
     const int inst = (a.hyb_role == 2) ? a.order[blockIdx.x] : (int)blockIdx.x;
+#else
+    const int inst = (int)blockIdx.x;
+#endif
     if (inst >= a.B) return;
     const int tid = (int)threadIdx.x;
     const int wave = tid >> 6;
@@ -199,7 +203,7 @@ __global__ __launch_bounds__(64 * W, 1) void k_sqp_rti_rowpar(KParams P, KArgs a
     float* const wdz = dummy + (size_t)256 * 4 * KS + ((size_t)(inst & 255) * 4 + wave) * 16 + r;  // dummy DZ
     const bool w0 = wave == 0;
     float* const tdummy = rbase + (size_t)N * KS + 15 * rec_lane<RSS, QM>();  // nobody reads it
-    const bool warm = P.warm && a.warm && a.warm[inst] && !(a.reset && a.reset[inst]);
+    const bool warm = P.warm && a.warm && a.warm[inst] == a.warm_tag && !(a.reset && a.reset[inst]);
     RP_STAMP(0);
 
 #define XB(k, j) a.xbar[((size_t)(k) * NX + (j)) * S + inst]
@@ -1265,7 +1269,8 @@ __global__ __launch_bounds__(64 * W, 1) void k_sqp_rti_rowpar(KParams P, KArgs a
         if (a.status) a.status[inst] = status;
         if (a.qp_iter) a.qp_iter[inst] = it_done;
         if (a.iter_key) a.iter_key[inst] = it_done;
-        if (a.warm) a.warm[inst] = (P.warm && status == 0 && it_done < P.iter_max && it_done <= P.warm_iter_max) ? 1 : 0;
+        if (a.warm)
+            a.warm[inst] = (P.warm && status == 0 && it_done < P.iter_max && it_done <= P.warm_iter_max) ? a.warm_tag : 0;
         if (a.qp_res) {
 #pragma unroll
             for (int j = 0; j < 3; j++) a.qp_res[(size_t)j * Bn + inst] = exit_res[j];
@@ -1310,7 +1315,11 @@ hipError_t launch_sqp_rti_rowpar(const KParams& P, const KArgs& a, int mode, hip
     const int W = a.rowpar >= 4 ? 4 : (a.rowpar == 2 ? 2 : 1);
     if (a.seg < 0 || a.seg > kSegMax || a.seg > 4 * W || (a.seg > 0 && P.N % a.seg != 0))
         return hipErrorInvalidValue;
+#ifdef NMPC_HYBRID
     const int grid = (a.hyb_role == 2) ? (a.B < a.hyb_cap ? a.B : a.hyb_cap) : a.B;
+#else
+    const int grid = a.B;
+#endif
     if (W == 4)  // four waves per robot (one per SIMD of its CU)
         if (a.seg > 0) hipLaunchKernelGGL((k_sqp_rti_rowpar<M, 4, true>), dim3(grid), dim3(256), lds, stream, P, a, mode);
         else hipLaunchKernelGGL((k_sqp_rti_rowpar<M, 4, false>), dim3(grid), dim3(256), lds, stream, P, a, mode);

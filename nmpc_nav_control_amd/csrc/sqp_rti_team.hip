@@ -113,8 +113,12 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a)
     const int team = a.split ? (int)blockIdx.x : (gt >> 4);
     const int row = a.split ? (int)(threadIdx.x >> 4) : 0;
     const int r = gt & 15;
-    // hybrid launch: the first hyb_n[0] ranks of the order run the segmented kernel on another stream
+#ifdef NMPC_HYBRID
+    // hybrid launch (A/B build): the first hyb_n[0] ranks of the order run the segmented kernel on another stream
     const int hoff = (a.hyb_role == 1) ? a.hyb_n[0] : 0;
+#else
+    constexpr int hoff = 0;
+#endif
     if (team >= a.B - hoff) return;  // whole DPP rows leave together
     const int N = P.N;
     const size_t S = (size_t)a.stride;  // resident state stride (capacity)
@@ -160,8 +164,9 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a)
     const int kb = has_b ? R::BS : 0;
     // this lane's DZ in the dense plane after the records: dzbase + k * 16 (every lane its own float)
     float* const dzbase = a.scratch + (size_t)a.sstride * (N + 1) * KS + (size_t)inst * (N + 1) * 16 + r;
-    // IPM warm start: the bound multipliers of the robot's previous successful solve are still in its records
-    const bool warm = P.warm && a.warm && a.warm[inst] && !(a.reset && a.reset[inst]);
+    // IPM warm start: the bound multipliers of the robot's previous successful solve are still in its records, in
+    // this launch's layout when its tag matches (nmpc_batch.h NMPC_WARM_TAG_*)
+    const bool warm = P.warm && a.warm && a.warm[inst] == a.warm_tag && !(a.reset && a.reset[inst]);
 
 #define XB(k, j) a.xbar[((size_t)(k) * NX + (j)) * S + inst]
 #define UBAR(k, j) a.ubar[((size_t)(k) * NU + (j)) * S + inst]
@@ -1106,7 +1111,8 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a)
         if (a.iter_key) a.iter_key[inst] = it_done;
         // warm-start the next solve only from a solve that converged (not from one that ran to qp_iter_max)
         // and only from an easy one (P.warm_iter_max, 12 by default: warm multipliers lengthen the hard QPs)
-        if (a.warm) a.warm[inst] = (P.warm && status == 0 && it_done < P.iter_max && it_done <= P.warm_iter_max) ? 1 : 0;
+        if (a.warm)
+            a.warm[inst] = (P.warm && status == 0 && it_done < P.iter_max && it_done <= P.warm_iter_max) ? a.warm_tag : 0;
         if (a.qp_res) {
 #pragma unroll
             for (int j = 0; j < 3; j++) a.qp_res[(size_t)j * Bn + inst] = exit_res[j];

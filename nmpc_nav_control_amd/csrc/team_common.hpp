@@ -91,6 +91,8 @@ struct TeamRec {
     static constexpr int BS = NBND * CW;         // bound floats per stage
     static_assert(!SPLIT_OK || (TL == 4 && LB == 8 && GV == 10 && GR == GV + NGV && NGV <= 3), "split record map");
     static_assert(!SPLIT_OK || (CS + BS) <= 16 * RSS, "split planes fit the robot's record region");
+    // split planes keep no DZ / DZA field: the forward sweep's direction must live in the DZ plane
+    static_assert(!SPLIT_OK || kDzPlane, "split record planes need the DZ plane (NMPC_DZ_IN_RECORD off)");
 };
 
 namespace {

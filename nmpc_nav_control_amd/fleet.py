@@ -30,7 +30,8 @@ class Fleet:
     / path callbacks call reset_mpc, NMPCNavControlROS.cpp:304-327); a dict overrides RENEW's keys (the tests use
     short ttls). False: every robot keeps its first goal / path (the fleet parks), as round-2 benches ran."""
 
-    def __init__(self, model, B, N, seed, dev, start=0, stream=None, solver_factory=None, schedule=None, renew=True):
+    def __init__(self, model, B, N, seed, dev, start=0, stream=None, solver_factory=None, schedule=None, renew=True,
+                 record_layout=None):
         self.model, self.B, self.N = model, B, N
         self.seed, self.start = int(seed), int(start)
         self.dev = torch.device(dev)
@@ -41,6 +42,8 @@ class Fleet:
         self.solver = solver_factory(model, N, B, device=self.dev)
         if schedule is not None and "NMPC_AMD_SCHED" not in os.environ:
             self.solver.set_schedule(schedule)
+        if record_layout is not None and "NMPC_AMD_REC_SPLIT" not in os.environ:
+            self.solver.set_record_layout(record_layout)
         fl = make_fleet(model, B, seed=seed, start=start)
         self.is_path = fl["is_path"]
         t = lambda a, dt=torch.float32: torch.from_numpy(np.ascontiguousarray(a)).to(self.dev, dt)  # noqa: E731
@@ -147,8 +150,13 @@ class FleetNode:
                 stream = torch.cuda.Stream(self.dev) if self.multi else None
                 sched = schedule if schedule is not None else ("interleaved" if len(models) > 1 and stream is not None
                                                                else None)
+                # diff's record layout: the handle's own choice alone (wide for the metric fleet), the split planes
+                # beside other models' records on the same device (mixed: 5.25 -> 5.70 M it/s).
+                # Decided here, once, from the node's configuration: no other handle can flip it
+                layout = "split" if (m == "diff" and len(models) > 1 and cuda) else None
                 self.fleets.append(Fleet(m, ghi - glo, N, seed + 100 * j, self.dev, start=lo + glo, stream=stream,
-                                         solver_factory=solver_factory, schedule=sched, renew=renew))
+                                         solver_factory=solver_factory, schedule=sched, renew=renew,
+                                         record_layout=layout))
         self.B = sum(f.B for f in self.fleets)
         self.offs = [int(v) for v in np.cumsum([0] + [f.B for f in self.fleets])]
         self.gather = CommandGather(5, [self.B] * world, self.dev) if gather else None

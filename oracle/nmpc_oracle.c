@@ -79,7 +79,10 @@ void oc_params_default(int model, int N, oc_params* prm)
     prm->mu0 = 1.0;
     prm->thr0 = 0.5;
     prm->tau = 0.995;
-    prm->infeas_lambda = OC_INFEAS_LAMBDA;
+    /* acados semantics by default: HPIPM has no infeasibility exit (generate_c_code.py:69), a
+     * hard QP runs to iter_max. The batched device API's early exit (nmpc_model_params.qp_infeas_lambda) is the
+     * builder's own rule; a comparison against it opts in with infeas_lambda = OC_INFEAS_LAMBDA */
+    prm->infeas_lambda = 0.0;
 }
 
 /* ------------------------------------------------------------------------------------------------ */

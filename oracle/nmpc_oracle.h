@@ -35,8 +35,9 @@ extern "C" {
 #define OC_NUMAX 4
 #define OC_NYMAX 15
 #define OC_NBMAX 8 /* bounded components per stage: nbu + nbx (omni4: 4 + 4) */
-/* IPM infeasibility exit (status 4): largest bound multiplier above OC_INFEAS_LAMBDA while the bound residual is
- * above OC_INFEAS_RES (the device kernel uses the same two constants) */
+/* IPM infeasibility exit (status 4), off by default (acados / HPIPM have none): largest bound multiplier above
+ * infeas_lambda (OC_INFEAS_LAMBDA: the batched device API's default) while the bound residual is above OC_INFEAS_RES
+ * (the device kernel uses the same two constants) */
 #define OC_INFEAS_LAMBDA 1e5
 #define OC_INFEAS_RES 1e-3
 
@@ -57,7 +58,8 @@ typedef struct oc_params {
     double tol_stat, tol_ineq, tol_comp;
     double mu0, thr0, tau;
     /* infeasibility exit: multiplier threshold infeas_lambda * max(1, w_max / 10) (w_max: the largest stage or
-     * terminal weight of the QP); 0 = off (HPIPM: run to iter_max). Default OC_INFEAS_LAMBDA, as the device. */
+     * terminal weight of the QP); 0 = off (HPIPM: run to iter_max), the default. OC_INFEAS_LAMBDA restates the
+     * batched device default (nmpc_model_params_default: qp_infeas_lambda 1e5). */
     double infeas_lambda;
 } oc_params;
 

@@ -16,6 +16,11 @@ _LIB_PATH = os.path.join(_HERE, "liboracle.so")
 OC_DIFF, OC_OMNI4, OC_TRIC = 0, 1, 2
 MODEL_IDS = {"diff": OC_DIFF, "omni4": OC_OMNI4, "tric": OC_TRIC}
 NBMAX = 8
+# IPM exit rules of the oracle (nmpc_oracle.h infeas_lambda): "acados" (the default) has no infeasibility exit, as
+# HPIPM (a hard QP runs to iter_max; the capsule ABI's semantics); "batched" restates the batched device API's
+# default early exit (status 4 once the bound multipliers pass 1e5 x the weight scale with the bound residual open,
+# nmpc_model_params_default qp_infeas_lambda). A comparison against the batched API states rule="batched".
+RULES = {"acados": 0.0, "batched": 1e5}
 
 
 class OcParams(ctypes.Structure):
@@ -99,12 +104,17 @@ def _ip(a):
 
 
 class Oracle:
-    """One model configuration of the CPU oracle."""
+    """One model configuration of the CPU oracle. `rule` is the IPM exit rule (RULES): "acados" by default, "batched"
+    for comparisons against the batched device API's default parameters."""
 
-    def __init__(self, model, N, **overrides):
+    def __init__(self, model, N, rule="acados", **overrides):
+        if rule not in RULES:
+            raise ValueError(f"rule must be one of {sorted(RULES)}")
         self.model = model
         self.prm = OcParams()
         lib().oc_params_default(MODEL_IDS[model], N, ctypes.byref(self.prm))
+        self.prm.infeas_lambda = RULES[rule]
+        self.rule = rule if "infeas_lambda" not in overrides else f"infeas_lambda={overrides['infeas_lambda']:g}"
         for k, v in overrides.items():
             cur = getattr(self.prm, k)
             if isinstance(cur, ctypes.Array):

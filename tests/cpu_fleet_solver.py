@@ -31,7 +31,7 @@ class OracleFleetSolver:
 
     def __init__(self, model, N, capacity, device="cpu"):
         self.model, self.N, self.B = model, N, capacity
-        self.o = Oracle(model, N)
+        self.o = Oracle(model, N, rule="batched")
         self.nu, self.nx = self.o.nu, self.o.nx
         xb, ub = self.o.iterate_create()
         self.xbar = np.repeat(xb[None], capacity, axis=0)

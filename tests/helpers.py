@@ -9,7 +9,7 @@ def oracle_closed_loop(model, N, B, ticks, seed=20250824, o=None, start=0, u0_lo
     """Run the fp64 oracle in closed loop (plant = RK4 of the model) for `ticks` ticks over robots
     [start, start + B) of the seeded fleet. Returns the oracle and, for the last tick, the solve inputs
     (x0, yref, We, xbar, ubar) per robot; appends each tick's u0 [B][nu] to `u0_log` when given."""
-    o = o or Oracle(model, N)
+    o = o or Oracle(model, N, rule="batched")
     fl = make_fleet(model, B, seed=seed, start=start)
     pose = fl["pose"].T.astype(np.float64).copy()
     vel = fl["vel"].T.astype(np.float64).copy()

@@ -48,7 +48,7 @@ def run(model, N, B, ticks, sample=64, check_every=10, reset_frac=0.02, reset_ev
     qp_iter = torch.zeros(B, dtype=torch.int32, device=dev)
     solver.fleet_sim_step(path, s, pose, vel, steer_arg, None, None, traj, tlen, advance=False)
     rng = np.random.default_rng([seed, 7])
-    o = Oracle(model, N)
+    o = Oracle(model, N, rule="batched")
     S = min(sample, B)
     report = dict(model=model, N=N, B=B, ticks=ticks, sample=S, kernel=kernel, checks=[], failed=0, resets=0,
                   qp_iter_mean=0.0, qp_iter_max=0)

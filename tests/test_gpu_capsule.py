@@ -53,7 +53,7 @@ def path(t0, n):
 def test_capsule_closed_loop_matches_oracle(built, model):
     ctl, Cmd = make(model)
     assert ctl.getHorizon() == N
-    o = Oracle(model, N)
+    o = Oracle(model, N, rule="acados")  # the capsule ABI: no early exit
     xb, ub = o.iterate_create()
     carried = np.zeros(o.nbx)
     pose, vel, steer = np.array([0.05, -0.02, 2.9]), np.array([0.1, 0.0, 0.05]), 0.0
@@ -118,12 +118,12 @@ def _set_tick(c, x0, yref):
 
 
 def test_capsule_warm_start_and_reset(built):
-    """A capsule with qp_warm_start = 1, solved tick after tick, starts its IPM from its own previous multipliers: a fresh
+    """A capsule with qp_warm_start = 2 (acados: primal and dual), solved tick after tick, starts its IPM from its own previous multipliers: a fresh
     capsule given the same inputs and iterate starts cold, in the same launch, and reaches the same QP solution.
     After reset the next solve is cold again: bit-identical to a fresh capsule's solve from a zero iterate."""
     a = make("diff")[0]
-    a.solver_opts_set("qp_warm_start", 1)  # (the capsule default is acados' cold start)
-    o = Oracle("diff", N)
+    a.solver_opts_set("qp_warm_start", 2)  # (the capsule default is acados' cold start)
+    o = Oracle("diff", N, rule="acados")
     x0 = np.array([0.05, -0.02, 2.9, 0.1, 0.05, 0.0, 0.0])
     yref = np.zeros((N + 1, a.ny))
     it_warm = it_cold = 0
@@ -131,7 +131,7 @@ def test_capsule_warm_start_and_reset(built):
         for k, p in enumerate(path(tick, N + 1)):
             yref[k, :3] = [p.x, p.y, np.unwrap([x0[2], p.theta])[1]]
         cold = make("diff")[0]
-        cold.solver_opts_set("qp_warm_start", 1)  # same options as a, so both share one launch; fresh, so cold
+        cold.solver_opts_set("qp_warm_start", 2)  # same options as a, so both share one launch; fresh, so cold
         xs, us = a.iterate()
         for k in range(N + 1):
             cold.out_set(k, "x", xs[k])
@@ -193,10 +193,10 @@ def test_capsule_cold_start_option_matches_oracle(built):
     reference's generated solver (scripts/diff/generate_c_code.py:68-74). Same QP solutions as the oracle; the
     cold capsule needs at least as many IPM iterations as the warm one over the same closed loop."""
     iters = {}
-    for warm in (1, 0):
+    for warm in (2, 0):
         ctl, Cmd = make("diff")
         ctl.solver_opts_set("qp_warm_start", warm)
-        o = Oracle("diff", N)
+        o = Oracle("diff", N, rule="acados")
         xb, ub = o.iterate_create()
         carried = np.zeros(o.nbx)
         pose, vel = np.array([0.05, -0.02, 2.9]), np.array([0.1, 0.0, 0.05])
@@ -215,7 +215,7 @@ def test_capsule_cold_start_option_matches_oracle(built):
             xn, v3, _ = plant("diff", o, x0, ub[0])
             pose, vel = xn[:3], np.array(v3)
         iters[warm] = its
-    assert sum(iters[0][1:]) >= sum(iters[1][1:]), iters
+    assert sum(iters[0][1:]) >= sum(iters[2][1:]), iters
 
 
 def test_capsule_infeasible_qp_has_no_early_exit(built):

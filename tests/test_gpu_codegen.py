@@ -59,7 +59,7 @@ def test_generated_defaults_drive_the_solve(built, tmp_path):
     S.diff2amr_acados_free_capsule(cap)
 
     d = gen.load_parameters("diff", dp)
-    o = Oracle("diff", N, dt=d["tf"] / d["N"], p=d["p"] + [0.0], W=d["W"] + [0.0] * 6, W_e=d["W_e"] + [0.0] * 4,
+    o = Oracle("diff", N, rule="acados", dt=d["tf"] / d["N"], p=d["p"] + [0.0], W=d["W"] + [0.0] * 6, W_e=d["W_e"] + [0.0] * 4,
                lbx=d["lbx"] + [0, 0], ubx=d["ubx"] + [0, 0], lbu=d["lbu"] + [0, 0], ubu=d["ubu"] + [0, 0],
                terminal_hack=0)
     xb, ub = o.iterate_create()
@@ -90,7 +90,7 @@ def test_reference_codegen_self_check(built, geometry):
     assert getattr(S, f"{name}_acados_create")(cap) == 0
     c = cap.contents
     assert getattr(S, f"{name}_acados_solve")(cap) == 0  # generate_c_code.py:79-83 raises otherwise
-    o = Oracle(geometry, d["N"], dt=d["tf"] / d["N"], p=d["p"] + [0.0] * (3 - len(d["p"])),
+    o = Oracle(geometry, d["N"], rule="acados", dt=d["tf"] / d["N"], p=d["p"] + [0.0] * (3 - len(d["p"])),
                W=d["W"] + [0.0] * (15 - len(d["W"])), W_e=d["W_e"] + [0.0] * (11 - len(d["W_e"])),
                lbx=d["lbx"] + [0.0] * (4 - len(d["lbx"])), ubx=d["ubx"] + [0.0] * (4 - len(d["ubx"])),
                lbu=d["lbu"] + [0.0] * (4 - len(d["lbu"])), ubu=d["ubu"] + [0.0] * (4 - len(d["ubu"])),

@@ -44,15 +44,23 @@ def replay_and_compare(fleet, oracle, tick_fn):
     return eu, max(ex, 0.0), ec, st, st_o, after["xbar"]
 
 
-@pytest.mark.parametrize("model,N,B,idx", [("diff", 40, 4096, 1), ("diff", 40, 1024, 1), ("omni4", 40, 4096, 2),
-                                           ("tric", 60, 8192, 3)])
-def test_bench_config_full_batch_replay(built, model, N, B, idx):
+@pytest.mark.parametrize("model,N,B,idx,layout", [("diff", 40, 4096, 1, "wide"), ("diff", 40, 4096, 1, "split"),
+                                                  ("diff", 40, 1024, 1, None), ("omni4", 40, 4096, 2, "wide"),
+                                                  ("tric", 60, 8192, 3, "split")])
+def test_bench_config_full_batch_replay(built, model, N, B, idx, layout):
     """BASELINE configs at full batch (the bench's own fleets): 20 closed-loop ticks with no failed solve, then
-    two ticks on which EVERY robot is replayed through the fp64 oracle. tric: >= 10 % of the robots have their
-    steering reference alpha_ref on its 45 deg bound somewhere on the horizon (SURVEY 8d config 4;
-    NMPCNavControlTric.cpp:24-29, scripts/tric/generate_c_code.py:47-57)."""
-    f = Fleet(model, B, N, SEED + idx, DEV)
-    o = Oracle(model, N)
+    two ticks on which EVERY robot is replayed through the fp64 oracle. The metric config runs once per record
+    layout of diff's team kernel (wide: its own default alone on the device, what bench.py's metric line runs;
+    split: the mixed fleet's), and the layout the launches took is asserted. tric: >= 10 % of
+    the robots have their steering reference alpha_ref on its 45 deg bound somewhere on the horizon (SURVEY 8d
+    config 4; NMPCNavControlTric.cpp:24-29, scripts/tric/generate_c_code.py:47-57)."""
+    f = Fleet(model, B, N, SEED + idx, DEV, record_layout=layout if model == "diff" else None)
+    plan = f.solver.plan_ex(B, "run")
+    if layout is None:
+        assert plan["kernel"] == "rowpar", plan  # diff1024: the segmented row-parallel kernel
+    else:
+        assert plan["kernel"] == "team" and plan["record_layout"] == layout, plan
+    o = Oracle(model, N, rule="batched")
     for tick in range(20):
         f.tick()
         if tick % 5 == 4:
@@ -85,7 +93,7 @@ def test_mixed_fleet_concurrent_streams_full_replay(built):
     node = FleetNode(MIXED, N, SEED + 4, DEV)
     assert node.multi and all(f.stream is not None for f in node.fleets)
     seq = [Fleet(m, b, N, SEED + 4 + 100 * j, DEV) for j, (m, b) in enumerate(MIXED)]
-    oracles = [Oracle(m, N) for m, _ in MIXED]
+    oracles = [Oracle(m, N, rule="batched") for m, _ in MIXED]
     for tick in range(20):
         node.step()
         for f in seq:
@@ -229,6 +237,88 @@ def test_failure_stays_on_its_robot(built):
     assert t_bad <= 1.10 * t_clean, (t_bad, t_clean)
 
 
+def test_layout_independent_of_other_handles(built):
+    """a handle's record layout is its own, fixed at create. A metric fleet (4096 diff robots,
+    107 MB of records: wide) ticks once undisturbed; then, from the same saved state, with a 214 MB diff handle
+    (capacity 8192, split by its own size) created beside it and destroyed again, and once more with another large
+    handle alive during the tick. Results, IPM counts, iterate and warm flags are bit-identical every time, and
+    the fleet's plan never changes."""
+    N, B = 40, 4096
+    f = Fleet("diff", B, N, SEED + 1, DEV)
+    for _ in range(20):
+        f.tick()
+    torch.cuda.synchronize()
+    assert f.solver.plan_ex(B, "run")["record_layout"] == "wide"
+    st0 = _save(f)
+
+    def tick():
+        f.solve()
+        torch.cuda.synchronize()
+        out = _outputs(f)
+        out["warm"] = f.solver.warm_state()[0].to_tensor()
+        return out
+
+    ref = tick()
+    assert int((ref["warm"][0, :B] == 1).sum()) > B // 2  # warm-started in the wide layout (NMPC_WARM_TAG_WIDE)
+    big = BatchSolver("diff", N, 8192)
+    p_big = big.plan_ex(8192, "run")
+    assert p_big["record_layout"] == "split" and p_big["record_bytes"] > 200e6, p_big
+    big.close()
+    _restore(f, st0)
+    got = tick()
+    big2 = BatchSolver("diff", N, 8192)
+    _restore(f, st0)
+    got2 = tick()
+    big2.close()
+    for k in ref:
+        assert torch.equal(got[k], ref[k]) and torch.equal(got2[k], ref[k]), k
+    assert f.solver.plan_ex(B, "run")["record_layout"] == "wide"
+
+
+def test_warm_tags_across_kernel_switch(built):
+    """one tric handle alternates launches of 1025 robots (the team kernel, split record planes) and 1024
+    robots (the segmented row-parallel kernel, wide records). Each robot's warm flag carries the tag of the layout
+    its multipliers sit in (NMPC_WARM_TAG_SPLIT 2 / _WIDE 1), so a robot whose kernel changes starts cold on its own
+    and no launch reads records another layout wrote; the robot outside the smaller launches keeps its flag. Every
+    tick, every launched robot is replayed through the oracle from the GPU's pre-tick state."""
+    N, BF = 40, 1025
+    f = Fleet("tric", BF, N, SEED + 3, DEV)
+    o = Oracle("tric", N, rule="batched")
+    assert f.solver.plan_ex(BF, "run")["kernel"] == "team" and f.solver.plan_ex(BF - 1, "run")["kernel"] == "rowpar"
+    for _ in range(6):
+        f.tick()
+    for tick in range(6):
+        n = BF if tick % 2 == 0 else BF - 1
+        torch.cuda.synchronize()
+        warm_before = f.solver.warm_state()[0].to_tensor()[0, :BF].clone()
+        sn = f.snapshot()
+        sl = lambda a: None if a is None else np.ascontiguousarray(a[:n])  # noqa: E731
+        cols = lambda t_: t_[..., :n].contiguous()  # noqa: E731
+        u0 = torch.zeros(2, n, device=DEV)
+        cmd = torch.zeros(3, n, device=DEV)
+        status = torch.full((n,), -7, dtype=torch.int32, device=DEV)
+        f.solver.run(cols(f.pose), cols(f.vel), cols(f.traj), steer=cols(f.steer), traj_len=cols(f.tlen),
+                     reset=cols(f.reset), cmd=cmd, u0=u0, status=status)
+        torch.cuda.synchronize()
+        warm = f.solver.warm_state()[0].to_tensor()[0, :BF]
+        tag = 2 if n == BF else 1
+        assert set(warm[:n].unique().tolist()) <= {0, tag}, (tick, warm[:n].unique())
+        assert int((warm[:n] == tag).sum()) > n // 2, tick
+        if n < BF:
+            assert int(warm[BF - 1]) == int(warm_before[BF - 1]), tick  # the robot outside the launch: untouched
+        xb_o, ub_o, cr_o = sl(sn["xbar"]).copy(), sl(sn["ubar"]).copy(), sl(sn["carried"]).copy()
+        _, cmd_o, u0_o, st_o, _ = o.batch_tick(sl(sn["pose"]), sl(sn["vel"]), sl(sn["steer"]), sl(sn["traj"]),
+                                               sl(sn["tlen"]), sl(sn["reset"]), cr_o, xb_o, ub_o, nthreads=NTHREADS)
+        st = status.cpu().numpy()
+        assert (st == 0).all() and (st_o == 0).all(), tick
+        eu = float(np.abs(u0.cpu().numpy().T - u0_o).max())
+        assert eu <= TOL_U, (tick, n, eu)
+        f.u0[:, :n] = u0
+        f.cmd[:, :n] = cmd
+        f.status[:n] = status
+        f.advance()
+
+
 def test_reset_mode_keeps_carried_refs(built):
     """nmpc_batch_init_iterate(mode=1) is {name}_acados_reset: the iterate is zeroed and the carried vel-ref
     states stay (as the per-robot reset mask does; NMPCNavControlDiff.cpp:177-181 resets only the capsule);
@@ -255,7 +345,7 @@ def test_renewal_on_device(built):
     lo, hi = 2, 6
     N, B, seed = 40, 1024, SEED + 1
     f = Fleet("diff", B, N, seed, DEV, renew=dict(ttl_min=lo, ttl_max=hi))
-    o = Oracle("diff", N)
+    o = Oracle("diff", N, rule="batched")
     gi = np.arange(B)
     total = 0
     for tick in range(12):

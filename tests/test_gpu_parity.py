@@ -137,7 +137,7 @@ def test_run_closed_loop_matches_oracle(built, ipm, model, resets):
     reset_mask = torch.from_numpy((np.arange(B) % 5 == 0).astype(np.uint8)).to(DEV)
     fl = make_fleet(model, B, seed=11)
     solver = make_solver(model, N, B, ipm)
-    o = Oracle(model, N)
+    o = Oracle(model, N, rule="batched")
     _, _, cr = solver.state()
     cr.copy_from(t(fl["carried"]))
     pose, vel, steer, path, s = t(fl["pose"]), t(fl["vel"]), t(fl["steer"]), t(fl["path"]), t(fl["s"])

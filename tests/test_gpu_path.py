@@ -115,7 +115,7 @@ def test_follow_path_tick_on_device_matches_oracle(built):
     torch.cuda.synchronize()
     u0 = u0.cpu().numpy().T
     assert (status.cpu().numpy() == 0).all()
-    o = Oracle("diff", N)
+    o = Oracle("diff", N, rule="batched")
     xb0, ub0 = o.iterate_create()
     err = 0.0
     for i in range(B):

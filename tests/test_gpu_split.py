@@ -27,14 +27,18 @@ def t(a, dtype=torch.float32):
     return torch.from_numpy(np.ascontiguousarray(a)).to(device=DEV, dtype=dtype)
 
 
-def handle(monkeypatch, model, N, cap, **env):
-    """A handle created under the launch-choice overrides `env` (read at creation)."""
+def handle(monkeypatch, model, N, cap, layout=None, **env):
+    """A handle created under the launch-choice overrides `env` (read at creation), with the team kernel's record
+    layout `layout` (None: the model's own choice)."""
     for k, v in env.items():
         monkeypatch.setenv(k, str(v))
-    h = BatchSolver(model, N, cap, params=default_params(model, N))
+    h = BatchSolver(model, N, cap, params=default_params(model, N), record_layout=layout)
     for k in env:
         monkeypatch.delenv(k)
     return h
+
+
+LAYOUTS = {"diff": ("wide", "split"), "omni4": ("wide",), "tric": ("split",)}  # the team kernel's record layouts
 
 
 def pair(monkeypatch, model, N, cap):
@@ -127,13 +131,20 @@ def test_split_run_and_run_path_equal_unsplit(built, monkeypatch, holo):
 TOL_RP = 3e-4
 
 
+@pytest.mark.parametrize("layout", ["wide", "split"])
 @pytest.mark.parametrize("model", ["diff", "omni4", "tric"])
 @pytest.mark.parametrize("N,B", [(80, 13), (40, 64), (2, 5), (1, 3)])
-def test_rowpar_solve_matches_team(built, monkeypatch, model, N, B):
+def test_rowpar_solve_matches_team(built, monkeypatch, model, N, B, layout):
+    """The row-parallel kernel (wide records) against the team kernel in each record layout the model has (diff:
+    both, ADVICE r04: the split planes are the mixed fleet's default for diff)."""
+    if layout not in LAYOUTS[model]:
+        pytest.skip(f"{model}'s team kernel has no {layout} records")
     o, rec = oracle_closed_loop(model, N, B, 2)
     nx, nu = o.nx, o.nu
     rp = handle(monkeypatch, model, N, 64)
-    tm = handle(monkeypatch, model, N, 64, NMPC_AMD_ROWPAR_MAX=0, NMPC_AMD_SPLIT_MAX=0)
+    tm = handle(monkeypatch, model, N, 64, layout=layout, NMPC_AMD_ROWPAR_MAX=0, NMPC_AMD_SPLIT_MAX=0)
+    assert tm.plan_ex(B)["kernel"] == "team" and tm.plan_ex(B)["record_layout"] == layout
+    assert rp.plan_ex(B)["kernel"] == "rowpar" or N == 1
     x0 = t(np.stack([r[0] for r in rec]).T)
     yref = t(np.stack([r[1] for r in rec]).transpose(1, 2, 0))
     We = t(np.stack([r[2] for r in rec]).T)
@@ -161,7 +172,8 @@ def test_rowpar_solve_matches_team(built, monkeypatch, model, N, B):
 
 def test_rowpar_run_matches_team(built, monkeypatch):
     """run mode (pose / velocity packing, reference unwrap and padding with traj_len shorter than the horizon, the
-    diff terminal-weight hack, carry and command) over warm-started ticks: row-parallel against team kernel."""
+    diff terminal-weight hack, carry and command) over warm-started ticks: row-parallel against the team kernel in
+    both of diff's record layouts (wide, and the split planes the mixed fleet takes)."""
     N, B = 40, 24
     rng = np.random.default_rng(11)
     segs, nseg, nu = random_paths(B, seed=11, max_segs=4, reverse_frac=0.2)
@@ -174,7 +186,9 @@ def test_rowpar_run_matches_team(built, monkeypatch):
     P, V = t(pose.T), t(vel.T)
     S, NS, NU = t(segs, torch.float64), t(nseg, torch.int32), t(nu, torch.float64)
     tlen = t(np.where(np.arange(B) % 3 == 0, 1, np.where(np.arange(B) % 3 == 1, N // 2, N + 1)), torch.int32)
-    hs = (handle(monkeypatch, "diff", N, B), handle(monkeypatch, "diff", N, B, NMPC_AMD_ROWPAR_MAX=0))
+    hs = (handle(monkeypatch, "diff", N, B), handle(monkeypatch, "diff", N, B, "wide", NMPC_AMD_ROWPAR_MAX=0),
+          handle(monkeypatch, "diff", N, B, "split", NMPC_AMD_ROWPAR_MAX=0))
+    assert [h.plan_ex(B, "run")["record_layout"] for h in hs[1:]] == ["wide", "split"]
     for tick in range(4):
         traj = discretize(S, NS, NU, 1 / 40, N + 1, False)
         res = []
@@ -184,9 +198,12 @@ def test_rowpar_run_matches_team(built, monkeypatch):
             h.run(P, V, traj, traj_len=tlen, cmd=o_["cmd"], u0=o_["u0"], status=o_["status"])
             res.append(o_)
         torch.cuda.synchronize()
-        a, b = res
-        assert (a["status"] == 0).all() and (b["status"] == 0).all(), tick
-        assert close(a["u0"], b["u0"]) <= TOL_RP, (tick, close(a["u0"], b["u0"]))
-        assert close(a["cmd"], b["cmd"]) <= TOL_RP, tick
-        ca, cb = hs[0].state()[2].to_tensor(), hs[1].state()[2].to_tensor()
-        assert close(ca[:, :B], cb[:, :B]) <= TOL_RP, tick
+        a = res[0]
+        for j, b in enumerate(res[1:]):
+            assert (a["status"] == 0).all() and (b["status"] == 0).all(), (tick, j)
+            assert close(a["u0"], b["u0"]) <= TOL_RP, (tick, j, close(a["u0"], b["u0"]))
+            assert close(a["cmd"], b["cmd"]) <= TOL_RP, (tick, j)
+            ca, cb = hs[0].state()[2].to_tensor(), hs[1 + j].state()[2].to_tensor()
+            assert close(ca[:, :B], cb[:, :B]) <= TOL_RP, (tick, j)
+        # the two team layouts: the same arithmetic on differently placed records, bit for bit
+        assert torch.equal(res[1]["u0"], res[2]["u0"]) and torch.equal(res[1]["cmd"], res[2]["cmd"]), tick

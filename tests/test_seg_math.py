@@ -23,7 +23,7 @@ from oracle.oracle import Oracle  # noqa: E402
 def test_segmented_direction_equals_serial(model, N, S, chol):
     if N % S:
         pytest.skip("S must divide N")
-    o = Oracle(model, N)
+    o = Oracle(model, N, rule="batched")
     rng = np.random.default_rng(11)
     for _ in range(3):
         G, H, g = seg_emu.make_qp(o, N, rng, 1e6)

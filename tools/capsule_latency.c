@@ -12,7 +12,7 @@
  * usage: build/capsule_latency [ticks=300] [cold|warm]
  *   cold (default): HPIPM's cold start every tick, acados' default and the reference's generated OCP's
  *         (scripts/diff/generate_c_code.py:68-74 sets no qp_warm_start), also the capsule's default
- *   warm: ocp_nlp_solver_opts_set(.., "qp_warm_start", 1) -- the capsule's multiplier warm start
+ *   warm: ocp_nlp_solver_opts_set(.., "qp_warm_start", 2) -- the capsule's multiplier (dual) warm start
  */
 #include <string.h>
 #include <math.h>
@@ -51,7 +51,7 @@ int main(int argc, char** argv)
     if (diff2amr_acados_create(c) != 0) { fprintf(stderr, "create failed\n"); return 1; }
     const int N = c->nlp_dims->N;
     {
-        int ws = warm;
+        int ws = warm ? 2 : 0;  /* acados: 2 = warm-start primal and dual */
         ocp_nlp_solver_opts_set(c->nlp_config, c->nlp_opts, "qp_warm_start", &ws);
     }
     /* constructor: stage weights (NMPCNavControlDiff.cpp:62-73) */
