@@ -39,11 +39,28 @@ struct KParams {
 
 enum ModelId { kDiff = 0, kOmni4 = 1, kTric = 2 };
 
+// Column bitmask of one row of the discrete Jacobian [B A] in the team lane order (bit v: input v for v < NU,
+// state v - NU above), from a pattern string ('1' = structurally nonzero). gmask(i) of a model gives its constant
+// rows i >= NGV: the M block of the Riccati step multiplies them as uniform operands and skips the zeros
+// (team_common.hpp m_block). tests/test_oracle.py checks every pattern against the oracle's RK4 Jacobians.
+__host__ __device__ constexpr unsigned gmask_of(const char* p)
+{
+    unsigned m = 0;
+    for (int v = 0; p[v]; v++) m |= (p[v] == '1' ? 1u : 0u) << v;
+    return m;
+}
+
 struct Diff2 {
     static constexpr int ID = kDiff, NX = 7, NU = 2, NBX = 2, NBU = 2, NP = 2, NY = 9;
     // rows >= NGV of the discrete Jacobian [B A] do not depend on the state or input (theta, wheel and
     // ref rows are linear): they are computed once per launch (checked by tests/test_oracle.py)
     static constexpr int NGV = 2;
+    // constant rows th, vl, vr, vl_ref, vr_ref over columns [dvl_ref dvr_ref | x y th vl vr vl_ref vr_ref]
+    __host__ __device__ static constexpr unsigned gmask(int i)
+    {
+        return i == 2 ? gmask_of("11..11111") : i == 3 ? gmask_of("1....1.1.") : i == 4 ? gmask_of(".1....1.1")
+             : i == 5 ? gmask_of("1......1.") : i == 6 ? gmask_of(".1......1") : 0u;
+    }
     __host__ __device__ static constexpr int idxbx(int i) { return 5 + i; }
     __host__ __device__ static constexpr int idxbu(int i) { return i; }
 
@@ -99,6 +116,15 @@ struct Diff2 {
 struct Omni4 {
     static constexpr int ID = kOmni4, NX = 11, NU = 4, NBX = 4, NBU = 4, NP = 2, NY = 15;
     static constexpr int NGV = 2;  // x, y rows vary; theta / wheel / ref rows are linear
+    // constant rows th, v1..v4, v1_ref..v4_ref over columns [dv1_ref..dv4_ref | x y th v1..v4 v1_ref..v4_ref]
+    __host__ __device__ static constexpr unsigned gmask(int i)
+    {
+        return i == 2 ? gmask_of("1111..111111111") : i == 3 ? gmask_of("1......1...1...")
+             : i == 4 ? gmask_of(".1......1...1..") : i == 5 ? gmask_of("..1......1...1.")
+             : i == 6 ? gmask_of("...1......1...1") : i == 7 ? gmask_of("1..........1...")
+             : i == 8 ? gmask_of(".1..........1..") : i == 9 ? gmask_of("..1..........1.")
+             : i == 10 ? gmask_of("...1..........1") : 0u;
+    }
     __host__ __device__ static constexpr int idxbx(int i) { return 7 + i; }
     __host__ __device__ static constexpr int idxbu(int i) { return i; }
 
@@ -160,6 +186,12 @@ struct Omni4 {
 struct Tric3 {
     static constexpr int ID = kTric, NX = 7, NU = 2, NBX = 2, NBU = 2, NP = 3, NY = 9;
     static constexpr int NGV = 3;  // x, y, theta rows vary; v / alpha / ref rows are linear
+    // constant rows v, alpha, v_ref, alpha_ref over columns [dv_ref dalpha_ref | x y th v alpha v_ref alpha_ref]
+    __host__ __device__ static constexpr unsigned gmask(int i)
+    {
+        return i == 3 ? gmask_of("1....1.1.") : i == 4 ? gmask_of(".1....1.1") : i == 5 ? gmask_of("1......1.")
+             : i == 6 ? gmask_of(".1......1") : 0u;
+    }
     __host__ __device__ static constexpr int idxbx(int i) { return 5 + i; }
     __host__ __device__ static constexpr int idxbu(int i) { return i; }
 

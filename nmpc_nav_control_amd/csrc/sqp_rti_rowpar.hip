@@ -488,6 +488,12 @@ __global__ __launch_bounds__(64 * W, 1) void k_sqp_rti_rowpar(KParams P, KArgs a
     double gcol64[NX];
 #pragma unroll
     for (int i = 0; i < NX; i++) gcol64[i] = (double)gcol[i];
+#ifdef NMPC_ROWPAR_MCOL
+    // A/B only: the column-form M block needs 20 more registers, which pushes the segmented kernels past the 256
+    // that two waves per SIMD allow (diff 250 -> 256 + 14 AGPRs; tests/test_reg_usage.py), so the row form stays
+    GConst<M> gcs;  // the constant rows of [B A] as uniform operands of the M block (m_block)
+    gconst_load<M>(gcs, gcol);
+#endif
     const int m = N * NU + N * M::NBX;
     const float inv_m2 = 0.5f / (float)m;
 
@@ -740,7 +746,11 @@ __global__ __launch_bounds__(64 * W, 1) void k_sqp_rti_rowpar(KParams P, KArgs a
 #pragma unroll
                     for (int jj = 0; jj < NV; jj++) Lr[jj] = onehot[jj] * dg;
                     double pivot;
+#ifdef NMPC_ROWPAR_MCOL
+                    m_block<M>(Lr, pivot, pg, Gd, gcs);
+#else
                     mrow_pg_block<NX, NU>(Lr, pivot, pg, Gd);
+#endif
                     sfor<0, NU>([&](auto jc) {
                         constexpr int j2 = decltype(jc)::value;
                         if (!(pivot > 0.0) && srow) fail = true;
@@ -1071,7 +1081,11 @@ __global__ __launch_bounds__(64 * W, 1) void k_sqp_rti_rowpar(KParams P, KArgs a
     #pragma unroll
                         for (int j = 0; j < NV; j++) Lr[j] = onehot[j] * dg;
                         double pivot;
+#ifdef NMPC_ROWPAR_MCOL
+                        m_block<M>(Lr, pivot, pg, Gd, gcs);
+#else
                         mrow_pg_block<NX, NU>(Lr, pivot, pg, Gd);
+#endif
                         sfor<0, NU>([&](auto jc) {
                             constexpr int j = decltype(jc)::value;
                             if (!(pivot > 0.0)) fail = true;

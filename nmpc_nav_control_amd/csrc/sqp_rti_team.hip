@@ -576,6 +576,10 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a)
     double gcol64[NX];
 #pragma unroll
     for (int i = 0; i < NX; i++) gcol64[i] = (double)gcol[i];
+#ifndef NMPC_MROW
+    GConst<M> gcs;  // the constant rows of [B A] as uniform operands of the M block (m_block)
+    gconst_load<M>(gcs, gcol);
+#endif
 
     STAMP(1);
     // infeasibility threshold of this robot: qp_infeas_lambda scaled by its largest weight (terminal hack included)
@@ -778,8 +782,12 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a)
                 double Lr[NV];
 #pragma unroll
                 for (int j = 0; j < NV; j++) Lr[j] = onehot[j] * dg;
-                double pivot;
-                mrow_pg_block<NX, NU>(Lr, pivot, pg, Gd);  // pivot = M[0][0]
+                double pivot;  // = M[0][0]
+#ifndef NMPC_MROW
+                m_block<M>(Lr, pivot, pg, Gd, gcs);  // column form: uniform constant rows + NGV broadcast rows
+#else
+                mrow_pg_block<NX, NU>(Lr, pivot, pg, Gd);  // A/B: the row form (NX x NV broadcast FMAs)
+#endif
                 STAMPF(4);
                 sfor<0, NU>([&](auto jc) {
                     constexpr int j = decltype(jc)::value;

@@ -126,6 +126,57 @@ __device__ __forceinline__ void mrow_pg_block(double (&acc)[NX + NU], double& md
     if constexpr (NX == 7 && NU == 2) mrow_pg_block_7_2(acc, md0, pg, gd);
     else mrow_pg_block_11_4(acc, md0, pg, gd);
 }
+// Rows of [B A] the column-form M block broadcasts across the team (m_block): the NGV state-dependent rows and
+// theta's row (constant, but the densest: 7 of 9 / 13 of 15 columns, cheaper in registers as 2 more broadcast FMAs)
+template <class M>
+constexpr int mcol_nbc() { return M::NGV > 3 ? M::NGV : 3; }
+
+// Constant entries of rows >= mcol_nbc of [B A] (M::gmask), identical for every robot of a launch (they depend on
+// the model parameters only, tests/test_oracle.py test_constant_jacobian_rows): read once per launch from lane r of
+// the wave's first team, so each is one uniform value (a scalar operand) for every lane
+template <class M>
+struct GConst {
+    double v[M::NX][M::NX + M::NU];
+};
+template <class M>
+__device__ __forceinline__ void gconst_load(GConst<M>& gc, const float (&gcol)[M::NX])
+{
+    constexpr int NX = M::NX, NV = M::NX + M::NU;
+    sfor<mcol_nbc<M>(), NX>([&](auto ic) {
+        constexpr int i = decltype(ic)::value;
+        sfor<0, NV>([&](auto rc) {
+            constexpr int r = decltype(rc)::value;
+            if constexpr ((M::gmask(i) >> r) & 1u)
+                gc.v[i][r] = (double)__int_as_float(__builtin_amdgcn_readlane(__float_as_int(gcol[i]), r));
+            else
+                gc.v[i][r] = 0.0;
+        });
+    });
+}
+
+// Column j of M = D + [B A]' P [B A] on lane j (M is symmetric: its row j), lane j holding column j of P [B A] in
+// pg and column j of [B A] in gd, Lr initialised with the diagonal D: the sparse constant rows (>= mcol_nbc) of
+// [B A] as uniform-operand FMAs over their structural nonzeros (diff and tric 10, omni4 20), the first mcol_nbc rows
+// as fused-DPP FMAs broadcasting G[i][r] from lane r (3 x NV). The row form it replaces (lane r: M[r][j] +=
+// PG[i][j] from lane j times G[i][r]) needed NX x NV broadcast FMAs: diff 63 -> 37, omni4 165 -> 65.
+// pivot = M[0][0] (lane 0's diagonal).
+template <class M>
+__device__ __forceinline__ void m_block(double (&Lr)[M::NX + M::NU], double& pivot, const double (&pg)[M::NX],
+                                        const double (&gd)[M::NX], const GConst<M>& gc)
+{
+    constexpr int NX = M::NX, NU = M::NU, NV = NX + NU;
+    static_assert(mcol_nbc<M>() == 3, "generated broadcast blocks cover three rows");
+    sfor<mcol_nbc<M>(), NX>([&](auto ic) {
+        constexpr int i = decltype(ic)::value;
+        sfor<0, NV>([&](auto rc) {
+            constexpr int r = decltype(rc)::value;
+            if constexpr ((M::gmask(i) >> r) & 1u) Lr[r] = __builtin_fma(gc.v[i][r], pg[i], Lr[r]);
+        });
+    });
+    if constexpr (NX == 7 && NU == 2) mcol_var_block_7_2_3(Lr, pivot, pg, gd);
+    else mcol_var_block_11_4_3(Lr, pivot, pg, gd);
+}
+
 template <int NX, int NU, int J>
 __device__ __forceinline__ void chol_update(double (&lr)[NX + NU], double lj, double& piv)
 {

@@ -15,6 +15,10 @@ import os
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUT = os.path.join(ROOT, "nmpc_nav_control_amd", "csrc", "team_asm_gen.hpp")
 SHAPES = [(7, 2), (11, 4)]  # (NX, NU): diff2amr / tric3amr, omni4amr
+# leading rows of [B A] the column-form M block broadcasts (team_common.hpp m_block): the NGV state-dependent rows
+# and theta's row, the densest constant one (7 of 9 / 13 of 15 columns: broadcasting it costs 2 more FMAs than its
+# uniform-operand form and saves 7 / 13 uniform fp64 registers)
+VAR_ROWS = {(7, 2): (3,), (11, 4): (3,)}
 M = " row_mask:0xf bank_mask:0xf"
 
 
@@ -46,6 +50,26 @@ def mrow_pg_block(nx, nu):
     ins = ", ".join([f'"v"(pg[{i}])' for i in range(nx)] + [f'"v"(gd[{i}])' for i in range(nx)])
     body = "\\n\\t".join(lines)
     return (f"__device__ __forceinline__ void mrow_pg_block_{nx}_{nu}(double (&acc)[{nv}], double& md0,"
+            f" const double (&pg)[{nx}], const double (&gd)[{nx}])\n{{\n    asm(\"{body}\"\n        : {outs}\n"
+            f"        : {ins});\n}}\n")
+
+
+def mcol_var_block(nx, nu, ngv):
+    # classic Riccati, column form of M = D + [B A]' P [B A] on lane j: acc[r] += bcast_r(Gd[i]) * pg[i] over the
+    # ngv state-dependent rows i of [B A] (lane r holds column r of [B A], lane j column j of P [B A]); the constant
+    # rows are the caller's uniform-operand FMAs (team_common.hpp m_block). Then md0 = bcast_0(acc[0]), the first
+    # pivot. M is symmetric, so lane j's column j is its row j. Operands: acc 0..nv-1 (+v), md0 (=v), Gd.., pg..
+    nv = nx + nu
+    lines = ["s_nop 1"]
+    for i in range(ngv):
+        for r in range(nv):
+            lines.append(f"v_fmac_f64_dpp %{r}, %{nv + 1 + i}, %{nv + 1 + ngv + i} row_newbcast:{r}{M}")
+    lines.append("s_nop 1")
+    lines.append(f"v_mov_b64_dpp %{nv}, %0 row_newbcast:0{M}")
+    outs = ", ".join([f'"+v"(acc[{r}])' for r in range(nv)] + ['"=&v"(md0)'])
+    ins = ", ".join([f'"v"(gd[{i}])' for i in range(ngv)] + [f'"v"(pg[{i}])' for i in range(ngv)])
+    body = "\\n\\t".join(lines)
+    return (f"__device__ __forceinline__ void mcol_var_block_{nx}_{nu}_{ngv}(double (&acc)[{nv}], double& md0,"
             f" const double (&pg)[{nx}], const double (&gd)[{nx}])\n{{\n    asm(\"{body}\"\n        : {outs}\n"
             f"        : {ins});\n}}\n")
 
@@ -200,7 +224,8 @@ def main():
              "#pragma once", "", "#include <hip/hip_runtime.h>", "", "namespace nmpc {", ""]
     for nx, nu in SHAPES:
         nv = nx + nu
-        parts += [pg_block(nx, nu), mrow_pg_block(nx, nu), chol_update(nx, nu),
+        parts += [pg_block(nx, nu), mrow_pg_block(nx, nu)] + [mcol_var_block(nx, nu, g) for g in VAR_ROWS[(nx, nu)]]
+        parts += [chol_update(nx, nu),
                   dot_f32(nx, nu, f"dot_x_{nx}_{nu}"), dot_f32(nv, 0, f"dot_v_{nx}_{nu}"),
                   mst_rowmul(nx, nu), mst_rowmul_lt(nx, nu), mst_rowdot(nx, nu), mst_chol(nx, nu), mst_trsv(nx, nu), mst_vdot(nx, nu)]
     parts += ["}  // namespace nmpc", ""]
