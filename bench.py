@@ -50,7 +50,7 @@ MODEL_FLOPS = {"diff": dict(nx=7, nu=2, nbx=2, nbu=2, nnz_jx=12, nnz_ju=2, c_f=2
                "omni4": dict(nx=11, nu=4, nbx=4, nbu=4, nnz_jx=22, nnz_ju=4, c_f=40),
                "tric": dict(nx=7, nu=2, nbx=2, nbu=2, nnz_jx=12, nnz_ju=2, c_f=24)}
 FP32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 vector (and FP32-input MFMA) peak
-FP64_PEAK_SPEC_TFLOPS = 78.6  # AMD spec FP64 vector; replaced by the measured rate when profiles/<round> has it
+FP64_PEAK_SPEC_TFLOPS = 78.6  # AMD spec FP64 vector (half the FP32 rate; the guide gives no FP64 figure)
 PROFILE_ROUND = "r04"
 HBM_PEAK_GBS = 8000.0
 
@@ -79,12 +79,17 @@ def _profile_json(name):
     return None, None
 
 
-def valu_peaks():
-    """(FP32, FP64) vector peaks in TFLOP/s. FP32: MI355X_MICROARCH.md (157.3, = the FP32 MFMA rate); FP64: the
-    full-occupancy v_fma_f64 rate measured by tools/ubench_valu.hip (the guide gives none; spec 78.6)."""
+def valu_peaks(basis="spec"):
+    """(FP32, FP64) vector peaks in TFLOP/s on one stated basis:
+    'spec'     -- FP32 157.3 (MI355X_MICROARCH.md) and FP64 78.6 (AMD spec; the guide gives none): the line's frac;
+    'measured' -- both full-occupancy FMA rates of tools/ubench_valu.hip on this device (profiles/<round>/
+                  ubench_valu.json: FP32 114.0, FP64 62.6), None when that record is absent."""
+    if basis == "spec":
+        return FP32_PEAK_TFLOPS, FP64_PEAK_SPEC_TFLOPS
     ub, _ = _profile_json("ubench_valu.json")
-    fp64 = float(ub["fp64_full"]["tflops"]) if ub else FP64_PEAK_SPEC_TFLOPS
-    return FP32_PEAK_TFLOPS, fp64
+    if not ub:
+        return None
+    return float(ub["fp32_full"]["tflops"]), float(ub["fp64_full"]["tflops"])
 
 
 def roofline(fleets, node, kernel_ms, steps, step_s=None):
@@ -106,10 +111,12 @@ def roofline(fleets, node, kernel_ms, steps, step_s=None):
         f32 += f.B * a
         f64 += f.B * b
         cbytes += f.B * bytes_per_instance(f.model, f.N)
-    p32, p64 = valu_peaks()
+    p32, p64 = valu_peaks("spec")
     a32, a64 = f32 / t_k / 1e12, f64 / t_k / 1e12
     frac = a32 / p32 + a64 / p64
     achieved = a32 + a64
+    meas = valu_peaks("measured")
+    frac_meas = (a32 / meas[0] + a64 / meas[1]) if meas else None
     per_model = {}
     for f in fleets:
         per_model[(f.model, f.N)] = per_model.get((f.model, f.N), 0) + f.B
@@ -128,11 +135,16 @@ def roofline(fleets, node, kernel_ms, steps, step_s=None):
                       "note": "one of the step's %d concurrent launches (%d robots)" % (n_launch, fleets[0].B)}
     return {"bound": "valu", "achieved": round(achieved, 4), "peak": round(achieved / frac, 2), "unit": "TFLOP/s",
             "frac": round(frac, 6), "traffic": traffic, "per_launch": per_launch,
+            "peak_basis": "spec: FP32 157.3 TF (MI355X_MICROARCH.md), FP64 78.6 TF (AMD spec); each half of the flops "
+                          "priced at its own peak, frac = fp32 / FP32 peak + fp64 / FP64 peak",
+            "frac_measured_basis": (round(frac_meas, 6) if frac_meas is not None else None),
+            "measured_peaks_tflops": ({"fp32": meas[0], "fp64": meas[1],
+                                       "source": "tools/ubench_valu.hip full occupancy (profiles/%s/ubench_valu.json)"
+                                       % PROFILE_ROUND} if meas else None),
             "fp32": {"flop_per_step": f32, "achieved_tflops": round(a32, 4), "peak_tflops": p32,
                      "frac": round(a32 / p32, 6)},
             "fp64": {"flop_per_step": f64, "achieved_tflops": round(a64, 4), "peak_tflops": p64,
-                     "frac": round(a64 / p64, 6), "peak_source": "tools/ubench_valu.hip (profiles/%s/ubench_valu.json)"
-                     % PROFILE_ROUND},
+                     "frac": round(a64 / p64, 6)},
             "issue": ({k: pmc.get(k) for k in ("valu_insts_per_wave", "valu_issue_frac", "valu_issue_est_frac",
                                                "valu_active_frac", "valu_fma_f64_per_wave", "wait_frac",
                                                "active_frac", "source_commit")} if pmc else None),
@@ -413,7 +425,7 @@ def main():
             nthreads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
             cpu_rate, u0_err, nf, ns, rate_1 = cpu_baseline(fleets, args.cpu_sample, args.cpu_ticks, nthreads)
             cpu_base = {"value": round(cpu_rate, 1), "unit": "SQP-RTI iterations/sec", "cores": nthreads,
-                        "kind": "port",
+                        "kind": "port", "oracle_rule": "batched (the batched API's IPM exit rule; oracle/oracle.py RULES)",
                         "sample": f"{ns} instance-iterations: {'all' if args.cpu_sample <= 0 else args.cpu_sample} robots of each model x "
                                   f"{args.cpu_ticks} closed-loop ticks after the timed region, fp64 oracle/nmpc_oracle.c, "
                                   f"OpenMP {nthreads} threads, identical inputs", "failed": nf,

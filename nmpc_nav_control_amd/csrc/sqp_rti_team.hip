@@ -784,11 +784,18 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a)
                 for (int j = 0; j < NV; j++) Lr[j] = onehot[j] * dg;
                 double pivot;  // = M[0][0]
 #ifndef NMPC_MROW
-                m_block<M>(Lr, pivot, pg, Gd, gcs);  // column form: uniform constant rows + NGV broadcast rows
+                double m11, m10;
+                m_block<M>(Lr, pivot, m11, m10, pg, Gd, gcs);  // column form: uniform constant rows + 3 broadcast rows
+                STAMPF(4);
+#ifndef NMPC_SEQ_PIVOTS
+                if constexpr (NU == 2) {
+                    chol_input_2<NX>(Lr, pivot, m11, m10, r, fail);  // both pivots up front
+                } else
+#endif
 #else
                 mrow_pg_block<NX, NU>(Lr, pivot, pg, Gd);  // A/B: the row form (NX x NV broadcast FMAs)
-#endif
                 STAMPF(4);
+#endif
                 sfor<0, NU>([&](auto jc) {
                     constexpr int j = decltype(jc)::value;
                     if (!(pivot > 0.0)) fail = true;

@@ -159,10 +159,11 @@ __device__ __forceinline__ void gconst_load(GConst<M>& gc, const float (&gcol)[M
 // [B A] as uniform-operand FMAs over their structural nonzeros (diff and tric 10, omni4 20), the first mcol_nbc rows
 // as fused-DPP FMAs broadcasting G[i][r] from lane r (3 x NV). The row form it replaces (lane r: M[r][j] +=
 // PG[i][j] from lane j times G[i][r]) needed NX x NV broadcast FMAs: diff 63 -> 37, omni4 165 -> 65.
-// pivot = M[0][0] (lane 0's diagonal).
+// pivot = M[0][0] (lane 0's diagonal); NU = 2 also m11 = M[1][1] and m10 = M[0][1] (the input block, whose two
+// pivots are then known at once: chol_input_2).
 template <class M>
-__device__ __forceinline__ void m_block(double (&Lr)[M::NX + M::NU], double& pivot, const double (&pg)[M::NX],
-                                        const double (&gd)[M::NX], const GConst<M>& gc)
+__device__ __forceinline__ void m_block(double (&Lr)[M::NX + M::NU], double& pivot, double& m11, double& m10,
+                                        const double (&pg)[M::NX], const double (&gd)[M::NX], const GConst<M>& gc)
 {
     constexpr int NX = M::NX, NU = M::NU, NV = NX + NU;
     static_assert(mcol_nbc<M>() == 3, "generated broadcast blocks cover three rows");
@@ -173,8 +174,34 @@ __device__ __forceinline__ void m_block(double (&Lr)[M::NX + M::NU], double& piv
             if constexpr ((M::gmask(i) >> r) & 1u) Lr[r] = __builtin_fma(gc.v[i][r], pg[i], Lr[r]);
         });
     });
-    if constexpr (NX == 7 && NU == 2) mcol_var_block_7_2_3(Lr, pivot, pg, gd);
-    else mcol_var_block_11_4_3(Lr, pivot, pg, gd);
+    if constexpr (NX == 7 && NU == 2) {
+        mcol_var_block_7_2_3(Lr, pivot, m11, m10, pg, gd);
+    } else {
+        mcol_var_block_11_4_3(Lr, pivot, pg, gd);
+        m11 = m10 = 0.0;
+    }
+}
+
+// Right-looking Cholesky of a 2 x 2 input block held row-wise (lane r: Lr = row r of M, m00 / m11 / m10 its
+// entries broadcast to every lane), leaving the Schur complement in the state block. Both pivots come from the
+// block up front -- d0 = M00, d1 = M11 - M10^2 / M00 = det / M00 with det = M00 M11 - M10^2, so
+// 1 / sqrt(d1) = sqrt(M00) / sqrt(det) = (M00 / sqrt(M00)) rsq(det) -- and their two rsq + Newton chains run side by
+// side instead of one after the other (the second waited for the first column's update). fail: a pivot <= 0.
+template <int NX>
+__device__ __forceinline__ void chol_input_2(double (&Lr)[NX + 2], double m00, double m11, double m10, int r, bool& fail)
+{
+    const double det = __builtin_fma(m00, m11, -(m10 * m10));
+    if (!(m00 > 0.0) || !(det > 0.0)) fail = true;
+    const double rd0 = drsq(fmax(m00, 1e-300));
+    const double rq = drsq(fmax(det, 1e-300));
+    const double rd1 = (m00 * rd0) * rq;
+    const double l0 = Lr[0] * rd0;
+    Lr[0] = l0;
+    if constexpr (NX == 7) chol_update_np_7_2_0(Lr, l0);
+    const double l1 = (r >= 1) ? Lr[1] * rd1 : 0.0;
+    Lr[1] = l1;
+    if constexpr (NX == 7) chol_update_np_7_2_1(Lr, l1);
+    static_assert(NX == 7, "generated for NX = 7 (diff, tric)");
 }
 
 template <int NX, int NU, int J>

@@ -173,3 +173,15 @@ def test_descriptors_pinned_to_the_reference_loader():
             assert (d["lbu"], d["ubu"]) == ([-ref["A_MAX"], -ref["DALPHA_MAX"]], [ref["A_MAX"], ref["DALPHA_MAX"]])
         else:
             assert d["lbu"] == [-ref["A_MAX"]] * nb and d["ubu"] == [ref["A_MAX"]] * nb
+
+
+def test_team_asm_header_is_generated():
+    """csrc/team_asm_gen.hpp is the output of tools/gen_team_asm.py, byte for byte (the kernels'
+    fused-DPP asm blocks are edited in the generator, never in the header)."""
+    import importlib.util
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location("gen_team_asm", os.path.join(root, "tools", "gen_team_asm.py"))
+    gen = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(gen)
+    with open(gen.OUT) as fh:
+        assert fh.read() == gen.generate(), "team_asm_gen.hpp differs from tools/gen_team_asm.py: regenerate it"

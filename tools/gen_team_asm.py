@@ -8,9 +8,11 @@ written and no accumulator is a DPP source), and the terms are ordered so that c
 accumulators. Measured on MI355X (scratch microbenchmark, one wave per SIMD): v_fmac_f64_dpp 5.6 cycles,
 s_nop 1 8.4 cycles, so per-term nops would cost more than the FMAs.
 
-Usage: python tools/gen_team_asm.py   (rewrites the header; `make` in csrc does not run it)
+Usage: python tools/gen_team_asm.py [out]   (rewrites the header; `make` in csrc does not run it;
+tests/test_codegen.py::test_team_asm_header_is_generated checks the committed header against generate())
 """
 import os
+import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUT = os.path.join(ROOT, "nmpc_nav_control_amd", "csrc", "team_asm_gen.hpp")
@@ -59,17 +61,25 @@ def mcol_var_block(nx, nu, ngv):
     # ngv state-dependent rows i of [B A] (lane r holds column r of [B A], lane j column j of P [B A]); the constant
     # rows are the caller's uniform-operand FMAs (team_common.hpp m_block). Then md0 = bcast_0(acc[0]), the first
     # pivot. M is symmetric, so lane j's column j is its row j. Operands: acc 0..nv-1 (+v), md0 (=v), Gd.., pg..
+    # NU = 2 also broadcasts M[1][1] and M[0][1] (m11, m10): both input pivots then come from the 2 x 2 block at
+    # once (the second as det / M00), so their rsq chains run side by side (sqp_rti_team.hip P1)
     nv = nx + nu
+    npv = 3 if nu == 2 else 1
     lines = ["s_nop 1"]
     for i in range(ngv):
         for r in range(nv):
-            lines.append(f"v_fmac_f64_dpp %{r}, %{nv + 1 + i}, %{nv + 1 + ngv + i} row_newbcast:{r}{M}")
+            lines.append(f"v_fmac_f64_dpp %{r}, %{nv + npv + i}, %{nv + npv + ngv + i} row_newbcast:{r}{M}")
     lines.append("s_nop 1")
     lines.append(f"v_mov_b64_dpp %{nv}, %0 row_newbcast:0{M}")
-    outs = ", ".join([f'"+v"(acc[{r}])' for r in range(nv)] + ['"=&v"(md0)'])
+    if npv == 3:
+        lines.append(f"v_mov_b64_dpp %{nv + 1}, %1 row_newbcast:1{M}")
+        lines.append(f"v_mov_b64_dpp %{nv + 2}, %0 row_newbcast:1{M}")
+    outs = ", ".join([f'"+v"(acc[{r}])' for r in range(nv)] + ['"=&v"(md0)'] +
+                     (['"=&v"(m11)', '"=&v"(m10)'] if npv == 3 else []))
     ins = ", ".join([f'"v"(gd[{i}])' for i in range(ngv)] + [f'"v"(pg[{i}])' for i in range(ngv)])
     body = "\\n\\t".join(lines)
-    return (f"__device__ __forceinline__ void mcol_var_block_{nx}_{nu}_{ngv}(double (&acc)[{nv}], double& md0,"
+    extra = ", double& m11, double& m10" if npv == 3 else ""
+    return (f"__device__ __forceinline__ void mcol_var_block_{nx}_{nu}_{ngv}(double (&acc)[{nv}], double& md0{extra},"
             f" const double (&pg)[{nx}], const double (&gd)[{nx}])\n{{\n    asm(\"{body}\"\n        : {outs}\n"
             f"        : {ins});\n}}\n")
 
@@ -95,6 +105,16 @@ def chol_update(nx, nu):
         body = "\\n\\t".join(lines)
         out.append(f"__device__ __forceinline__ void chol_update_{nx}_{nu}_{j}(double (&lr)[{nv}], double lj, double& piv)\n"
                    f"{{\n    asm(\"{body}\"\n        : {outs}\n        : \"v\"(lj));\n}}\n")
+    # the same updates without the next pivot's broadcast (input columns j < nu, when the pivots are known up front)
+    for j in range(nu):
+        lines = ["s_nop 1"]
+        ops = []
+        for k, jp in enumerate(range(j + 1, nv)):
+            lines.append(f"v_fmac_f64_dpp %{k}, -%{nv - j - 1}, %{nv - j - 1} row_newbcast:{jp}{M}")
+            ops.append(f'"+v"(lr[{jp}])')
+        body = "\\n\\t".join(lines)
+        out.append(f"__device__ __forceinline__ void chol_update_np_{nx}_{nu}_{j}(double (&lr)[{nv}], double lj)\n"
+                   f"{{\n    asm(\"{body}\"\n        : {', '.join(ops)}\n        : \"v\"(lj));\n}}\n")
     # dispatcher
     cases = "\n".join(f"    if constexpr (J == {j}) chol_update_{nx}_{nu}_{j}(lr, lj, piv);" for j in range(nv - 1))
     out.append(f"template <int J>\n__device__ __forceinline__ void chol_update_{nx}_{nu}(double (&lr)[{nv}], double lj,"
@@ -218,7 +238,7 @@ def mst_vdot(n, off):
             f"    return acc + p1;\n}}\n")
 
 
-def main():
+def generate():
     parts = ["// team_asm_gen.hpp -- GENERATED by tools/gen_team_asm.py; do not edit.",
              "// Whole-block fused-DPP kernels of the team Riccati step (see the generator's docstring).",
              "#pragma once", "", "#include <hip/hip_runtime.h>", "", "namespace nmpc {", ""]
@@ -229,9 +249,14 @@ def main():
                   dot_f32(nx, nu, f"dot_x_{nx}_{nu}"), dot_f32(nv, 0, f"dot_v_{nx}_{nu}"),
                   mst_rowmul(nx, nu), mst_rowmul_lt(nx, nu), mst_rowdot(nx, nu), mst_chol(nx, nu), mst_trsv(nx, nu), mst_vdot(nx, nu)]
     parts += ["}  // namespace nmpc", ""]
-    with open(OUT, "w") as fh:
-        fh.write("\n".join(parts))
-    print("wrote", OUT)
+    return "\n".join(parts)
+
+
+def main():
+    out = sys.argv[1] if len(sys.argv) > 1 else OUT
+    with open(out, "w") as fh:
+        fh.write(generate())
+    print("wrote", out)
 
 
 if __name__ == "__main__":
