@@ -37,6 +37,8 @@ struct nmpc_batch {
     // horizon segments of the row-parallel kernel (sqp_rti_rowpar.hip SEG): -1 = chosen per launch (seg_count),
     // 0 = the serial phases B / C, S > 0 = S segments when N % S == 0 (NMPC_AMD_SEG overrides)
     int seg = -1;
+    // rows that may hold a segment above 256 robots: the first wave's 4 (NMPC_AMD_SEG_ROWS = 8: both waves, A/B)
+    int seg_rows = 4;
     int* iter_key = nullptr;     // [capacity] last executed IPM iterations per robot (written by the team kernel)
     int* order = nullptr;        // [capacity] team slot -> robot
     unsigned char* warm = nullptr;  // [capacity] the robot's last solve succeeded: its scratch records hold its
@@ -161,21 +163,30 @@ inline int seg_count(int N, int rows)
     return best;
 }
 
+// LDS a row-parallel launch of B robots may give each block: the CU's 160 KiB shared by the ceil(B / 256) robots
+// each CU holds (one block per robot on 256 CUs), so that every robot of the launch is resident at once
+inline size_t rowpar_lds_cap(int B)
+{
+    const int per_cu = (B + 255) / 256;
+    return (size_t)163840 / (size_t)(per_cu > 0 ? per_cu : 1);
+}
+
 template <class M>
 bool rowpar_ok(const nmpc_batch* b, KArgs& a, int mode)
 {
     if (b->kp.ipm != NMPC_IPM_SINGLE || a.segs || a.B > b->rowpar_max) return false;
-    const int rows = a.B <= 256 ? 16 : 4;  // segments: any row up to 256 robots, the first wave's rows above
+    const int rows = a.B <= 256 ? 16 : b->seg_rows;  // segments: any row up to 256 robots, the first wave's above
+    const size_t cap = rowpar_lds_cap(a.B);
     int S = b->seg >= 0 ? b->seg : seg_count(b->prm.N, rows);
     if (S > rows || S > kSegMax || (S > 0 && b->prm.N % S)) S = 0;
-    if (S > 0 && rowpar_lds_bytes<M>(b->prm.N, mode, S) > 65536) S = 0;
+    if (S > 0 && rowpar_lds_bytes<M>(b->prm.N, mode, S) > cap) S = 0;
     if (a.B > 256 && S == 0 && b->seg < 0) return false;  // one wave per robot only with segments (auto)
     // above 256 robots two robots' waves share a SIMD, which needs <= 256 registers per lane: diff and tric's
     // segmented kernels take 246-250, omni4's (11 x 11 master blocks) 357 (tools/reg_usage.py), so omni4 keeps the
     // team kernel there
     if (a.B > 256 && M::NU == 4 && b->rowpar_max <= 1024) return false;
     a.seg = S;
-    return rowpar_lds_bytes<M>(b->prm.N, mode, S) <= 65536;
+    return rowpar_lds_bytes<M>(b->prm.N, mode, S) <= cap;
 }
 
 // Records one sweep of the team kernel touches over the handle's capacity in the wide layout (9 or 16 slots of
@@ -475,6 +486,7 @@ int nmpc_batch_create(const nmpc_model_params* prm, int capacity, nmpc_batch** o
     if (const char* v = std::getenv("NMPC_AMD_ROWPAR_MAX")) b->rowpar_max = std::atoi(v);  // A/B: 0 = never
     if (const char* v = std::getenv("NMPC_AMD_SEG")) b->seg = std::atoi(v);  // A/B: 0 = serial, S = S segments
     if (const char* v = std::getenv("NMPC_AMD_ROWPAR_W")) b->rowpar_w = std::atoi(v) == 1 ? 1 : 2;  // A/B
+    if (const char* v = std::getenv("NMPC_AMD_SEG_ROWS")) b->seg_rows = std::atoi(v) == 8 ? 8 : 4;  // A/B
 #ifdef NMPC_HYBRID
     if (const char* v = std::getenv("NMPC_AMD_HYBRID")) b->hybrid_h = std::atoi(v);  // A/B: 0 = off
     if (const char* v = std::getenv("NMPC_AMD_HYBRID_CAP")) b->hybrid_cap = std::atoi(v);

@@ -14,7 +14,9 @@
 // reductions (LDS) combine the rows; the Riccati factorisation (phase B: fp64 P G, G'P G, input-block Cholesky,
 // rhs) and the forward recursion of the directions (phase C) are the only stage-serial passes, and every wave
 // computes them identically on its row 0 (same records, same DPP broadcasts inside the row), so no wave waits on
-// another; wave 0 stores them, the other waves store to a per-wave dummy block. P0 likewise: the RK4
+// another; wave 0 stores them, the other waves store to pads. The fields an IPM iteration makes and uses up stay in
+// LDS (ItLds: barrier weights, rhs terms, factor columns, the direction), so only the iterate, slacks and
+// multipliers are written back to the global records per iteration. P0 likewise: the RK4
 // linearisation of stage k on row k mod 4 W, then the serial initial-iterate pass from LDS.
 // One robot per block also makes every loop exit block-uniform (no lockstep teams).
 #include "nmpc_kernels.hpp"
@@ -22,26 +24,33 @@
 
 namespace nmpc {
 
-// Record layout: TeamRec<M, true> (the team kernel's single-direction layout: the warm-start multipliers LL / LU,
-// the DZ plane and the record stride are shared, so a handle may alternate kernels between solves) plus three
-// fields the team kernel leaves unused under the single-direction rule (its RU / DZA slots and the DZ register
-// slot): SIG (barrier weight), C0 (h z + g - (l_lo - l_up), the stationarity term without the adjoint) and GH
-// (the bound part of the rhs), written by phase A for phase B.
+// Record layout: TeamRec<M, true> (the team kernel's single-direction layout: the warm-start multipliers LL / LU
+// and the record stride are shared, so a handle may alternate kernels between solves). Global memory keeps what
+// outlives an IPM iteration -- the iterate Z, slacks / multipliers TL TU LL LU (phase A), bounds LB UB, Jacobian rows
+// GV and gradient GR (P0) -- and the fields an iteration makes and uses up live in LDS (ItLds): SIG (barrier
+// weight), C0 (h z + g - (l_lo - l_up), the stationarity term without the adjoint) and GH (the bound part of the
+// rhs) from phase A for phase B, LR / LM (the factor's input columns and rhs) from phase B for phase C, DZ (the
+// direction) from phase C for phases D and A. SIG / C0 / GH are register-image slots past GR only.
 template <class M>
 struct RowRec {
     using T = TeamRec<M, true>;
     static constexpr int NX = M::NX, NU = M::NU, NV = NX + NU, NGV = M::NGV;
     static constexpr int LR = T::LR, LM = T::LM, Z = T::Z, TL = T::TL, TU = T::TU, LL = T::LL, LU = T::LU;
     static constexpr int LB = T::LB, UB = T::UB, GV = T::GV, GR = T::GR, RS = T::RS, RSS = T::RSS;
-    // GH goes to the LR slot when the stored record has no room past C0 (tric: 16 stored floats): phase A writes
-    // it there after the previous phase C has read LR, and phase B reads it before it stores the new LR
-    static constexpr bool GH_IN_LR = GR + 3 >= RSS;
-    static constexpr int SIG = GR + 1, C0 = GR + 2, GH = GH_IN_LR ? T::LR : GR + 3;
-    static_assert(C0 < RSS && GH < RSS, "phase-A fields fit the stored team record");
-    static_assert(T::L2 ? (SIG == T::RU && C0 == T::DZA) : (SIG > T::DZA && SIG > T::RU),
-                  "phase-A fields reuse only slots the single-direction team kernel leaves unused");
-    static constexpr int BF1 = GH_IN_LR ? C0 + 1 : GH + 1;  // phase B's contiguous fields [GV, BF1) (+ GH)
+    static constexpr int SIG = GR + 1, C0 = GR + 2, GH = GR + 3;
+    static_assert(GH < RS, "phase-A fields fit the register image");
     static_assert(LM + NU <= Z && Z < TL, "LR / LM below Z");
+};
+
+// The per-iteration stage fields in LDS (RowRec): [N+1][NF][NV] floats, live slots only (lane r < NV reads / writes
+// slot r; idle lanes read slot 0 and write a pad). Round 4 kept them in the global records, which cost about 1.06 KB
+// of writes per robot, stage and IPM iteration at diff1024 (phase A's SIG / C0 / GH sector, phase B's LR / LM into
+// the sector phase A had just written, the DZ plane): 6.3x the fetched bytes
+template <class M>
+struct ItLds {
+    static constexpr int NU = M::NU, NV = M::NX + M::NU;
+    static constexpr int SIG = 0, C0 = 1, GH = 2, LR = 3, LM = 4, DZ = 4 + NU, NF = 5 + NU;
+    __host__ __device__ static constexpr size_t floats(int N) { return (size_t)(N + 1) * NF * NV; }
 };
 
 // LDS of the segmented phases (SEG, a.seg = S > 0), in floats from its base (8-byte aligned; fp64 parts at even
@@ -51,42 +60,55 @@ struct RowRec {
 template <class M>
 struct SegLayout {
     static constexpr int NX = M::NX, NU = M::NU, NXP = (M::NX + 3) / 4 * 4;
-    int SUM_P, SUM_PB, SUM_PHI, SUM_GAM, SUM_T, QS, CS, PHS, LT, SL, ZL;
+    int SUM_P, SUM_PB, SUM_PHI, SUM_GAM, SUM_T, QS, CS, PHS, LT, XA, SL, ZL;
     __host__ __device__ explicit SegLayout(int S)
     {
         SUM_P = 0;                          // [S][NX][NX] double
-        SUM_PB = SUM_P + 2 * S * NX * NX;   // [S][NX]
+        SUM_GAM = SUM_P + 2 * S * NX * NX;  // [S][NX][NX] double (fp64 sum: the dual sweep factors -Gam_0)
+        SUM_PB = SUM_GAM + 2 * S * NX * NX; // [S][NX]
         SUM_PHI = SUM_PB + S * NX;          // [S][NX][NX]
-        SUM_GAM = SUM_PHI + S * NX * NX;    // [S][NX][NX]
-        SUM_T = SUM_GAM + S * NX * NX;      // [S][NX]
+        SUM_T = SUM_PHI + S * NX * NX;      // [S][NX]
         QS = (SUM_T + S * NX + 1) / 2 * 2;  // [S][NX][NX] double
         CS = QS + 2 * S * NX * NX;          // [S][NX] double
         PHS = CS + 2 * S * NX;              // [S][NX] double
-        LT = PHS + 2 * S * NX;              // [NX][NX] double: the master's transpose scratch
-        SL = LT + 2 * NX * NX;              // [S + 1][2][NX]: s_q, lam_q
+        LT = PHS + 2 * S * NX;              // [2][NX][NX] double: the master rows' transpose scratch
+        XA = LT + 4 * NX * NX;              // [2][NX + 1][NX] double: Phat_m, phat_m / Shat_m, shat_m for the join
+        SL = XA + 4 * (NX + 1) * NX;        // [S + 1][2][NX]: s_q, lam_q
         ZL = SL + (S + 1) * 2 * NX;         // [N + 1][NU][NXP]
     }
     __host__ __device__ size_t floats(int N) const { return (size_t)ZL + (size_t)(N + 1) * NU * NXP; }
 };
 
 // layout of the kernel's dynamic LDS (floats): P0's stage inputs [N+1][SF][16], reference poses [N+1][3], block
-// reductions [W][8], dx [N+1][16], unwrapped references [N+1][3]; then (SEG) the segment area, which reuses the
-// stage-input region when it fits there (P0 is done with it before the first IPM iteration)
+// reductions [W][8], dx [N+1][16], unwrapped references [N+1][3], 64 pad floats (per-lane store targets nobody
+// reads); then the IPM's per-iteration stage fields (ItLds) and (SEG) the segment area, each reusing the stage-input
+// region where it fits there (P0 is done with it before the first IPM iteration, behind a block barrier)
 template <class M>
 struct RowLds {
     static constexpr int SF = 5 + M::NGV;
-    // ... followed by 64 pad floats (per-lane store targets nobody reads)
+    __host__ __device__ static constexpr size_t r4(size_t f) { return (f + 3) / 4 * 4; }
+    __host__ __device__ static constexpr size_t stage_floats(int N) { return (size_t)(N + 1) * SF * 16; }
     __host__ __device__ static constexpr size_t pad_off(int N) { return (size_t)(N + 1) * (16 * SF + 3 + 16 + 3) + 32; }
     __host__ __device__ static constexpr size_t base_floats(int N) { return pad_off(N) + 64; }
+    __host__ __device__ static constexpr size_t it_off(int N)
+    {
+        return ItLds<M>::floats(N) <= stage_floats(N) ? 0 : r4(base_floats(N));
+    }
+    __host__ __device__ static constexpr size_t it_end(int N) { return r4(it_off(N) + ItLds<M>::floats(N)); }
     __host__ __device__ static size_t seg_off(int N, int S)
     {
-        return SegLayout<M>(S).floats(N) <= (size_t)(N + 1) * SF * 16 ? 0 : (base_floats(N) + 3) / 4 * 4;
+        const size_t sf = SegLayout<M>(S).floats(N);
+        if (it_off(N) == 0) return it_end(N) + sf <= stage_floats(N) ? it_end(N) : r4(base_floats(N));
+        return it_end(N);
     }
     __host__ __device__ static size_t floats(int N, int S)
     {
-        if (S <= 0) return base_floats(N);
-        const size_t end = seg_off(N, S) + SegLayout<M>(S).floats(N);
-        return end > base_floats(N) ? end : base_floats(N);
+        size_t end = base_floats(N) > it_end(N) ? base_floats(N) : it_end(N);
+        if (S > 0) {
+            const size_t se = seg_off(N, S) + SegLayout<M>(S).floats(N);
+            end = se > end ? se : end;
+        }
+        return end;
     }
 };
 
@@ -142,15 +164,14 @@ __device__ __forceinline__ float wave_min_rows(float v)
 }
 
 // W waves per robot (one per SIMD): the stage-parallel phases run on all 4 W rows; every wave runs the serial
-// phases (identically) and wave 0 stores their results (the other waves store into dummy stage blocks of the same
-// layout: per-lane scattered dummy addresses made the serial phases' stores 1.6x slower, measured).
+// phases (identically) and wave 0 stores their results (into LDS; the other waves store into pads).
 // SEG: the horizon is cut into a.seg segments of L = N / S stages whose Riccati sweeps (phase B) and forward
 // recursions (phase C) run at the same time, one segment per row, joined by a master recursion over the segment
 // boundaries (DESIGN.md "Segmented Riccati"); a robot's serial chain shrinks from N + 1 stage steps to L + 1 plus S - 1
 // master steps. The rhs is built in absolute form (no adjoint), so the stationarity residual of the stopping rule is
 // evaluated by its own serial adjoint pass, only when the rest of the exit test already holds.
 template <class M, int W, bool SEG>
-__global__ __launch_bounds__(64 * W, 1) void k_sqp_rti_rowpar(KParams P, KArgs a, int mode)
+__global__ __launch_bounds__(64 * W, (SEG && M::NX < 10) ? 2 : 1) void k_sqp_rti_rowpar(KParams P, KArgs a, int mode)
 {
     using R = RowRec<M>;
     constexpr int NX = M::NX, NU = M::NU, NV = R::NV, NGV = R::NGV, RS = R::RS, RSS = R::RSS;
@@ -193,14 +214,9 @@ __global__ __launch_bounds__(64 * W, 1) void k_sqp_rti_rowpar(KParams P, KArgs a
     float* const rbase = a.scratch + (size_t)inst * (N + 1) * KS;
     float* const tbase = rbase + (lv ? r : 0) * rec_lane<RSS, QM>();   // idle slots read slot 0
     float* const tbase_own = rbase + r * rec_lane<RSS, QM>();          // every lane's own slot
-    float* const dzbase = a.scratch + (size_t)a.sstride * (N + 1) * KS + (size_t)inst * (N + 1) * 16 + r;
     // Stores of the serial phases: wave 0 stores (its four rows the same values to the same addresses, as one
-    // row would); waves 1.. store into a dummy stage block of their own with the same slot layout (the same
-    // coalescing as the real store; nobody reads it). Idle slots and rows past the last stage of a stage-parallel
-    // phase store into tdummy.
-    float* const dummy = a.scratch + (size_t)a.sstride * (N + 1) * 16 * (RSS + 1);
-    float* const wblk = dummy + ((size_t)(inst & 255) * 4 + wave) * KS;      // this wave's dummy stage block
-    float* const wdz = dummy + (size_t)256 * 4 * KS + ((size_t)(inst & 255) * 4 + wave) * 16 + r;  // dummy DZ
+    // row would); the other waves store into pads. Idle slots and rows past the last stage of a stage-parallel
+    // phase store into tdummy (global records) or a pad (LDS).
     const bool w0 = wave == 0;
     float* const tdummy = rbase + (size_t)N * KS + 15 * rec_lane<RSS, QM>();  // nobody reads it
     const bool warm = P.warm && a.warm && a.warm[inst] == a.warm_tag && !(a.reset && a.reset[inst]);
@@ -274,6 +290,13 @@ __global__ __launch_bounds__(64 * W, 1) void k_sqp_rti_rowpar(KParams P, KArgs a
     // a per-lane LDS slot nobody reads: the target of P0's stores for lanes / rounds without data (a store under a
     // lane mask leaves the compiler's later waits uncounted, i.e. full drains)
     float* const lpad = s_row + RowLds<M>::pad_off(N) + (tid & 63);
+    // the IPM's per-iteration stage fields (ItLds): reads of idle lanes take slot 0, writes of lanes without an entry
+    // go to their pad
+    using IT = ItLds<M>;
+    float* const it_lds = s_row + RowLds<M>::it_off(N);
+    const int rv = lv ? r : 0;
+    auto it_rd = [&](int k, int f) -> float { return it_lds[((size_t)k * IT::NF + f) * NV + rv]; };
+    auto it_wr = [&](int k, int f, bool w) -> float* { return w ? it_lds + ((size_t)k * IT::NF + f) * NV + r : lpad; };
     {
         struct In {
             float x[NX], u[NU], y, xnext, tq;
@@ -473,7 +496,6 @@ __global__ __launch_bounds__(64 * W, 1) void k_sqp_rti_rowpar(KParams P, KArgs a
 #pragma unroll
         for (int i = 0; i < NGV; i++) rec[R::GV + i] = (k < N && lv) ? st[(5 + i) * 16] : 0.0f;
         rec_store_range<0, RSS, RS, QM>(kv ? tbase_own + (size_t)k * KS : tdummy, rec);  // idle slots: own unused slot
-        dzbase[(size_t)k * 16] = 0.0f;  // (rows past the end repeat stage N's zero)
     }
     {
         float v[6] = {wave_sum_rows(row_sum16(lv ? sum_c0 : 0.0f)), 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
@@ -482,12 +504,6 @@ __global__ __launch_bounds__(64 * W, 1) void k_sqp_rti_rowpar(KParams P, KArgs a
         sum_c0 = v[0];
     }
 
-    double onehot[NV];
-#pragma unroll
-    for (int j = 0; j < NV; j++) onehot[j] = (r == j) ? 1.0 : 0.0;
-    double gcol64[NX];
-#pragma unroll
-    for (int i = 0; i < NX; i++) gcol64[i] = (double)gcol[i];
 #ifdef NMPC_ROWPAR_MCOL
     // A/B only: the column-form M block needs 20 more registers, which pushes the segmented kernels past the 256
     // that two waves per SIMD allow (diff 250 -> 256 + 14 AGPRs; tests/test_reg_usage.py), so the row form stays
@@ -511,20 +527,33 @@ __global__ __launch_bounds__(64 * W, 1) void k_sqp_rti_rowpar(KParams P, KArgs a
         const float cr = dot_v<NX, NU>(0.0f, dzv, grow);
         return (xi >= NGV) ? cr : nx_;
     };
-    // phase B's record fields: [GV, BF1) and GH (in the LR slot when the stored record has no room past C0)
-    auto ld_bfields = [&](const float* p, float (&v)[RS]) {
-        ld_range<R::GV, R::BF1, RS, QM>(p, v);
-        if constexpr (R::GH_IN_LR) ld_range<R::GH, R::GH + 1, RS, QM>(p, v);
+    // the fields of one stage each serial pass reads: the Jacobian rows GV from the global record, the rest from LDS
+    // (phase B: SIG, C0, GH; phase C: LR, LM; the adjoint: C0)
+    auto ld_bfields = [&](int k, float (&v)[RS]) {
+        ld_range<R::GV, R::GV + NGV, RS, QM>(tbase + (size_t)k * KS, v);
+        v[R::SIG] = it_rd(k, IT::SIG);
+        v[R::C0] = it_rd(k, IT::C0);
+        v[R::GH] = it_rd(k, IT::GH);
     };
-    // serial sweep k0 -> k1 with the next stage's fields [F0, F1) in flight (BF: phase B's fields, ld_bfields)
+    auto ld_cfields = [&](int k, float (&v)[RS]) {
+        ld_range<R::GV, R::GV + NGV, RS, QM>(tbase + (size_t)k * KS, v);
+        v[R::LR] = it_rd(k, IT::LR);
+#pragma unroll
+        for (int qq = 0; qq < NU; qq++) v[R::LM + qq] = it_rd(k, IT::LM + qq);
+    };
+    auto ld_adj = [&](int k, float (&v)[RS]) {
+        ld_range<R::GV, R::GV + NGV, RS, QM>(tbase + (size_t)k * KS, v);
+        v[R::C0] = it_rd(k, IT::C0);
+    };
+    // phase B's factor output of stage k (LR, LM) into LDS; w: this lane stores it
+    auto st_lrlm = [&](int k, const float (&v)[RS], bool w) {
+        *it_wr(k, IT::LR, w) = v[R::LR];
+#pragma unroll
+        for (int qq = 0; qq < NU; qq++) *it_wr(k, IT::LM + qq, w) = v[R::LM + qq];
+    };
+    // serial sweep k0 -> k1 with the next stage's fields (load(k, v)) in flight
     // (ping-pong buffers, loads never predicated: the loop is wave-uniform)
-    auto serial = [&](auto f0c, auto f1c, auto bfc, int k0, int k1, int dir, auto&& body) {
-        constexpr int F0 = decltype(f0c)::value, F1 = decltype(f1c)::value;
-        constexpr bool BF = decltype(bfc)::value;
-        auto load = [&](int k, float (&v)[RS]) {
-            if constexpr (BF) ld_bfields(tbase + (size_t)k * KS, v);
-            else ld_range<F0, F1, RS, QM>(tbase + (size_t)k * KS, v);
-        };
+    auto serial = [&](int k0, int k1, int dir, auto&& load, auto&& body) {
         float ra[RS], rb[RS];
         load(k0, ra);
         for (int k = k0;; k += 2 * dir) {
@@ -548,7 +577,7 @@ __global__ __launch_bounds__(64 * W, 1) void k_sqp_rti_rowpar(KParams P, KArgs a
             const int kr = j * ROWS + q;
             const int k = kr <= N ? kr : N;
             ld_range<F0, F1, RS, QM>(tbase + (size_t)k * KS, v);
-            dzv = dzbase[(size_t)k * 16];
+            dzv = it_rd(k, IT::DZ);
         };
         float ra[RS], rb[RS], da, db;
         load(0, ra, da);
@@ -568,8 +597,7 @@ __global__ __launch_bounds__(64 * W, 1) void k_sqp_rti_rowpar(KParams P, KArgs a
     float* const seg_lds = s_row + (SEG ? RowLds<M>::seg_off(N, a.seg) : 0);
     auto adjoint = [&](float& res_stat, float& cpi_max) {
         float piv = 0.0f, rs = 0.0f, cm = 0.0f;
-        serial(std::integral_constant<int, R::GV>{}, std::integral_constant<int, R::C0 + 1>{}, std::false_type{}, N, 0,
-               -1, [&](int k, float (&rc)[RS]) {
+        serial(N, 0, -1, ld_adj, [&](int k, float (&rc)[RS]) {
             const bool vu = is_u && k < N;
             const bool vx = is_x && k >= 1;
             float Gc[NX];
@@ -608,6 +636,7 @@ __global__ __launch_bounds__(64 * W, 1) void k_sqp_rti_rowpar(KParams P, KArgs a
             {
                 const float rl = z - lb - tl, rr = ubd - z - tu;
                 const float itl = frcp(tl), itu = frcp(tu);
+                dz = (it > 0) ? dz : 0.0f;  // (iteration 0 applies no step; the LDS field is not written yet)
                 const BoundDir d = bound_dir(dz, rl, rr, tl, tu, ll, lu, itl, itu, sigma_mu, sigma_mu);
                 const float ab = bnd ? a_upd : 0.0f, av = valid ? a_upd : 0.0f;
                 tl += ab * d.dtl;
@@ -635,17 +664,11 @@ __global__ __launch_bounds__(64 * W, 1) void k_sqp_rti_rowpar(KParams P, KArgs a
             rc[R::TU] = tu;
             rc[R::LL] = ll;
             rc[R::LU] = lu;
-            rc[R::SIG] = sig;
-            rc[R::C0] = c0;
-            rc[R::GH] = valid ? gh : 0.0f;
             float* const pk = (lv && kv) ? tbase + (size_t)k * KS : tdummy;
-            rec_store_range<R::Z, R::LU + 1, RS, QM>(pk, rc);
-            if constexpr (R::GH_IN_LR) {
-                rec_store_range<R::SIG, R::C0 + 1, RS, QM>(pk, rc);
-                rec_store_range<R::GH, R::GH + 1, RS, QM>(pk, rc);
-            } else {
-                rec_store_range<R::SIG, R::GH + 1, RS, QM>(pk, rc);
-            }
+            rec_store_range<R::Z, R::LU + 1, RS, QM>(pk, rc);  // the iterate and slacks / multipliers: global
+            *it_wr(k, IT::SIG, lv && kv) = sig;  // phase B's inputs: LDS
+            *it_wr(k, IT::C0, lv && kv) = c0;
+            *it_wr(k, IT::GH, lv && kv) = valid ? gh : 0.0f;
         });
         {
             float v[6] = {wave_sum_rows(row_sum16(lv ? sum_c : 0.0f)), wave_max_rows(row_max16(lv ? max_c : 0.0f)),
@@ -707,11 +730,15 @@ __global__ __launch_bounds__(64 * W, 1) void k_sqp_rti_rowpar(KParams P, KArgs a
             const int Sg = a.seg, Ls = N / Sg;
             const bool srow = q < Sg, slast = q == Sg - 1;
             double Lrow[NV];
-            float pv = 0.0f, Phi[NX], Gam[NX], tt = 0.0f, nanb = 0.0f;
+            float pv = 0.0f, Phi[NX], tt = 0.0f, nanb = 0.0f;
+            double Gam[NX];  // fp64 sum of exact fp32 products (an fp32 sum broke the dual sweep's factor of -Gam_0)
 #pragma unroll
             for (int j = 0; j < NV; j++) Lrow[j] = 0.0;
 #pragma unroll
-            for (int c = 0; c < NX; c++) Phi[c] = Gam[c] = 0.0f;
+            for (int c = 0; c < NX; c++) {
+                Phi[c] = 0.0f;
+                Gam[c] = 0.0;
+            }
             bool fail = false;
             if (4 * wave < Sg) {  // (wave-uniform) the wave holds a segment
                 auto kof = [&](int j) { return srow ? (q + 1) * Ls - j : N; };
@@ -736,7 +763,7 @@ __global__ __launch_bounds__(64 * W, 1) void k_sqp_rti_rowpar(KParams P, KArgs a
                     }
                     double Gd[NX];
 #pragma unroll
-                    for (int l = 0; l < NX; l++) Gd[l] = (l < NGV) ? (double)Gc[l] : gcol64[l];
+                    for (int l = 0; l < NX; l++) Gd[l] = (double)Gc[l];
                     double pg[NX];
 #pragma unroll
                     for (int i = 0; i < NX; i++) pg[i] = 0.0;
@@ -744,7 +771,7 @@ __global__ __launch_bounds__(64 * W, 1) void k_sqp_rti_rowpar(KParams P, KArgs a
                     const double dg = valid ? (double)h_stage + (double)sig : 1.0;
                     double Lr[NV];
 #pragma unroll
-                    for (int jj = 0; jj < NV; jj++) Lr[jj] = onehot[jj] * dg;
+                    for (int jj = 0; jj < NV; jj++) Lr[jj] = (r == jj) ? dg : 0.0;
                     double pivot;
 #ifdef NMPC_ROWPAR_MCOL
                     m_block<M>(Lr, pivot, pg, Gd, gcs);
@@ -804,9 +831,9 @@ __global__ __launch_bounds__(64 * W, 1) void k_sqp_rti_rowpar(KParams P, KArgs a
                     }
 #pragma unroll
                     for (int c = 0; c < NX; c++) {
-                        float g = Gam[c];
+                        double g = Gam[c];
 #pragma unroll
-                        for (int j2 = 0; j2 < NU; j2++) g -= zi[j2] * zc[j2][c];
+                        for (int j2 = 0; j2 < NU; j2++) g -= (double)zi[j2] * (double)zc[j2][c];
                         Gam[c] = g;
                         float s = zc[0][c];
 #pragma unroll
@@ -822,10 +849,9 @@ __global__ __launch_bounds__(64 * W, 1) void k_sqp_rti_rowpar(KParams P, KArgs a
                     }
 #pragma unroll
                     for (int jj = 0; jj < NV; jj++) Lrow[jj] = Lr[jj];
-                    rec_store_range<R::LR, R::LM + NU, RS, QM>(
-                        lv ? (srow ? tbase + (size_t)k * KS : wblk + r * rec_lane<RSS, QM>()) : tdummy, rc);
+                    st_lrlm(k, rc, lv && srow);
                 };
-                auto load = [&](int j, float (&v)[RS]) { ld_bfields(tbase + (size_t)kof(j) * KS, v); };
+                auto load = [&](int j, float (&v)[RS]) { ld_bfields(kof(j), v); };
                 float ra[RS], rb[RS];
                 load(0, ra);
                 for (int j = 0;; j += 2) {
@@ -846,7 +872,7 @@ __global__ __launch_bounds__(64 * W, 1) void k_sqp_rti_rowpar(KParams P, KArgs a
 #pragma unroll
                     for (int c = 0; c < NX; c++) {
                         seg_lds[SegL.SUM_PHI + (q * NX + xi) * NX + c] = Phi[c];
-                        seg_lds[SegL.SUM_GAM + (q * NX + xi) * NX + c] = Gam[c];
+                        reinterpret_cast<double*>(seg_lds + SegL.SUM_GAM)[(q * NX + xi) * NX + c] = Gam[c];
                     }
                 }
             }
@@ -866,37 +892,58 @@ __global__ __launch_bounds__(64 * W, 1) void k_sqp_rti_rowpar(KParams P, KArgs a
             }
             RP_STAMP(4 + 4 * it);
 
-            // ---- master (row 0 of wave 0, fp64): the two-point recursion over the segment boundaries,
-            //   s_{i+1} = Phi_i' s_i + Gam_i lam_{i+1} + t_i,   lam_i = P_i s_i + pbar_i + Phi_i lam_{i+1},
-            // backward lam_i = Phat_i s_i + phat_i with Q_i = Phat_{i+1} (I - Gam_i Phat_{i+1})^-1, formed through the
-            // factor L L' = Phat_{i+1} as Q_i = Y Y', Y = L R^-T, R R' = K = I - L' Gam_i L (K >= I: Cholesky without
-            // pivoting; Q_i positive semidefinite by construction), forward from s_0 = 0. Lane NU + r holds row r of every matrix and element r
-            // of every vector (the fused-DPP blocks of team_asm_gen.hpp); segment data come from LDS
-            if (tid < 16 && Sg > 1) {
+            // ---- master (fp64): the two-point recursion over the segment boundaries,
+            //   s_{i+1} = Phi_i' s_i + Gam_i lam_{i+1} + t_i,   lam_i = P_i s_i + pbar_i + Phi_i lam_{i+1}   (s_0 = 0),
+            // solved from both ends at once and joined at boundary m = S / 2 (round 5: the chain of factorisations
+            // falls from S - 1 boundary steps to max(S - 1 - m, m - 1) + 1, e.g. 7 -> 4 at N = 80, S = 8, 3 -> 2 at S = 4):
+            //  - row 0 of wave 0, the backward sweep lam_i = Phat_i s_i + phat_i (Phat_{S-1} = P_{S-1}) down to m, with
+            //    Q_i = Phat_{i+1} (I - Gam_i Phat_{i+1})^-1, Phat_i = P_i + Phi_i Q_i Phi_i', c_i = t_i + Gam_i phat_{i+1},
+            //    phat_i = pbar_i + Phi_i (Q_i c_i + phat_{i+1});
+            //  - row 0 of wave 1 (wave 0 after the backward sweep when the block has one wave), the dual sweep
+            //    s_i = -Shat_i lam_i + shat_i (Shat_1 = -Gam_0, shat_1 = t_0) up to m, with Q'_i = (I + Shat_i P_i)^-1 Shat_i,
+            //    Shat_{i+1} = -Gam_i + Phi_i' Q'_i Phi_i, u_i = shat_i - Q'_i (pbar_i + P_i shat_i), shat_{i+1} = t_i + Phi_i' u_i;
+            //  - the join (row 0 of wave 0): lam_m = Q_j (shat_m - Shat_m phat_m) + phat_m with Q_j = Phat_m (I + Shat_m
+            //    Phat_m)^-1, s_m = shat_m - Shat_m lam_m;
+            //  - then wave 0 propagates s, lam forward to S - 1 (lam_{i+1} = Q_i (Phi_i' s_i + c_i) + phat_{i+1}, s_{i+1} =
+            //    Phi_i' s_i + Gam_i lam_{i+1} + t_i) while the dual row propagates them back to 1 (s_i = u_i - Q'_i Phi_i
+            //    lam_{i+1}, lam_i = P_i s_i + pbar_i + Phi_i lam_{i+1}).
+            // Every Q (Q_i, Q'_i, Q_j) is A (I + C A)^-1 = L (I + L' C L)^-1 L' with C >= 0, formed through the factor
+            // L L' = A (pivots below 1e-13 of their diagonal entry dropped) as Y Y', Y = L R^-T, R R' = K = I + L' C L (K >= I:
+            // Cholesky without pivoting; positive semidefinite by construction; the Woodbury form and a factor of -Gam
+            // both failed numerically, tools/seg_case_study.py). Lane NU + r holds row r of every matrix and element r of
+            // every vector (the fused-DPP blocks of team_asm_gen.hpp); segment data come from LDS
+#ifdef NMPC_SEQ_MASTER
+            constexpr bool kSeqM = true;  // A/B only: the round-4 master (backward over all S - 1 boundaries, then forward)
+#else
+            constexpr bool kSeqM = false;
+#endif
+            const int mj = kSeqM ? 0 : Sg / 2;        // the join boundary (1 <= m <= S - 1)
+            const bool mrow0 = tid < 16;              // backward sweep, join, forward propagation
+            const bool mrowd = (W > 1) ? (tid >= 64 && tid < 80) : (tid < 16);  // the dual sweep
+            if (Sg > 1 && (mrow0 || mrowd)) {
                 const double* const sP = reinterpret_cast<const double*>(seg_lds + SegL.SUM_P);
                 double* const sQ = reinterpret_cast<double*>(seg_lds + SegL.QS);
                 double* const sCv = reinterpret_cast<double*>(seg_lds + SegL.CS);
                 double* const sPh = reinterpret_cast<double*>(seg_lds + SegL.PHS);
-                double* const sLt = reinterpret_cast<double*>(seg_lds + SegL.LT);
+                double* const sLt = reinterpret_cast<double*>(seg_lds + SegL.LT) + (wave > 0 ? NX * NX : 0);
+                double* const sXa = reinterpret_cast<double*>(seg_lds + SegL.XA);
                 auto ldrow = [&](int i, int off, double (&v)[NX]) {  // row xi of segment i's fp32 matrix at off
 #pragma unroll
                     for (int c = 0; c < NX; c++) v[c] = (double)seg_lds[off + (i * NX + xi) * NX + c];
                 };
-                double Ph[NX], ph;
+                auto ldgam = [&](int i, double (&v)[NX]) {  // row xi of Gam_i (fp64)
 #pragma unroll
-                for (int c = 0; c < NX; c++) Ph[c] = sP[((size_t)(Sg - 1) * NX + xi) * NX + c];
-                ph = (double)seg_lds[SegL.SUM_PB + (Sg - 1) * NX + xi];
-                for (int i = Sg - 2; i >= 0; i--) {
-                    double Fr[NX], Gr[NX], Gn[NX];
-                    ldrow(i, SegL.SUM_PHI, Fr);
-                    ldrow(i, SegL.SUM_GAM, Gr);
+                    for (int c = 0; c < NX; c++) v[c] = reinterpret_cast<const double*>(seg_lds + SegL.SUM_GAM)[(i * NX + xi) * NX + c];
+                };
+                auto ldcol = [&](int i, int off, double (&v)[NX]) {  // column xi (row xi of the transpose)
 #pragma unroll
-                    for (int c = 0; c < NX; c++) Gn[c] = -Gr[c];
-                    const double ti = (double)seg_lds[SegL.SUM_T + i * NX + xi];
-                    // L L' = Phat (pivots below 1e-13 of their diagonal entry dropped), L' through the LDS scratch
+                    for (int c = 0; c < NX; c++) v[c] = (double)seg_lds[off + (i * NX + c) * NX + xi];
+                };
+                // Q = L (I + L' C L)^-1 L' from A = L L' (row r of A in Ar, of C in Cr): the master's factorisations
+                auto qform = [&](const double (&Ar)[NX], const double (&Cr)[NX], double (&Q)[NX]) {
                     double Lp[NX], Lt[NX], V[NX], K[NX], rdv[NX];
 #pragma unroll
-                    for (int c = 0; c < NX; c++) Lp[c] = Ph[c];
+                    for (int c = 0; c < NX; c++) Lp[c] = Ar[c];
                     rowchol<NX, NU, true>(Lp, rdv, xi, 0.0, 1e-13);
                     if (is_x) {
 #pragma unroll
@@ -909,30 +956,40 @@ __global__ __launch_bounds__(64 * W, 1) void k_sqp_rti_rowpar(KParams P, KArgs a
                         V[c] = 0.0;
                         K[c] = (xi == c) ? 1.0 : 0.0;
                     }
-                    mst_rowmul_lt<NX, NU>(V, Gn, Lp);  // V = -Gam L (L lower triangular: 28 terms)
-                    mst_rowmul_lt<NX, NU>(K, Lt, V);   // lower triangle of K = I + L' V = I - L' Gam L
+                    mst_rowmul_lt<NX, NU>(V, Cr, Lp);  // V = C L (L lower triangular: 28 terms)
+                    mst_rowmul_lt<NX, NU>(K, Lt, V);   // lower triangle of K = I + L' V = I + L' C L
                     rowchol<NX, NU, false>(K, rdv, xi, 0.5);
-                    // Y = L R^-T (row-wise forward substitution), in place of Lp; Q = Y Y' is positive semidefinite
-                    // by construction (the Woodbury form Phat - Phat C K^-1 C' Phat cancels when -Gam Phat >> 1, and a
-                    // factor of -Gam itself, a nearly singular fp32 sum, blew up: tools/seg_case_study.py)
-                    sfor<0, NX>([&](auto jc) {
+                    sfor<0, NX>([&](auto jc) {         // Y = L R^-T (row-wise forward substitution), in place of Lp
                         constexpr int j = decltype(jc)::value;
                         const double y = Lp[j] * rdv[j];
                         Lp[j] = y;
                         if constexpr (j + 1 < NX) mst_trsv<NX, NU, j>(Lp, K[j], y);
                     });
-                    double Q[NX];
 #pragma unroll
                     for (int c = 0; c < NX; c++) Q[c] = 0.0;
                     mst_rowdot<NX, NU>(Q, Lp, Lp);
-                    const double cv = mst_vdot<NX, NU>(ti, ph, Gr);  // c_i = t_i + Gam_i phat_{i+1}
-                    if (is_x) {
+                };
+                auto backward = [&]() {
+                    double Ph[NX], ph;
 #pragma unroll
-                        for (int c = 0; c < NX; c++) sQ[((size_t)i * NX + xi) * NX + c] = Q[c];
-                        sCv[i * NX + xi] = cv;
-                        sPh[i * NX + xi] = ph;
-                    }
-                    if (i >= 1) {
+                    for (int c = 0; c < NX; c++) Ph[c] = sP[((size_t)(Sg - 1) * NX + xi) * NX + c];
+                    ph = (double)seg_lds[SegL.SUM_PB + (Sg - 1) * NX + xi];
+                    for (int i = Sg - 2; i >= mj; i--) {
+                        double Gn[NX], Q[NX];
+                        ldgam(i, Gn);
+#pragma unroll
+                        for (int c = 0; c < NX; c++) Gn[c] = -Gn[c];
+                        qform(Ph, Gn, Q);  // Q_i = Phat_{i+1} (I - Gam_i Phat_{i+1})^-1
+                        double Fr[NX], Gr[NX];
+                        ldrow(i, SegL.SUM_PHI, Fr);
+                        ldgam(i, Gr);
+                        const double cv = mst_vdot<NX, NU>((double)seg_lds[SegL.SUM_T + i * NX + xi], ph, Gr);
+                        if (is_x) {
+#pragma unroll
+                            for (int c = 0; c < NX; c++) sQ[((size_t)i * NX + xi) * NX + c] = Q[c];
+                            sCv[i * NX + xi] = cv;
+                            sPh[i * NX + xi] = ph;
+                        }
                         // Phat_i = P_i + Phi_i Q_i Phi_i',  phat_i = pbar_i + Phi_i (Q_i c_i + phat_{i+1})
                         double T[NX];
 #pragma unroll
@@ -940,24 +997,123 @@ __global__ __launch_bounds__(64 * W, 1) void k_sqp_rti_rowpar(KParams P, KArgs a
                             T[c] = 0.0;
                             Ph[c] = sP[((size_t)i * NX + xi) * NX + c];
                         }
-                        mst_rowdot<NX, NU>(T, Q, Fr);  // T = Q Phi'
+                        mst_rowdot<NX, NU>(T, Q, Fr);   // T = Q Phi'
                         mst_rowmul<NX, NU>(Ph, Fr, T);  // Phat_i = P_i + Phi T
                         const double w = mst_vdot<NX, NU>(ph, cv, Q);
                         ph = mst_vdot<NX, NU>((double)seg_lds[SegL.SUM_PB + i * NX + xi], w, Fr);
                     }
+                    if (is_x) {  // Phat_m, phat_m for the join
+#pragma unroll
+                        for (int c = 0; c < NX; c++) sXa[xi * NX + c] = Ph[c];
+                        sXa[NX * NX + xi] = ph;
+                    }
+                };
+                auto dual = [&]() {
+                    double Sh[NX], sh;
+                    ldgam(0, Sh);
+#pragma unroll
+                    for (int c = 0; c < NX; c++) Sh[c] = -Sh[c];  // Shat_1 = -Gam_0
+                    sh = (double)seg_lds[SegL.SUM_T + xi];        // shat_1 = t_0
+                    for (int i = 1; i < mj; i++) {
+                        double Pr[NX], Q[NX];
+#pragma unroll
+                        for (int c = 0; c < NX; c++) Pr[c] = sP[((size_t)i * NX + xi) * NX + c];
+                        qform(Sh, Pr, Q);  // Q'_i = (I + Shat_i P_i)^-1 Shat_i
+                        const double e = mst_vdot<NX, NU>((double)seg_lds[SegL.SUM_PB + i * NX + xi], sh, Pr);
+                        const double u = mst_vdot<NX, NU>(sh, -e, Q);  // u_i = shat_i - Q'_i (pbar_i + P_i shat_i)
+                        if (is_x) {
+#pragma unroll
+                            for (int c = 0; c < NX; c++) sQ[((size_t)i * NX + xi) * NX + c] = Q[c];
+                            sCv[i * NX + xi] = u;
+                        }
+                        // Shat_{i+1} = -Gam_i + Phi_i' Q'_i Phi_i,  shat_{i+1} = t_i + Phi_i' u_i
+                        double Fc[NX], T[NX];
+                        ldcol(i, SegL.SUM_PHI, Fc);
+                        ldgam(i, Sh);
+#pragma unroll
+                        for (int c = 0; c < NX; c++) {
+                            T[c] = 0.0;
+                            Sh[c] = -Sh[c];
+                        }
+                        mst_rowdot<NX, NU>(T, Q, Fc);   // T = Q' Phi
+                        mst_rowmul<NX, NU>(Sh, Fc, T);  // Shat_{i+1} = -Gam_i + Phi' T
+                        sh = mst_vdot<NX, NU>((double)seg_lds[SegL.SUM_T + i * NX + xi], u, Fc);
+                    }
+                    if (is_x) {  // Shat_m, shat_m for the join
+#pragma unroll
+                        for (int c = 0; c < NX; c++) sXa[(NX + 1 + xi) * NX + c] = Sh[c];
+                        sXa[(2 * NX + 1) * NX + xi] = sh;
+                    }
+                };
+                if (kSeqM) {
+                    if (mrow0) backward();
+                } else if (W > 1) {
+                    if (mrow0) backward();
+                    else dual();
+                } else {
+                    backward();
+                    dual();
                 }
-                lds_fence();  // (Q_i, c_i, phat_{i+1} of every lane stored)
-                // forward: s_0 = 0; lam_{i+1} = Q_i (Phi_i' s_i + c_i) + phat_{i+1}; s_{i+1} = Phi_i' s_i + Gam_i lam_{i+1} + t_i
-                double sv = 0.0;
-                float* const sl = seg_lds + SegL.SL;
-                for (int i = 0; i <= Sg - 2; i++) {
+            }
+            __syncthreads();  // Phat_m, phat_m and Shat_m, shat_m in LDS
+            float* const sl = seg_lds + SegL.SL;
+            if (Sg > 1 && mrow0) {
+                const double* const sXa = reinterpret_cast<const double*>(seg_lds + SegL.XA);
+                const double* const sQ = reinterpret_cast<const double*>(seg_lds + SegL.QS);
+                const double* const sCv = reinterpret_cast<const double*>(seg_lds + SegL.CS);
+                const double* const sPh = reinterpret_cast<const double*>(seg_lds + SegL.PHS);
+                double* const sLt = reinterpret_cast<double*>(seg_lds + SegL.LT);
+                double Sr[NX], Q[NX];
+                if (!kSeqM) {  // Q_j = L (I + L' Shat_m L)^-1 L', L L' = Phat_m (the qform of the sweeps)
+                    double Lp[NX], Lt[NX], V[NX], K[NX], rdv[NX];
+#pragma unroll
+                    for (int c = 0; c < NX; c++) Lp[c] = sXa[xi * NX + c];
+                    rowchol<NX, NU, true>(Lp, rdv, xi, 0.0, 1e-13);
+                    if (is_x) {
+#pragma unroll
+                        for (int c = 0; c < NX; c++) sLt[xi * NX + c] = Lp[c];
+                    }
+                    lds_fence();
+#pragma unroll
+                    for (int c = 0; c < NX; c++) {
+                        Lt[c] = sLt[c * NX + xi];
+                        V[c] = 0.0;
+                        K[c] = (xi == c) ? 1.0 : 0.0;
+                    }
+#pragma unroll
+                    for (int c = 0; c < NX; c++) Sr[c] = sXa[(NX + 1 + xi) * NX + c];
+                    mst_rowmul_lt<NX, NU>(V, Sr, Lp);
+                    mst_rowmul_lt<NX, NU>(K, Lt, V);
+                    rowchol<NX, NU, false>(K, rdv, xi, 0.5);
+                    sfor<0, NX>([&](auto jc) {
+                        constexpr int j = decltype(jc)::value;
+                        const double y = Lp[j] * rdv[j];
+                        Lp[j] = y;
+                        if constexpr (j + 1 < NX) mst_trsv<NX, NU, j>(Lp, K[j], y);
+                    });
+#pragma unroll
+                    for (int c = 0; c < NX; c++) Q[c] = 0.0;
+                    mst_rowdot<NX, NU>(Q, Lp, Lp);
+                }
+                const double ph = sXa[NX * NX + xi], shm = sXa[(2 * NX + 1) * NX + xi];
+                const double v1 = mst_vdot<NX, NU>(shm, -ph, Sr);   // shat_m - Shat_m phat_m
+                const double lam_m = mst_vdot<NX, NU>(ph, v1, Q);  // lam_m
+                double sv = kSeqM ? 0.0 : mst_vdot<NX, NU>(shm, -lam_m, Sr);  // s_m = shat_m - Shat_m lam_m
+                if (is_x && !kSeqM) {
+                    sl[mj * 2 * NX + xi] = (float)sv;
+                    sl[mj * 2 * NX + NX + xi] = (float)lam_m;
+                    reinterpret_cast<double*>(seg_lds + SegL.XA)[xi] = lam_m;  // (full precision for the dual row)
+                }
+                if (W == 1) lds_fence();
+                // forward from m: lam_{i+1} = Q_i (Phi_i' s_i + c_i) + phat_{i+1}, s_{i+1} = Phi_i' s_i + Gam_i lam_{i+1} + t_i
+                for (int i = mj; i <= Sg - 2; i++) {
                     double Fc[NX], Gr[NX], Qr[NX];
 #pragma unroll
                     for (int l = 0; l < NX; l++) {
                         Fc[l] = (double)seg_lds[SegL.SUM_PHI + (i * NX + l) * NX + xi];
                         Qr[l] = sQ[((size_t)i * NX + xi) * NX + l];
+                        Gr[l] = reinterpret_cast<const double*>(seg_lds + SegL.SUM_GAM)[(i * NX + xi) * NX + l];
                     }
-                    ldrow(i, SegL.SUM_GAM, Gr);
                     const double fs = mst_vdot<NX, NU>(0.0, sv, Fc);
                     const double v = fs + sCv[i * NX + xi];
                     const double lam = mst_vdot<NX, NU>(sPh[i * NX + xi], v, Qr);
@@ -965,6 +1121,30 @@ __global__ __launch_bounds__(64 * W, 1) void k_sqp_rti_rowpar(KParams P, KArgs a
                     if (is_x) {
                         sl[(i + 1) * 2 * NX + xi] = (float)sv;
                         sl[(i + 1) * 2 * NX + NX + xi] = (float)lam;
+                    }
+                }
+            }
+            if (W > 1) __syncthreads();  // lam_m for the dual row
+            if (Sg > 1 && mrowd) {
+                // back from m: s_i = u_i - Q'_i Phi_i lam_{i+1}, lam_i = P_i s_i + pbar_i + Phi_i lam_{i+1}
+                const double* const sP = reinterpret_cast<const double*>(seg_lds + SegL.SUM_P);
+                const double* const sQ = reinterpret_cast<const double*>(seg_lds + SegL.QS);
+                const double* const sCv = reinterpret_cast<const double*>(seg_lds + SegL.CS);
+                double lv_ = reinterpret_cast<const double*>(seg_lds + SegL.XA)[xi];  // lam_m
+                for (int i = mj - 1; i >= 1; i--) {
+                    double Fr[NX], Qr[NX], Pr[NX];
+#pragma unroll
+                    for (int l = 0; l < NX; l++) {
+                        Fr[l] = (double)seg_lds[SegL.SUM_PHI + (i * NX + xi) * NX + l];
+                        Qr[l] = sQ[((size_t)i * NX + xi) * NX + l];
+                        Pr[l] = sP[((size_t)i * NX + xi) * NX + l];
+                    }
+                    const double fl = mst_vdot<NX, NU>(0.0, lv_, Fr);               // Phi_i lam_{i+1}
+                    const double si = mst_vdot<NX, NU>(sCv[i * NX + xi], -fl, Qr);  // u_i - Q'_i Phi_i lam_{i+1}
+                    lv_ = mst_vdot<NX, NU>((double)seg_lds[SegL.SUM_PB + i * NX + xi] + fl, si, Pr);
+                    if (is_x) {
+                        sl[i * 2 * NX + xi] = (float)si;
+                        sl[i * 2 * NX + NX + xi] = (float)lv_;
                     }
                 }
             }
@@ -1024,10 +1204,10 @@ __global__ __launch_bounds__(64 * W, 1) void k_sqp_rti_rowpar(KParams P, KArgs a
                         if (r == qq) dz = du_all[qq];
                     dz = is_x ? ((k >= 1) ? dxs : 0.0f) : dz;
                     dz = valid ? dz : 0.0f;
-                    *(live ? dzbase + (size_t)k * 16 : wdz) = dz;
+                    *it_wr(k, IT::DZ, live && lv) = dz;
                     if (k < N) dxs = dyn(rc, dz);
                 };
-                auto load = [&](int j, float (&v)[RS]) { ld_range<0, R::GV + NGV, RS, QM>(tbase + (size_t)kof(j) * KS, v); };
+                auto load = [&](int j, float (&v)[RS]) { ld_cfields(kof(j), v); };
                 float ra[RS], rb[RS];
                 load(0, ra);
                 for (int j = 0;; j += 2) {
@@ -1048,8 +1228,7 @@ __global__ __launch_bounds__(64 * W, 1) void k_sqp_rti_rowpar(KParams P, KArgs a
             float pv = 0.0f, piv = 0.0f, res_stat = 0.0f, cpi_max = 0.0f;
             bool fail = false;
             if (!(nanf_ > 0.0f || mu != mu)) {
-                serial(std::integral_constant<int, R::GV>{}, std::integral_constant<int, R::BF1>{},
-                       std::true_type{}, N, 0, -1, [&](int k, float (&rc)[RS]) {
+                serial(N, 0, -1, ld_bfields, [&](int k, float (&rc)[RS]) {
                     const bool vu = is_u && k < N;
                     const bool vx = is_x && k >= 1;
                     const bool valid = vu || vx;
@@ -1071,7 +1250,7 @@ __global__ __launch_bounds__(64 * W, 1) void k_sqp_rti_rowpar(KParams P, KArgs a
                     } else {
                         double Gd[NX];
     #pragma unroll
-                        for (int l = 0; l < NX; l++) Gd[l] = (l < NGV) ? (double)Gc[l] : gcol64[l];
+                        for (int l = 0; l < NX; l++) Gd[l] = (double)Gc[l];
                         double pg[NX];
     #pragma unroll
                         for (int i = 0; i < NX; i++) pg[i] = 0.0;
@@ -1079,7 +1258,7 @@ __global__ __launch_bounds__(64 * W, 1) void k_sqp_rti_rowpar(KParams P, KArgs a
                         const double dg = valid ? (double)h_stage + (double)sig : 1.0;
                         double Lr[NV];
     #pragma unroll
-                        for (int j = 0; j < NV; j++) Lr[j] = onehot[j] * dg;
+                        for (int j = 0; j < NV; j++) Lr[j] = (r == j) ? dg : 0.0;
                         double pivot;
 #ifdef NMPC_ROWPAR_MCOL
                         m_block<M>(Lr, pivot, pg, Gd, gcs);
@@ -1112,9 +1291,8 @@ __global__ __launch_bounds__(64 * W, 1) void k_sqp_rti_rowpar(KParams P, KArgs a
                         pv = is_x ? y : 0.0f;
     #pragma unroll
                         for (int j = 0; j < NV; j++) Lrow[j] = Lr[j];
-                        // LR, LM (every row stores the same values; idle slots store into the dummy record)
-                        rec_store_range<R::LR, R::LM + NU, RS, QM>(
-                            lv ? (w0 ? tbase + (size_t)k * KS : wblk + r * rec_lane<RSS, QM>()) : tdummy, rc);
+                        // LR, LM (wave 0's rows store the same values; the other waves and idle slots: pads)
+                        st_lrlm(k, rc, lv && w0);
                     }
                     piv = pi_new;
                 });
@@ -1159,8 +1337,7 @@ __global__ __launch_bounds__(64 * W, 1) void k_sqp_rti_rowpar(KParams P, KArgs a
             sigma_mu = tg_rhs;
             {
                 float dxs = 0.0f;
-                serial(std::integral_constant<int, 0>{}, std::integral_constant<int, R::GV + NGV>{}, std::false_type{},
-                       0, N, 1, [&](int k, float (&rc)[RS]) {
+                serial(0, N, 1, ld_cfields, [&](int k, float (&rc)[RS]) {
                     const bool vu = is_u && k < N;
                     const bool vx = is_x && k >= 1;
                     const bool valid = vu || vx;
@@ -1191,7 +1368,7 @@ __global__ __launch_bounds__(64 * W, 1) void k_sqp_rti_rowpar(KParams P, KArgs a
                         if (r == qq) dz = du_all[qq];
                     dz = is_x ? ((k >= 1) ? dxs : 0.0f) : dz;
                     dz = valid ? dz : 0.0f;
-                    *(w0 ? dzbase + (size_t)k * 16 : wdz) = dz;  // every slot its own entry (idle slots: 0)
+                    *it_wr(k, IT::DZ, w0 && lv) = dz;
                     if (k < N) dxs = dyn(rc, dz);
                 });
             }
@@ -1324,7 +1501,7 @@ hipError_t launch_sqp_rti_rowpar(const KParams& P, const KArgs& a, int mode, hip
 {
     if (a.B <= 0) return hipSuccess;
     const size_t lds = rowpar_lds_bytes<M>(P.N, mode, a.seg);
-    if (lds > 65536 || P.ipm != 1 || a.segs) return hipErrorInvalidValue;
+    if (lds > 163840 || P.ipm != 1 || a.segs) return hipErrorInvalidValue;  // (the host keeps every robot resident)
     // segments: N % S == 0, at most kSegMax and at most one per row of the block
     const int W = a.rowpar >= 4 ? 4 : (a.rowpar == 2 ? 2 : 1);
     if (a.seg < 0 || a.seg > kSegMax || a.seg > 4 * W || (a.seg > 0 && P.N % a.seg != 0))
@@ -1334,16 +1511,21 @@ hipError_t launch_sqp_rti_rowpar(const KParams& P, const KArgs& a, int mode, hip
 #else
     const int grid = a.B;
 #endif
+    // (a block above 64 KiB of LDS -- a long horizon on four waves, or omni4's wider stage fields -- asks for it)
+    auto go = [&](auto kern, int threads) {
+        if (lds > 65536) {
+            const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+            if (e != hipSuccess) return e;
+        }
+        hipLaunchKernelGGL(kern, dim3(grid), dim3(threads), lds, stream, P, a, mode);
+        return hipGetLastError();
+    };
     if (W == 4)  // four waves per robot (one per SIMD of its CU)
-        if (a.seg > 0) hipLaunchKernelGGL((k_sqp_rti_rowpar<M, 4, true>), dim3(grid), dim3(256), lds, stream, P, a, mode);
-        else hipLaunchKernelGGL((k_sqp_rti_rowpar<M, 4, false>), dim3(grid), dim3(256), lds, stream, P, a, mode);
-    else if (W == 2 && a.seg > 0)  // two waves per robot above 256 robots (the default there)
-        hipLaunchKernelGGL((k_sqp_rti_rowpar<M, 2, true>), dim3(grid), dim3(128), lds, stream, P, a, mode);
-    else if (a.seg > 0)
-        hipLaunchKernelGGL((k_sqp_rti_rowpar<M, 1, true>), dim3(grid), dim3(64), lds, stream, P, a, mode);
-    else
-        hipLaunchKernelGGL((k_sqp_rti_rowpar<M, 1, false>), dim3(grid), dim3(64), lds, stream, P, a, mode);
-    return hipGetLastError();
+        return a.seg > 0 ? go(k_sqp_rti_rowpar<M, 4, true>, 256) : go(k_sqp_rti_rowpar<M, 4, false>, 256);
+    if (W == 2 && a.seg > 0)  // two waves per robot above 256 robots (the default there)
+        return go(k_sqp_rti_rowpar<M, 2, true>, 128);
+    return a.seg > 0 ? go(k_sqp_rti_rowpar<M, 1, true>, 64) : go(k_sqp_rti_rowpar<M, 1, false>, 64);
 }
 
 #define INST(M)                                                                                                      \

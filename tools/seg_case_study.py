@@ -44,7 +44,7 @@ def main():
         if a.N % S:
             continue
         for m in a.masters:
-            it, u = run(lambda e, sig, gh, S=S, m=m: seg_riccati(e, sig, gh, S, True, m))
+            it, u = run(lambda e, sig, gh, S=S, m=m: seg_riccati(e, sig, gh, S, os.environ.get("SENS64") is None, m))
             print(f"S={S} {m:7s} iters", it.tolist(), f"u0 max diff {np.nanmax(np.abs(u - u_s)):.2e}")
 
 

@@ -79,11 +79,77 @@ def seg_riccati(emu, sig, ghat, S, sens32=True, master="gj"):
             P = 0.5 * (P + P.transpose(0, 2, 1))
             p = w[:, nu:] - np.einsum("bij,bj->bi", LM, lr)
             Phi = f32(Y[:, nu:] - LM @ Z, sens32)
-            Gam = f32(Gam - Z.transpose(0, 2, 1) @ Z, sens32)
+            g64 = os.environ.get("GAM64") == "1" or (os.environ.get("GAM64") == "0only" and q == 0)
+            Gam = f32(Gam - Z.transpose(0, 2, 1) @ Z, sens32 and not g64)
             t = f32(t - np.einsum("bji,bj->bi", Z, lr), sens32)
             fac[k] = (Lc, LM, lr, Z)
         segs.append(dict(P=P, p=p, Phi=Phi, Gam=Gam, t=t))
     # master (fp64)
+    if master.startswith("bidir"):
+        s, lam = master_bidir(segs, S, nx, Bn, master)
+    else:
+        s, lam = master_serial(segs, S, nx, Bn, master)
+    return seg_forward(emu, fac, s, lam, S, L)
+
+
+def qform_b(A, C):
+    """The device master's Q = A (I + C A)^-1 = Y Y', Y = L R^-T, L L' = A (pivots below 1e-13 of their diagonal entry
+    dropped), R R' = I + L' C L (sqp_rti_rowpar.hip SEG master, qform)."""
+    eye = np.broadcast_to(np.eye(A.shape[-1]), A.shape)
+    Lp = psd_chol_b(A, rel=1e-13)
+    R = psd_chol_b(eye + Lp.transpose(0, 2, 1) @ C @ Lp, drop=False, thr=0.5)
+    Y = np.linalg.solve(R, Lp.transpose(0, 2, 1)).transpose(0, 2, 1)
+    return Y @ Y.transpose(0, 2, 1)
+
+
+def master_bidir(segs, S, nx, Bn, variant="bidir"):
+    """The round-5 device master: the backward sweep from S - 1 down to m = S / 2 and the dual sweep
+    s_i = -Shat_i lam_i + shat_i from 1 up to m, joined at m, then propagated outwards."""
+    mv = lambda A, x: np.einsum("bij,bj->bi", A, x)  # noqa: E731
+    tr = lambda A: A.transpose(0, 2, 1)  # noqa: E731
+    m = S // 2
+    Ph, ph = segs[S - 1]["P"], segs[S - 1]["p"]
+    Qs, cs, phs = {}, {}, {}
+    for i in range(S - 2, m - 1, -1):
+        sg = segs[i]
+        Qm = qform_b(Ph, -sg["Gam"])
+        c = sg["t"] + mv(sg["Gam"], ph)
+        Qs[i], cs[i], phs[i] = Qm, c, ph
+        Ph = sg["P"] + sg["Phi"] @ Qm @ tr(sg["Phi"])
+        ph = sg["p"] + mv(sg["Phi"], mv(Qm, c) + ph)
+    Sh, sh = -segs[0]["Gam"], segs[0]["t"]
+    Qd, us = {}, {}
+    for i in range(1, m):
+        sg = segs[i]
+        if variant == "bidir_gj":
+            Qm = np.linalg.solve(np.eye(nx) + sg["P"] @ Sh, Sh.transpose(0, 2, 1)).transpose(0, 2, 1)
+        else:
+            Qm = qform_b(Sh, sg["P"])
+        u = sh - mv(Qm, sg["p"] + mv(sg["P"], sh))
+        Qd[i], us[i] = Qm, u
+        Sh = -sg["Gam"] + tr(sg["Phi"]) @ Qm @ sg["Phi"]
+        sh = sg["t"] + mv(tr(sg["Phi"]), u)
+    Qj = np.linalg.solve(np.eye(nx) + Sh @ Ph, Ph.transpose(0, 2, 1)).transpose(0, 2, 1) if variant == "bidir_gj" \
+        else qform_b(Ph, Sh)
+    s = [None] * S
+    lam = [None] * (S + 1)
+    s[0], lam[S] = np.zeros((Bn, nx)), np.zeros((Bn, nx))
+    lam[m] = ph + mv(Qj, sh - mv(Sh, ph))
+    s[m] = sh - mv(Sh, lam[m])
+    for i in range(m, S - 1):
+        sg = segs[i]
+        fs = mv(tr(sg["Phi"]), s[i])
+        lam[i + 1] = mv(Qs[i], fs + cs[i]) + phs[i]
+        s[i + 1] = fs + mv(sg["Gam"], lam[i + 1]) + sg["t"]
+    for i in range(m - 1, 0, -1):
+        sg = segs[i]
+        fl = mv(sg["Phi"], lam[i + 1])
+        s[i] = us[i] - mv(Qd[i], fl)
+        lam[i] = mv(sg["P"], s[i]) + sg["p"] + fl
+    return s, lam
+
+
+def master_serial(segs, S, nx, Bn, master):
     Ph, ph = segs[S - 1]["P"], segs[S - 1]["p"]
     Qs, cs, phs = [None] * S, [None] * S, [None] * S
     eye = np.broadcast_to(np.eye(nx), (Bn, nx, nx))
@@ -120,6 +186,11 @@ def seg_riccati(emu, sig, ghat, S, sens32=True, master="gj"):
         v = np.einsum("bli,bl->bi", sg["Phi"], s[i]) + cs[i]
         lam[i + 1] = np.einsum("bij,bj->bi", Qs[i], v) + phs[i]
         s.append(np.einsum("bli,bl->bi", sg["Phi"], s[i]) + np.einsum("bij,bj->bi", sg["Gam"], lam[i + 1]) + sg["t"])
+    return s, lam
+
+
+def seg_forward(emu, fac, s, lam, S, L):
+    Q, N, nx, nu, Bn = emu.Q, emu.N, emu.nx, emu.nu, emu.B
     dz = np.zeros((Bn, N + 1, nu + nx))
     for q in range(S):
         x = f32(s[q], True)  # the kernel hands s_q and lam_{q+1} to the segments in fp32
