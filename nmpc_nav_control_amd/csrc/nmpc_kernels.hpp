@@ -80,7 +80,7 @@ template <class M>
 hipError_t launch_sqp_rti_rowpar(const KParams& P, const KArgs& a, int mode, hipStream_t stream);
 template <class M>
 size_t rowpar_lds_bytes(int N, int mode, int seg);
-constexpr int kSegMax = 8;  // most horizon segments of the segmented row-parallel kernel
+constexpr int kSegMax = 16;  // most horizon segments of the segmented row-parallel kernel
 template <class M>
 hipError_t launch_fleet_sim(const KParams& P, int B, int stride, float* path, float* s, float* pose, float* vel,
                             float* steer, const float* u0, const int* status, const float* carried, float* traj,

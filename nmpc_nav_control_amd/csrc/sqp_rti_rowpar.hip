@@ -125,8 +125,21 @@ extern "C" int nmpc_debug_stamps_rowpar(unsigned long long* host)
 {
     return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_rp_stamps), sizeof(g_rp_stamps), 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -2;
 }
+// the segment master's parts, per IPM iteration: [0] start (lane 0), [1] backward sweep done (lane 0), [2] dual
+// sweep done (lane 64), [3] after the first barrier, [4] join done, [5] forward propagation done (lane 0),
+// [6] backward propagation done (lane 64), [7] after the last barrier
+__device__ unsigned long long g_rp_mstamps[256][kRpIts][8];
+#define RP_MSTAMP(slot, lane)                                                                                    \
+    do {                                                                                                         \
+        if (tid == (lane) && inst < 256 && it < kRpIts) g_rp_mstamps[inst][it][(slot)] = __builtin_amdgcn_s_memtime(); \
+    } while (0)
+extern "C" int nmpc_debug_mstamps_rowpar(unsigned long long* host)
+{
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_rp_mstamps), sizeof(g_rp_mstamps), 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -2;
+}
 #else
 #define RP_STAMP(slot) ((void)0)
+#define RP_MSTAMP(slot, lane) ((void)0)
 #endif
 
 namespace {
@@ -139,12 +152,6 @@ __device__ __forceinline__ void ld_range(const float* p, float (&v)[RS])
 
 // zeros: the warm-start multiplier source of a cold robot (the flag selects the address, not the value)
 __device__ __attribute__((aligned(16))) float g_rp_zero4[4];
-
-// LDS writes of this wave complete before its next LDS reads (the master's cross-lane exchanges within one wave)
-__device__ __forceinline__ void lds_fence()
-{
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-}
 
 // cross-row reductions of the wave (the four rows hold disjoint stages in the stage-parallel phases)
 __device__ __forceinline__ float wave_sum_rows(float v)
@@ -939,35 +946,8 @@ __global__ __launch_bounds__(64 * W, (SEG && M::NX < 10) ? 2 : 1) void k_sqp_rti
 #pragma unroll
                     for (int c = 0; c < NX; c++) v[c] = (double)seg_lds[off + (i * NX + c) * NX + xi];
                 };
-                // Q = L (I + L' C L)^-1 L' from A = L L' (row r of A in Ar, of C in Cr): the master's factorisations
                 auto qform = [&](const double (&Ar)[NX], const double (&Cr)[NX], double (&Q)[NX]) {
-                    double Lp[NX], Lt[NX], V[NX], K[NX], rdv[NX];
-#pragma unroll
-                    for (int c = 0; c < NX; c++) Lp[c] = Ar[c];
-                    rowchol<NX, NU, true>(Lp, rdv, xi, 0.0, 1e-13);
-                    if (is_x) {
-#pragma unroll
-                        for (int c = 0; c < NX; c++) sLt[xi * NX + c] = Lp[c];
-                    }
-                    lds_fence();
-#pragma unroll
-                    for (int c = 0; c < NX; c++) {
-                        Lt[c] = sLt[c * NX + xi];
-                        V[c] = 0.0;
-                        K[c] = (xi == c) ? 1.0 : 0.0;
-                    }
-                    mst_rowmul_lt<NX, NU>(V, Cr, Lp);  // V = C L (L lower triangular: 28 terms)
-                    mst_rowmul_lt<NX, NU>(K, Lt, V);   // lower triangle of K = I + L' V = I + L' C L
-                    rowchol<NX, NU, false>(K, rdv, xi, 0.5);
-                    sfor<0, NX>([&](auto jc) {         // Y = L R^-T (row-wise forward substitution), in place of Lp
-                        constexpr int j = decltype(jc)::value;
-                        const double y = Lp[j] * rdv[j];
-                        Lp[j] = y;
-                        if constexpr (j + 1 < NX) mst_trsv<NX, NU, j>(Lp, K[j], y);
-                    });
-#pragma unroll
-                    for (int c = 0; c < NX; c++) Q[c] = 0.0;
-                    mst_rowdot<NX, NU>(Q, Lp, Lp);
+                    mst_qform<NX, NU>(Ar, Cr, Q, sLt, xi, is_x);
                 };
                 auto backward = [&]() {
                     double Ph[NX], ph;
@@ -1045,6 +1025,7 @@ __global__ __launch_bounds__(64 * W, (SEG && M::NX < 10) ? 2 : 1) void k_sqp_rti
                         sXa[(2 * NX + 1) * NX + xi] = sh;
                     }
                 };
+                RP_MSTAMP(0, 0);
                 if (kSeqM) {
                     if (mrow0) backward();
                 } else if (W > 1) {
@@ -1054,8 +1035,11 @@ __global__ __launch_bounds__(64 * W, (SEG && M::NX < 10) ? 2 : 1) void k_sqp_rti
                     backward();
                     dual();
                 }
+                RP_MSTAMP(1, 0);
+                RP_MSTAMP(2, 64);
             }
             __syncthreads();  // Phat_m, phat_m and Shat_m, shat_m in LDS
+            RP_MSTAMP(3, 0);
             float* const sl = seg_lds + SegL.SL;
             if (Sg > 1 && mrow0) {
                 const double* const sXa = reinterpret_cast<const double*>(seg_lds + SegL.XA);
@@ -1064,36 +1048,13 @@ __global__ __launch_bounds__(64 * W, (SEG && M::NX < 10) ? 2 : 1) void k_sqp_rti
                 const double* const sPh = reinterpret_cast<const double*>(seg_lds + SegL.PHS);
                 double* const sLt = reinterpret_cast<double*>(seg_lds + SegL.LT);
                 double Sr[NX], Q[NX];
-                if (!kSeqM) {  // Q_j = L (I + L' Shat_m L)^-1 L', L L' = Phat_m (the qform of the sweeps)
-                    double Lp[NX], Lt[NX], V[NX], K[NX], rdv[NX];
 #pragma unroll
-                    for (int c = 0; c < NX; c++) Lp[c] = sXa[xi * NX + c];
-                    rowchol<NX, NU, true>(Lp, rdv, xi, 0.0, 1e-13);
-                    if (is_x) {
+                for (int c = 0; c < NX; c++) Sr[c] = sXa[(NX + 1 + xi) * NX + c];
+                if (!kSeqM) {  // Q_j = L (I + L' Shat_m L)^-1 L', L L' = Phat_m
+                    double Pm[NX];
 #pragma unroll
-                        for (int c = 0; c < NX; c++) sLt[xi * NX + c] = Lp[c];
-                    }
-                    lds_fence();
-#pragma unroll
-                    for (int c = 0; c < NX; c++) {
-                        Lt[c] = sLt[c * NX + xi];
-                        V[c] = 0.0;
-                        K[c] = (xi == c) ? 1.0 : 0.0;
-                    }
-#pragma unroll
-                    for (int c = 0; c < NX; c++) Sr[c] = sXa[(NX + 1 + xi) * NX + c];
-                    mst_rowmul_lt<NX, NU>(V, Sr, Lp);
-                    mst_rowmul_lt<NX, NU>(K, Lt, V);
-                    rowchol<NX, NU, false>(K, rdv, xi, 0.5);
-                    sfor<0, NX>([&](auto jc) {
-                        constexpr int j = decltype(jc)::value;
-                        const double y = Lp[j] * rdv[j];
-                        Lp[j] = y;
-                        if constexpr (j + 1 < NX) mst_trsv<NX, NU, j>(Lp, K[j], y);
-                    });
-#pragma unroll
-                    for (int c = 0; c < NX; c++) Q[c] = 0.0;
-                    mst_rowdot<NX, NU>(Q, Lp, Lp);
+                    for (int c = 0; c < NX; c++) Pm[c] = sXa[xi * NX + c];
+                    mst_qform<NX, NU>(Pm, Sr, Q, sLt, xi, is_x);
                 }
                 const double ph = sXa[NX * NX + xi], shm = sXa[(2 * NX + 1) * NX + xi];
                 const double v1 = mst_vdot<NX, NU>(shm, -ph, Sr);   // shat_m - Shat_m phat_m
@@ -1104,6 +1065,7 @@ __global__ __launch_bounds__(64 * W, (SEG && M::NX < 10) ? 2 : 1) void k_sqp_rti
                     sl[mj * 2 * NX + NX + xi] = (float)lam_m;
                     reinterpret_cast<double*>(seg_lds + SegL.XA)[xi] = lam_m;  // (full precision for the dual row)
                 }
+                RP_MSTAMP(4, 0);
                 if (W == 1) lds_fence();
                 // forward from m: lam_{i+1} = Q_i (Phi_i' s_i + c_i) + phat_{i+1}, s_{i+1} = Phi_i' s_i + Gam_i lam_{i+1} + t_i
                 for (int i = mj; i <= Sg - 2; i++) {
@@ -1123,6 +1085,7 @@ __global__ __launch_bounds__(64 * W, (SEG && M::NX < 10) ? 2 : 1) void k_sqp_rti
                         sl[(i + 1) * 2 * NX + NX + xi] = (float)lam;
                     }
                 }
+                RP_MSTAMP(5, 0);
             }
             if (W > 1) __syncthreads();  // lam_m for the dual row
             if (Sg > 1 && mrowd) {
@@ -1147,8 +1110,10 @@ __global__ __launch_bounds__(64 * W, (SEG && M::NX < 10) ? 2 : 1) void k_sqp_rti
                         sl[i * 2 * NX + NX + xi] = (float)lv_;
                     }
                 }
+                RP_MSTAMP(6, 64);
             }
             __syncthreads();  // the boundary states and costates
+            RP_MSTAMP(7, 0);
             RP_STAMP(5 + 4 * it);
 
             // ---- phase C (segments in parallel, 0 -> N): row q starts at x_{qL} = s_q and takes the stored

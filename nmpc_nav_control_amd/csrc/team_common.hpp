@@ -273,7 +273,7 @@ __device__ __forceinline__ double mst_vdot(double acc, double x, const double (&
 // positive semidefinite matrix; the relative test keeps rounding-level pivots of a nearly singular matrix from
 // scaling their column by 1 / sqrt(noise)) or poisons the factor with NaN (!DROP: a breakdown the IPM's NaN test
 // reports); a NaN pivot always propagates.
-template <int NX, int NU, bool DROP>
+template <int NX, int NU, bool DROP, bool RAW_RSQ = false>
 __device__ __forceinline__ void rowchol(double (&lr)[NX], double (&rdv)[NX], int xi, double thr, double rel = 0.0)
 {
     double d0 = 0.0;
@@ -284,12 +284,57 @@ __device__ __forceinline__ void rowchol(double (&lr)[NX], double (&rdv)[NX], int
     sfor<0, NX>([&](auto jc) {
         constexpr int j = decltype(jc)::value;
         const double tj = fmax(thr, bc64<NU + j>(d0));
-        const double rd = (piv > tj) ? drsq(piv) : ((DROP && piv == piv) ? 0.0 : __builtin_nan(""));
+        const double rq = RAW_RSQ ? __builtin_amdgcn_rsq(piv) : drsq(piv);  // RAW_RSQ: A/B timing only
+        const double rd = (piv > tj) ? rq : ((DROP && piv == piv) ? 0.0 : __builtin_nan(""));
         rdv[j] = rd;
         const double lj = (xi >= j) ? lr[j] * rd : 0.0;
         lr[j] = lj;
         if constexpr (j + 1 < NX) mst_chol<NX, NU, j>(lr, lj, piv);
     });
+}
+
+// LDS writes of this wave complete before its next LDS reads (the master's cross-lane exchanges within one wave)
+__device__ __forceinline__ void lds_fence()
+{
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+}
+
+// The segment master's step matrix Q = A (I + C A)^-1 = L (I + L' C L)^-1 L' from A = L L' (A, C >= 0; row xi of A
+// in Ar, of C in Cr, on lane NU + xi of a 16-lane row), formed as Y Y', Y = L R^-T, R R' = K = I + L' C L: pivots of
+// A below 1e-13 of their diagonal entry dropped, K >= I factored without pivoting. sLt: NX x NX doubles of LDS
+// scratch private to the row (L' crosses lanes through it). Positive semidefinite by construction; the Woodbury
+// form and a factor of C both failed numerically (tools/seg_case_study.py).
+template <int NX, int NU>
+__device__ __forceinline__ void mst_qform(const double (&Ar)[NX], const double (&Cr)[NX], double (&Q)[NX],
+                                          double* sLt, int xi, bool is_x)
+{
+    double Lp[NX], Lt[NX], V[NX], K[NX], rdv[NX];
+#pragma unroll
+    for (int c = 0; c < NX; c++) Lp[c] = Ar[c];
+    rowchol<NX, NU, true>(Lp, rdv, xi, 0.0, 1e-13);
+    if (is_x) {
+#pragma unroll
+        for (int c = 0; c < NX; c++) sLt[xi * NX + c] = Lp[c];
+    }
+    lds_fence();
+#pragma unroll
+    for (int c = 0; c < NX; c++) {
+        Lt[c] = sLt[c * NX + xi];
+        V[c] = 0.0;
+        K[c] = (xi == c) ? 1.0 : 0.0;
+    }
+    mst_rowmul_lt<NX, NU>(V, Cr, Lp);  // V = C L (L lower triangular: 28 terms)
+    mst_rowmul_lt<NX, NU>(K, Lt, V);   // lower triangle of K = I + L' V
+    rowchol<NX, NU, false>(K, rdv, xi, 0.5);
+    sfor<0, NX>([&](auto jc) {         // Y = L R^-T (row-wise forward substitution), in place of Lp
+        constexpr int j = decltype(jc)::value;
+        const double y = Lp[j] * rdv[j];
+        Lp[j] = y;
+        if constexpr (j + 1 < NX) mst_trsv<NX, NU, j>(Lp, K[j], y);
+    });
+#pragma unroll
+    for (int c = 0; c < NX; c++) Q[c] = 0.0;
+    mst_rowdot<NX, NU>(Q, Lp, Lp);
 }
 
 template <class M>

@@ -57,3 +57,17 @@ print("P0a cycles", (st[:, 1] - st[:, 0]).tolist(), "P0b", (st[:, 2] - st[:, 1])
 for k, v in ph.items():
     v = np.array(v)
     print(k, "mean %.0f p50 %.0f max %.0f n %d per stage %.0f" % (v.mean(), np.median(v), v.max(), len(v), v.mean() / (N + 1)))
+
+# the segment master's parts (diag builds with g_rp_mstamps): per iteration deltas
+if seg and hasattr(L, "nmpc_debug_mstamps_rowpar"):
+    mb = (ctypes.c_ulonglong * (256 * 64 * 8))()
+    L.nmpc_debug_mstamps_rowpar.argtypes = [ctypes.c_void_p]
+    if L.nmpc_debug_mstamps_rowpar(mb) == 0:
+        ms = np.frombuffer(mb, dtype=np.uint64).reshape(256, 64, 8).astype(np.int64)[:min(B, 256)]
+        parts = {"backward sweep (w0)": (0, 1), "dual sweep (w1)": (0, 2), "barrier 1": (1, 3), "join": (3, 4),
+                 "forward prop (w0)": (4, 5), "backward prop (w1)": (4, 6), "to last barrier": (5, 7), "total": (0, 7)}
+        for name, (a, b) in parts.items():
+            v = np.array([ms[r, i, b] - ms[r, i, a] for r in range(ms.shape[0]) for i in range(int(it[r]))
+                          if ms[r, i, a] > 0 and ms[r, i, b] > 0])
+            if len(v):
+                print("  master %-20s mean %7.0f p50 %7.0f n %d" % (name, v.mean(), np.median(v), len(v)))

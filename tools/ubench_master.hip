@@ -1,7 +1,8 @@
 // ubench_master.hip -- unit check of the segmented-Riccati master's fused-DPP blocks (team_asm_gen.hpp mst_*,
 // team_common.hpp rowchol) on one 16-lane row against a host fp64 reference: for a positive semidefinite G (= -Gam,
 // full rank, rank 3 and zero), Q = Phat (I + G Phat)^-1 as Y Y', Y = L R^-T (L L' = Phat, R R' = I + L' G L),
-// Phat' = Phat + F Q F', the vector blocks c = t + (-G) phat and w = phat + Q c. Prints one JSON line per case.
+// Phat' = Phat + F Q F', the vector blocks c = t + (-G) phat and w = phat + Q c. Prints one JSON line per case, and
+// (first case) the cycles per step of chained master steps and of their parts (k_master_time).
 // build: make -C nmpc_nav_control_amd/csrc ubench_master   run: build/ubench_master
 #include <hip/hip_runtime.h>
 
@@ -74,6 +75,149 @@ __global__ void k_master(const double* Ph, const double* G, const double* F, con
     }
 }
 
+// Timing: a chain of `steps` dependent master steps on row 0 of one wave, the segment data in LDS as in the kernel.
+// VAR 0: the kernel's backward step (qform + Phat_i = P + Phi Q Phi' + the vector terms); 1: one rowchol of Phat per
+// step; 2: qform only (Phat <- P + Q); 3: the two products of the Phat update only. cyc[0, 1]: s_memtime and
+// s_memrealtime (100 MHz) deltas of the chain.
+template <int VAR>
+__global__ void k_master_time(const double* Ph0, const double* G, const double* F, int steps,
+                              unsigned long long* cyc, double* sink)
+{
+    __shared__ double sP[NX * NX], sG[NX * NX], sL[NX * NX];
+    __shared__ float sF[NX * NX], sV[2 * NX];
+    for (int i = threadIdx.x; i < NX * NX; i += blockDim.x) {
+        sP[i] = Ph0[i];
+        sG[i] = -G[i];  // Gam
+        sF[i] = (float)F[i];
+    }
+    for (int i = threadIdx.x; i < 2 * NX; i += blockDim.x) sV[i] = 0.01f * (float)i;
+    __syncthreads();
+    const int r = threadIdx.x & 15;
+    const bool is_x = r >= NU && r < NU + NX;
+    const int xi = is_x ? r - NU : 0;
+    double Ph[NX], ph = 0.0;
+#pragma unroll
+    for (int c = 0; c < NX; c++) Ph[c] = sP[xi * NX + c];
+    const unsigned long long t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+#pragma unroll 1
+    for (int k = 0; k < steps; k++) {
+        if constexpr (VAR == 0) {
+            double Gn[NX], Q[NX];
+#pragma unroll
+            for (int c = 0; c < NX; c++) Gn[c] = -sG[xi * NX + c];
+            mst_qform<NX, NU>(Ph, Gn, Q, sL, xi, is_x);
+            double Fr[NX], Gr[NX], T[NX];
+#pragma unroll
+            for (int c = 0; c < NX; c++) {
+                Fr[c] = (double)sF[xi * NX + c];
+                Gr[c] = sG[xi * NX + c];
+                T[c] = 0.0;
+                Ph[c] = sP[xi * NX + c];
+            }
+            const double cv = mst_vdot<NX, NU>((double)sV[xi], ph, Gr);
+            mst_rowdot<NX, NU>(T, Q, Fr);
+            mst_rowmul<NX, NU>(Ph, Fr, T);
+            const double w = mst_vdot<NX, NU>(ph, cv, Q);
+            ph = mst_vdot<NX, NU>((double)sV[NX + xi], w, Fr);
+        } else if constexpr (VAR == 1) {
+            double Lp[NX], rdv[NX];
+#pragma unroll
+            for (int c = 0; c < NX; c++) Lp[c] = Ph[c];
+            rowchol<NX, NU, true>(Lp, rdv, xi, 0.0, 1e-13);
+#pragma unroll
+            for (int c = 0; c < NX; c++) Ph[c] = sP[xi * NX + c] + 1e-3 * Lp[c];
+        } else if constexpr (VAR == 4) {
+            double Lp[NX], rdv[NX];
+#pragma unroll
+            for (int c = 0; c < NX; c++) Lp[c] = Ph[c];
+            rowchol<NX, NU, true, true>(Lp, rdv, xi, 0.0, 1e-13);
+#pragma unroll
+            for (int c = 0; c < NX; c++) Ph[c] = sP[xi * NX + c] + 1e-3 * Lp[c];
+        } else if constexpr (VAR == 5) {  // the LDS transpose round trip of qform alone
+#pragma unroll
+            for (int c = 0; c < NX; c++)
+                if (is_x) sL[xi * NX + c] = Ph[c];
+            lds_fence();
+#pragma unroll
+            for (int c = 0; c < NX; c++) Ph[c] = sL[c * NX + xi] * 0.999 + sP[xi * NX + c];
+        } else if constexpr (VAR == 2) {
+            double Gn[NX], Q[NX];
+#pragma unroll
+            for (int c = 0; c < NX; c++) Gn[c] = -sG[xi * NX + c];
+            mst_qform<NX, NU>(Ph, Gn, Q, sL, xi, is_x);
+#pragma unroll
+            for (int c = 0; c < NX; c++) Ph[c] = sP[xi * NX + c] + Q[c];
+        } else {
+            double Fr[NX], T[NX], Q[NX];
+#pragma unroll
+            for (int c = 0; c < NX; c++) {
+                Fr[c] = (double)sF[xi * NX + c];
+                T[c] = 0.0;
+                Q[c] = 1e-3 * Ph[c];
+                Ph[c] = sP[xi * NX + c];
+            }
+            mst_rowdot<NX, NU>(T, Q, Fr);
+            mst_rowmul<NX, NU>(Ph, Fr, T);
+        }
+    }
+    const unsigned long long t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+    if (threadIdx.x == 0) {
+        cyc[0] = t1 - t0;
+        cyc[1] = r1 - r0;
+    }
+    double acc = ph;
+#pragma unroll
+    for (int c = 0; c < NX; c++) acc += Ph[c];
+    sink[threadIdx.x] = acc;
+}
+
+// accuracy of the hardware fp64 reciprocal square root (v_rsq_f64) against 1 / sqrt in fp64
+__global__ void k_rsq_acc(const double* x, double* out, int n)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = __builtin_amdgcn_rsq(x[i]);
+}
+
+static void rsq_accuracy()
+{
+    const int n = 1 << 16;
+    std::vector<double> x(n), y(n);
+    std::mt19937_64 rng(11);
+    std::uniform_real_distribution<double> ud(-30.0, 30.0);
+    for (auto& v : x) v = std::pow(10.0, ud(rng) / 3.0);
+    double *dx, *dy;
+    (void)hipMalloc(&dx, n * 8);
+    (void)hipMalloc(&dy, n * 8);
+    (void)hipMemcpy(dx, x.data(), n * 8, hipMemcpyHostToDevice);
+    hipLaunchKernelGGL(k_rsq_acc, dim3(n / 256), dim3(256), 0, nullptr, dx, dy, n);
+    (void)hipMemcpy(y.data(), dy, n * 8, hipMemcpyDeviceToHost);
+    double worst = 0.0;
+    for (int i = 0; i < n; i++) worst = std::fmax(worst, std::fabs(y[i] * std::sqrt(x[i]) - 1.0));
+    std::printf("{\"rsq_f64_max_rel_err\": %.3e, \"samples\": %d}\n", worst, n);
+    (void)hipFree(dx);
+    (void)hipFree(dy);
+}
+
+template <int VAR>
+static void time_variant(const double* dPh, const double* dG, const double* dF, const char* name)
+{
+    unsigned long long* dc;
+    double* ds;
+    (void)hipMalloc(&dc, 2 * sizeof(unsigned long long));
+    (void)hipMalloc(&ds, 64 * sizeof(double));
+    const int steps = 256;
+    unsigned long long c[2] = {0, 0};
+    for (int rep = 0; rep < 3; rep++) {  // the last of three launches (the first ones warm the instruction cache)
+        hipLaunchKernelGGL(k_master_time<VAR>, dim3(1), dim3(64), 0, nullptr, dPh, dG, dF, steps, dc, ds);
+        (void)hipMemcpy(c, dc, sizeof(c), hipMemcpyDeviceToHost);
+    }
+    const double ghz = c[1] ? (double)c[0] / ((double)c[1] * 10.0) : 0.0;
+    std::printf("{\"timing\": \"%s\", \"steps\": %d, \"cycles_per_step\": %.1f, \"ns_per_step\": %.1f, "
+                "\"clock_ghz\": %.3f}\n", name, steps, (double)c[0] / steps, (double)c[1] * 10.0 / steps, ghz);
+    (void)hipFree(dc);
+    (void)hipFree(ds);
+}
+
 // host reference: A^-1 B by Gauss-Jordan with partial pivoting (n x n, row-major)
 static void solve(std::vector<double> A, std::vector<double>& B, int n)
 {
@@ -140,6 +284,15 @@ int main()
         (void)hipMemcpy(dvp, vp.data(), n * 8, hipMemcpyHostToDevice);
         hipLaunchKernelGGL(k_master, dim3(1), dim3(64), 0, nullptr, dPh, dG, dF, dvt, dvp, dout + nn, dout + 2 * nn,
                            dout + 3 * nn, dout + 3 * nn + n);
+        if (cs == 0) {
+            time_variant<0>(dPh, dG, dF, "backward_step");
+            time_variant<1>(dPh, dG, dF, "rowchol");
+            time_variant<2>(dPh, dG, dF, "qform");
+            time_variant<3>(dPh, dG, dF, "phat_update_products");
+            time_variant<4>(dPh, dG, dF, "rowchol_raw_rsq");
+            time_variant<5>(dPh, dG, dF, "lds_transpose");
+            rsq_accuracy();
+        }
         std::vector<double> out(3 * nn + 2 * n);
         if (hipMemcpy(out.data(), dout, out.size() * 8, hipMemcpyDeviceToHost) != hipSuccess) {
             std::fprintf(stderr, "hip error\n");
