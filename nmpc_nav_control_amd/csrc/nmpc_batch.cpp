@@ -165,6 +165,13 @@ inline int seg_count(int N, int rows)
 
 // LDS a row-parallel launch of B robots may give each block: the CU's 160 KiB shared by the ceil(B / 256) robots
 // each CU holds (one block per robot on 256 CUs), so that every robot of the launch is resident at once
+// waves per robot of a row-parallel launch of B robots (eight waves per robot up to 64 robots measured no faster:
+// the one-robot phases are chains, not rounds; profiles/r05/ab/w8_rowchol2.txt)
+inline int rowpar_waves(const nmpc_batch* b, int B)
+{
+    return B <= 256 ? 4 : b->rowpar_w;
+}
+
 inline size_t rowpar_lds_cap(int B)
 {
     const int per_cu = (B + 255) / 256;
@@ -232,7 +239,7 @@ hipError_t schedule(nmpc_batch* b, KArgs& a, int mode, hipStream_t s)
     case NMPC_MODEL_OMNI4AMR: a.rowpar = rowpar_ok<Omni4>(b, a, mode); break;
     default: a.rowpar = rowpar_ok<Tric3>(b, a, mode); break;
     }
-    if (a.rowpar) a.rowpar = (a.B <= 256) ? 4 : b->rowpar_w;  // waves per robot
+    if (a.rowpar) a.rowpar = rowpar_waves(b, a.B);  // waves per robot
     // the row-parallel kernel keeps the wide single-direction records; the team kernel the handle's layout
     a.rec_split = (!a.rowpar && b->kp.ipm == NMPC_IPM_SINGLE) ? b->rec_split : 0;
     a.warm_tag = warm_tag_of(b, a);
@@ -790,7 +797,7 @@ int nmpc_batch_plan_ex(const nmpc_batch* b, int B, int mode, nmpc_launch_plan* p
     a.rowpar = rp ? 1 : 0;
     a.rec_split = (!rp && b->kp.ipm == NMPC_IPM_SINGLE) ? b->rec_split : 0;
     plan->kernel = rp ? 1 : 0;
-    plan->waves_per_robot = rp ? (B <= 256 ? 4 : b->rowpar_w) : 0;
+    plan->waves_per_robot = rp ? rowpar_waves(b, B) : 0;
     plan->segments = rp ? a.seg : 0;
     plan->record_layout = a.rec_split ? NMPC_REC_SPLIT : NMPC_REC_WIDE;
     plan->warm_tag = warm_tag_of(b, a);

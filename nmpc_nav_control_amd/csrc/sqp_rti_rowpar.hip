@@ -926,7 +926,11 @@ __global__ __launch_bounds__(64 * W, (SEG && M::NX < 10) ? 2 : 1) void k_sqp_rti
 #endif
             const int mj = kSeqM ? 0 : Sg / 2;        // the join boundary (1 <= m <= S - 1)
             const bool mrow0 = tid < 16;              // backward sweep, join, forward propagation
-            const bool mrowd = (W > 1) ? (tid >= 64 && tid < 80) : (tid < 16);  // the dual sweep
+#ifndef NMPC_DUAL_WAVE
+#define NMPC_DUAL_WAVE 1  // (A/B: the wave of the dual sweep when the block has more than one)
+#endif
+            constexpr int kDW = (W > NMPC_DUAL_WAVE) ? NMPC_DUAL_WAVE : 1;
+            const bool mrowd = (W > 1) ? (tid >= 64 * kDW && tid < 64 * kDW + 16) : (tid < 16);  // the dual sweep
             if (Sg > 1 && (mrow0 || mrowd)) {
                 const double* const sP = reinterpret_cast<const double*>(seg_lds + SegL.SUM_P);
                 double* const sQ = reinterpret_cast<double*>(seg_lds + SegL.QS);
@@ -1036,7 +1040,7 @@ __global__ __launch_bounds__(64 * W, (SEG && M::NX < 10) ? 2 : 1) void k_sqp_rti
                     dual();
                 }
                 RP_MSTAMP(1, 0);
-                RP_MSTAMP(2, 64);
+                RP_MSTAMP(2, 64 * kDW);
             }
             __syncthreads();  // Phat_m, phat_m and Shat_m, shat_m in LDS
             RP_MSTAMP(3, 0);
@@ -1110,7 +1114,7 @@ __global__ __launch_bounds__(64 * W, (SEG && M::NX < 10) ? 2 : 1) void k_sqp_rti
                         sl[i * 2 * NX + NX + xi] = (float)lv_;
                     }
                 }
-                RP_MSTAMP(6, 64);
+                RP_MSTAMP(6, 64 * kDW);
             }
             __syncthreads();  // the boundary states and costates
             RP_MSTAMP(7, 0);

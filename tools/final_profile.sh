@@ -18,11 +18,12 @@ declare -A KEY=([metric]=diff_N40_B4096 [diff1024]=diff_N40_B1024 [omni4]=omni4_
 timeout -k 10 420 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $OUT/${TAG}_tests.log 2>&1; ok $? tests
 tail -1 $OUT/${TAG}_tests.log
 timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/${TAG}_smoke.log 2>&1; ok $? smoke
+timeout -k 10 60 build/ubench_valu > $OUT/${TAG}_ubench.json 2> $OUT/${TAG}_ubench.err; ok $? ubench
+mkdir -p profiles/$RND && cp $OUT/${TAG}_ubench.json profiles/$RND/ubench_valu.json  # the measured basis bench.py reads
 for c in $CONFIGS; do
   bash tools/pmc.sh ${TAG}_$c --config $c > $OUT/${TAG}_pmc_$c.log 2>&1; ok $? pmc_$c
   python3 tools/pmc_summary.py $OUT/${TAG}_$c ${KEY[$c]} --round $RND --last 10 --write > /dev/null; ok $? pmc_summary_$c
 done
-timeout -k 10 60 build/ubench_valu > $OUT/${TAG}_ubench.json 2> $OUT/${TAG}_ubench.err; ok $? ubench
 timeout -k 10 60 build/ubench_master > $OUT/${TAG}_master.json; ok $? ubench_master
 bash tools/mall_calibration.sh $TAG > $OUT/${TAG}_mall.log 2>&1; ok $? mall
 for mode in warm cold; do

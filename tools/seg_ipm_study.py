@@ -87,6 +87,8 @@ def seg_riccati(emu, sig, ghat, S, sens32=True, master="gj"):
     # master (fp64)
     if master.startswith("bidir"):
         s, lam = master_bidir(segs, S, nx, Bn, master)
+    elif master == "scan":
+        s, lam = master_scan(segs, S, nx, Bn)
     else:
         s, lam = master_serial(segs, S, nx, Bn, master)
     return seg_forward(emu, fac, s, lam, S, L)
@@ -146,6 +148,50 @@ def master_bidir(segs, S, nx, Bn, variant="bidir"):
         fl = mv(sg["Phi"], lam[i + 1])
         s[i] = us[i] - mv(Qd[i], fl)
         lam[i] = mv(sg["P"], s[i]) + sg["p"] + fl
+    return s, lam
+
+
+def master_scan(segs, S, nx, Bn):
+    """Tree (parallel-scan) form of the master: adjacent segments combine pairwise, level by level, into one element
+    (P, p, Phi, C = -Gam, t) of the same two-point form; the boundary values then expand back down the tree. Each
+    combine takes Qb = P_b (I + C_a P_b)^-1 and Qa = C_a (I + P_b C_a)^-1 (both qform_b, independent), so a level
+    costs one master step whatever its width: depth log2 S against the bidirectional master's S / 2."""
+    mv = lambda A, x: np.einsum("bij,bj->bi", A, x)  # noqa: E731
+    tr = lambda A: A.transpose(0, 2, 1)  # noqa: E731
+    eye = np.broadcast_to(np.eye(nx), (Bn, nx, nx))
+    level = [dict(P=g["P"], p=g["p"], Phi=g["Phi"], C=-g["Gam"], t=g["t"], lo=i, hi=i + 1) for i, g in enumerate(segs)]
+    levels = [level]
+    while len(level) > 1:
+        nxt = []
+        for k in range(0, len(level) - 1, 2):
+            a, b = level[k], level[k + 1]
+            Qb = qform_b(b["P"], a["C"])
+            Qa = qform_b(a["C"], b["P"])
+            E = eye - b["P"] @ Qa  # (I + P_b C_a)^-1
+            v = a["t"] - mv(a["C"], b["p"])
+            nxt.append(dict(P=a["P"] + a["Phi"] @ Qb @ tr(a["Phi"]), p=a["p"] + mv(a["Phi"], mv(Qb, v) + b["p"]),
+                            Phi=a["Phi"] @ E @ b["Phi"], C=b["C"] + tr(b["Phi"]) @ Qa @ b["Phi"],
+                            t=b["t"] + mv(tr(b["Phi"]) @ tr(E), v), lo=a["lo"], hi=b["hi"], a=a, b=b, Qa=Qa, E=E))
+        if len(level) % 2:
+            nxt.append(level[-1])
+        levels.append(nxt)
+        level = nxt
+    s = [None] * S
+    lam = [None] * (S + 1)
+    s[0], lam[S] = np.zeros((Bn, nx)), np.zeros((Bn, nx))
+
+    def expand(nd):
+        if "a" not in nd:
+            return
+        a, b = nd["a"], nd["b"]
+        si, lo = s[a["lo"]], lam[b["hi"]]
+        v = a["t"] - mv(a["C"], b["p"])
+        sm = mv(tr(nd["E"]), mv(tr(a["Phi"]), si) + v) - mv(nd["Qa"], mv(b["Phi"], lo))
+        s[b["lo"]] = sm
+        lam[b["lo"]] = mv(b["P"], sm) + b["p"] + mv(b["Phi"], lo)
+        expand(a)
+        expand(b)
+    expand(levels[-1][0])
     return s, lam
 
 
