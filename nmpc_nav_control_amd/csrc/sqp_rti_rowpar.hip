@@ -193,7 +193,7 @@ __global__ __launch_bounds__(64 * W, (SEG && M::NX < 10) ? 2 : 1) void k_sqp_rti
 #endif
     if (inst >= a.B) return;
     const int tid = (int)threadIdx.x;
-    const int wave = tid >> 6;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // (an SGPR: branches on it are wave-uniform)
     const int q = tid >> 4;  // row of the block: stage-parallel phases take stages q, q + ROWS, ...
     const int r = tid & 15;  // slot: variable r of the stage (as a team lane)
     const bool wr = tid < 16;  // the lanes that store the serial phases' results
@@ -1031,10 +1031,13 @@ __global__ __launch_bounds__(64 * W, (SEG && M::NX < 10) ? 2 : 1) void k_sqp_rti
                 };
                 RP_MSTAMP(0, 0);
                 if (kSeqM) {
-                    if (mrow0) backward();
+                    if (wave == 0 && mrow0) backward();
                 } else if (W > 1) {
-                    if (mrow0) backward();
-                    else dual();
+                    if (wave == 0) {  // (wave-uniform branches: neither wave issues the other's sweep under a zero mask)
+                        if (mrow0) backward();
+                    } else if (wave == kDW) {
+                        if (mrowd) dual();
+                    }
                 } else {
                     backward();
                     dual();
@@ -1045,7 +1048,7 @@ __global__ __launch_bounds__(64 * W, (SEG && M::NX < 10) ? 2 : 1) void k_sqp_rti
             __syncthreads();  // Phat_m, phat_m and Shat_m, shat_m in LDS
             RP_MSTAMP(3, 0);
             float* const sl = seg_lds + SegL.SL;
-            if (Sg > 1 && mrow0) {
+            if (Sg > 1 && wave == 0 && mrow0) {
                 const double* const sXa = reinterpret_cast<const double*>(seg_lds + SegL.XA);
                 const double* const sQ = reinterpret_cast<const double*>(seg_lds + SegL.QS);
                 const double* const sCv = reinterpret_cast<const double*>(seg_lds + SegL.CS);
@@ -1092,7 +1095,7 @@ __global__ __launch_bounds__(64 * W, (SEG && M::NX < 10) ? 2 : 1) void k_sqp_rti
                 RP_MSTAMP(5, 0);
             }
             if (W > 1) __syncthreads();  // lam_m for the dual row
-            if (Sg > 1 && mrowd) {
+            if (Sg > 1 && wave == (W > 1 ? kDW : 0) && mrowd) {
                 // back from m: s_i = u_i - Q'_i Phi_i lam_{i+1}, lam_i = P_i s_i + pbar_i + Phi_i lam_{i+1}
                 const double* const sP = reinterpret_cast<const double*>(seg_lds + SegL.SUM_P);
                 const double* const sQ = reinterpret_cast<const double*>(seg_lds + SegL.QS);

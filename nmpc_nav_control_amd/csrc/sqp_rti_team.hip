@@ -576,10 +576,13 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a)
     double gcol64[NX];
 #pragma unroll
     for (int i = 0; i < NX; i++) gcol64[i] = (double)gcol[i];
-#ifndef NMPC_MROW
-    GConst<M> gcs;  // the constant rows of [B A] as uniform operands of the M block (m_block)
-    gconst_load<M>(gcs, gcol);
+#ifdef NMPC_MROW
+    constexpr bool kMcol = false;  // A/B: the row form for every model
+#else
+    constexpr bool kMcol = M::kMcolForm;  // per model (nmpc_models.hpp)
 #endif
+    GConst<M> gcs;  // the constant rows of [B A] as uniform operands of the column-form M block (m_block)
+    if constexpr (kMcol) gconst_load<M>(gcs, gcol);
 
     STAMP(1);
     // infeasibility threshold of this robot: qp_infeas_lambda scaled by its largest weight (terminal hack included)
@@ -783,20 +786,22 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a)
 #pragma unroll
                 for (int j = 0; j < NV; j++) Lr[j] = onehot[j] * dg;
                 double pivot;  // = M[0][0]
-#ifndef NMPC_MROW
-                double m11, m10;
-                m_block<M>(Lr, pivot, m11, m10, pg, Gd, gcs);  // column form: uniform constant rows + 3 broadcast rows
-                STAMPF(4);
+                bool seq_pivots = true;
+                if constexpr (kMcol) {
+                    double m11, m10;
+                    m_block<M>(Lr, pivot, m11, m10, pg, Gd, gcs);  // column form: uniform constant rows + 3 broadcast rows
+                    STAMPF(4);
 #ifndef NMPC_SEQ_PIVOTS
-                if constexpr (NU == 2) {
-                    chol_input_2<NX>(Lr, pivot, m11, m10, r, fail);  // both pivots up front
-                } else
+                    if constexpr (NU == 2) {
+                        chol_input_2<NX>(Lr, pivot, m11, m10, r, fail);  // both pivots up front
+                        seq_pivots = false;
+                    }
 #endif
-#else
-                mrow_pg_block<NX, NU>(Lr, pivot, pg, Gd);  // A/B: the row form (NX x NV broadcast FMAs)
-                STAMPF(4);
-#endif
-                sfor<0, NU>([&](auto jc) {
+                } else {
+                    mrow_pg_block<NX, NU>(Lr, pivot, pg, Gd);  // the row form (NX x NV broadcast FMAs)
+                    STAMPF(4);
+                }
+                if (seq_pivots) sfor<0, NU>([&](auto jc) {
                     constexpr int j = decltype(jc)::value;
                     if (!(pivot > 0.0)) fail = true;
                     const double rd = drsq(fmax(pivot, 1e-300));

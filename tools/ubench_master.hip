@@ -83,7 +83,8 @@ template <int VAR>
 __global__ void k_master_time(const double* Ph0, const double* G, const double* F, int steps,
                               unsigned long long* cyc, double* sink)
 {
-    __shared__ double sP[NX * NX], sG[NX * NX], sL[NX * NX];
+    __shared__ double sP[NX * NX], sG[NX * NX], sLw[4][NX * NX];
+    double* const sL = sLw[threadIdx.x >> 6];
     __shared__ float sF[NX * NX], sV[2 * NX];
     for (int i = threadIdx.x; i < NX * NX; i += blockDim.x) {
         sP[i] = Ph0[i];
@@ -119,6 +120,43 @@ __global__ void k_master_time(const double* Ph0, const double* G, const double* 
             mst_rowmul<NX, NU>(Ph, Fr, T);
             const double w = mst_vdot<NX, NU>(ph, cv, Q);
             ph = mst_vdot<NX, NU>((double)sV[NX + xi], w, Fr);
+        } else if constexpr (VAR == 7) {  // wave 0 the backward step, the other waves the dual step (other code)
+            if (threadIdx.x < 64) {
+                double Gn[NX], Q[NX];
+#pragma unroll
+                for (int c = 0; c < NX; c++) Gn[c] = -sG[xi * NX + c];
+                mst_qform<NX, NU>(Ph, Gn, Q, sL, xi, is_x);
+                double Fr[NX], Gr[NX], T[NX];
+#pragma unroll
+                for (int c = 0; c < NX; c++) {
+                    Fr[c] = (double)sF[xi * NX + c];
+                    Gr[c] = sG[xi * NX + c];
+                    T[c] = 0.0;
+                    Ph[c] = sP[xi * NX + c];
+                }
+                const double cv = mst_vdot<NX, NU>((double)sV[xi], ph, Gr);
+                mst_rowdot<NX, NU>(T, Q, Fr);
+                mst_rowmul<NX, NU>(Ph, Fr, T);
+                const double w = mst_vdot<NX, NU>(ph, cv, Q);
+                ph = mst_vdot<NX, NU>((double)sV[NX + xi], w, Fr);
+            } else {
+                double Pr[NX], Q[NX];
+#pragma unroll
+                for (int c = 0; c < NX; c++) Pr[c] = sP[xi * NX + c];
+                mst_qform<NX, NU>(Ph, Pr, Q, sL, xi, is_x);
+                const double e = mst_vdot<NX, NU>((double)sV[NX + xi], ph, Pr);
+                const double u = mst_vdot<NX, NU>(ph, -e, Q);
+                double Fc[NX], T[NX];
+#pragma unroll
+                for (int c = 0; c < NX; c++) {
+                    Fc[c] = (double)sF[c * NX + xi];
+                    Ph[c] = sG[xi * NX + c];
+                    T[c] = 0.0;
+                }
+                mst_rowdot<NX, NU>(T, Q, Fc);
+                mst_rowmul<NX, NU>(Ph, Fc, T);
+                ph = mst_vdot<NX, NU>((double)sV[xi], u, Fc);
+            }
         } else if constexpr (VAR == 1) {
             double Lp[NX], rdv[NX];
 #pragma unroll
@@ -199,7 +237,7 @@ static void rsq_accuracy()
 }
 
 template <int VAR>
-static void time_variant(const double* dPh, const double* dG, const double* dF, const char* name)
+static void time_variant(const double* dPh, const double* dG, const double* dF, const char* name, int threads = 64)
 {
     unsigned long long* dc;
     double* ds;
@@ -208,12 +246,13 @@ static void time_variant(const double* dPh, const double* dG, const double* dF, 
     const int steps = 256;
     unsigned long long c[2] = {0, 0};
     for (int rep = 0; rep < 3; rep++) {  // the last of three launches (the first ones warm the instruction cache)
-        hipLaunchKernelGGL(k_master_time<VAR>, dim3(1), dim3(64), 0, nullptr, dPh, dG, dF, steps, dc, ds);
+        hipLaunchKernelGGL(k_master_time<VAR>, dim3(1), dim3(threads), 0, nullptr, dPh, dG, dF, steps, dc, ds);
         (void)hipMemcpy(c, dc, sizeof(c), hipMemcpyDeviceToHost);
     }
     const double ghz = c[1] ? (double)c[0] / ((double)c[1] * 10.0) : 0.0;
-    std::printf("{\"timing\": \"%s\", \"steps\": %d, \"cycles_per_step\": %.1f, \"ns_per_step\": %.1f, "
-                "\"clock_ghz\": %.3f}\n", name, steps, (double)c[0] / steps, (double)c[1] * 10.0 / steps, ghz);
+    std::printf("{\"timing\": \"%s\", \"waves\": %d, \"steps\": %d, \"cycles_per_step\": %.1f, "
+                "\"ns_per_step\": %.1f, \"clock_ghz\": %.3f}\n", name, threads / 64, steps, (double)c[0] / steps,
+                (double)c[1] * 10.0 / steps, ghz);
     (void)hipFree(dc);
     (void)hipFree(ds);
 }
@@ -291,6 +330,13 @@ int main()
             time_variant<3>(dPh, dG, dF, "phat_update_products");
             time_variant<4>(dPh, dG, dF, "rowchol_raw_rsq");
             time_variant<5>(dPh, dG, dF, "lds_transpose");
+            // the same chain on every wave of one block (the waves of a CU running master steps side by side)
+            time_variant<0>(dPh, dG, dF, "backward_step", 128);
+            time_variant<0>(dPh, dG, dF, "backward_step", 256);
+            time_variant<3>(dPh, dG, dF, "phat_update_products", 128);
+            time_variant<1>(dPh, dG, dF, "rowchol", 128);
+            time_variant<7>(dPh, dG, dF, "backward_beside_dual", 128);
+            time_variant<7>(dPh, dG, dF, "backward_beside_dual", 256);
             rsq_accuracy();
         }
         std::vector<double> out(3 * nn + 2 * n);
