@@ -26,6 +26,7 @@ for c in $CONFIGS; do
 done
 timeout -k 10 60 build/ubench_master > $OUT/${TAG}_master.json; ok $? ubench_master
 bash tools/mall_calibration.sh $TAG > $OUT/${TAG}_mall.log 2>&1; ok $? mall
+mkdir -p profiles/$RND/pmc && cp $OUT/${TAG}_mall.json profiles/$RND/pmc/mall_calibration.json  # (bench.py reads it)
 for mode in warm cold; do
   timeout -k 10 120 build/capsule_latency 300 $mode > $OUT/${TAG}_capsule_c_$mode.json 2> $OUT/${TAG}_capsule_c_$mode.err; ok $? capsule_$mode
 done

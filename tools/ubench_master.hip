@@ -79,7 +79,7 @@ __global__ void k_master(const double* Ph, const double* G, const double* F, con
 // VAR 0: the kernel's backward step (qform + Phat_i = P + Phi Q Phi' + the vector terms); 1: one rowchol of Phat per
 // step; 2: qform only (Phat <- P + Q); 3: the two products of the Phat update only. cyc[0, 1]: s_memtime and
 // s_memrealtime (100 MHz) deltas of the chain.
-template <int VAR>
+template <int VAR, int UNR = 1>
 __global__ void k_master_time(const double* Ph0, const double* G, const double* F, int steps,
                               unsigned long long* cyc, double* sink)
 {
@@ -100,7 +100,7 @@ __global__ void k_master_time(const double* Ph0, const double* G, const double* 
 #pragma unroll
     for (int c = 0; c < NX; c++) Ph[c] = sP[xi * NX + c];
     const unsigned long long t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
-#pragma unroll 1
+#pragma unroll UNR
     for (int k = 0; k < steps; k++) {
         if constexpr (VAR == 0) {
             double Gn[NX], Q[NX];
@@ -236,7 +236,7 @@ static void rsq_accuracy()
     (void)hipFree(dy);
 }
 
-template <int VAR>
+template <int VAR, int UNR = 1>
 static void time_variant(const double* dPh, const double* dG, const double* dF, const char* name, int threads = 64)
 {
     unsigned long long* dc;
@@ -246,12 +246,12 @@ static void time_variant(const double* dPh, const double* dG, const double* dF, 
     const int steps = 256;
     unsigned long long c[2] = {0, 0};
     for (int rep = 0; rep < 3; rep++) {  // the last of three launches (the first ones warm the instruction cache)
-        hipLaunchKernelGGL(k_master_time<VAR>, dim3(1), dim3(threads), 0, nullptr, dPh, dG, dF, steps, dc, ds);
+        hipLaunchKernelGGL((k_master_time<VAR, UNR>), dim3(1), dim3(threads), 0, nullptr, dPh, dG, dF, steps, dc, ds);
         (void)hipMemcpy(c, dc, sizeof(c), hipMemcpyDeviceToHost);
     }
     const double ghz = c[1] ? (double)c[0] / ((double)c[1] * 10.0) : 0.0;
-    std::printf("{\"timing\": \"%s\", \"waves\": %d, \"steps\": %d, \"cycles_per_step\": %.1f, "
-                "\"ns_per_step\": %.1f, \"clock_ghz\": %.3f}\n", name, threads / 64, steps, (double)c[0] / steps,
+    std::printf("{\"timing\": \"%s\", \"unroll\": %d, \"waves\": %d, \"steps\": %d, \"cycles_per_step\": %.1f, "
+                "\"ns_per_step\": %.1f, \"clock_ghz\": %.3f}\n", name, UNR, threads / 64, steps, (double)c[0] / steps,
                 (double)c[1] * 10.0 / steps, ghz);
     (void)hipFree(dc);
     (void)hipFree(ds);
@@ -337,6 +337,10 @@ int main()
             time_variant<1>(dPh, dG, dF, "rowchol", 128);
             time_variant<7>(dPh, dG, dF, "backward_beside_dual", 128);
             time_variant<7>(dPh, dG, dF, "backward_beside_dual", 256);
+            // loop bodies of 4, 8 and 16 steps (about 20 / 40 / 80 KB of code): the instruction-cache footprint
+            time_variant<0, 4>(dPh, dG, dF, "backward_step");
+            time_variant<0, 8>(dPh, dG, dF, "backward_step");
+            time_variant<0, 16>(dPh, dG, dF, "backward_step");
             rsq_accuracy();
         }
         std::vector<double> out(3 * nn + 2 * n);
