@@ -137,9 +137,26 @@ extern "C" int nmpc_debug_mstamps_rowpar(unsigned long long* host)
 {
     return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_rp_mstamps), sizeof(g_rp_mstamps), 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -2;
 }
+// per master step of the backward sweep (lane 0): [it][i] after boundary step i
+__device__ unsigned long long g_rp_sstamps[256][kRpIts][16];
+#define RP_SSTAMP(i)                                                                                            \
+    do {                                                                                                         \
+        if (tid == 0 && inst < 256 && it < kRpIts && (i) < 16) g_rp_sstamps[inst][it][(i)] = __builtin_amdgcn_s_memtime(); \
+    } while (0)
+// the dual sweep's steps (lane 64 * kDW): slot 8 + i after step i (i <= 7)
+#define RP_DSTAMP(i)                                                                                            \
+    do {                                                                                                         \
+        if ((tid & 63) == 0 && tid > 0 && inst < 256 && it < kRpIts && (i) < 8) g_rp_sstamps[inst][it][8 + (i)] = __builtin_amdgcn_s_memtime(); \
+    } while (0)
+extern "C" int nmpc_debug_sstamps_rowpar(unsigned long long* host)
+{
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_rp_sstamps), sizeof(g_rp_sstamps), 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -2;
+}
 #else
 #define RP_STAMP(slot) ((void)0)
 #define RP_MSTAMP(slot, lane) ((void)0)
+#define RP_SSTAMP(i) ((void)0)
+#define RP_DSTAMP(i) ((void)0)
 #endif
 
 namespace {
@@ -985,6 +1002,7 @@ __global__ __launch_bounds__(64 * W, (SEG && M::NX < 10) ? 2 : 1) void k_sqp_rti
                         mst_rowmul<NX, NU>(Ph, Fr, T);  // Phat_i = P_i + Phi T
                         const double w = mst_vdot<NX, NU>(ph, cv, Q);
                         ph = mst_vdot<NX, NU>((double)seg_lds[SegL.SUM_PB + i * NX + xi], w, Fr);
+                        RP_SSTAMP(i);
                     }
                     if (is_x) {  // Phat_m, phat_m for the join
 #pragma unroll
@@ -1022,6 +1040,7 @@ __global__ __launch_bounds__(64 * W, (SEG && M::NX < 10) ? 2 : 1) void k_sqp_rti
                         mst_rowdot<NX, NU>(T, Q, Fc);   // T = Q' Phi
                         mst_rowmul<NX, NU>(Sh, Fc, T);  // Shat_{i+1} = -Gam_i + Phi' T
                         sh = mst_vdot<NX, NU>((double)seg_lds[SegL.SUM_T + i * NX + xi], u, Fc);
+                        RP_DSTAMP(i);
                     }
                     if (is_x) {  // Shat_m, shat_m for the join
 #pragma unroll

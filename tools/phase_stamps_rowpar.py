@@ -71,3 +71,37 @@ if seg and hasattr(L, "nmpc_debug_mstamps_rowpar"):
                           if ms[r, i, a] > 0 and ms[r, i, b] > 0])
             if len(v):
                 print("  master %-20s mean %7.0f p50 %7.0f n %d" % (name, v.mean(), np.median(v), len(v)))
+
+# per boundary step of the backward sweep (diag builds with g_rp_sstamps): cycles between consecutive steps
+if seg and hasattr(L, "nmpc_debug_sstamps_rowpar") and hasattr(L, "nmpc_debug_mstamps_rowpar"):
+    sb = (ctypes.c_ulonglong * (256 * 64 * 16))()
+    L.nmpc_debug_sstamps_rowpar.argtypes = [ctypes.c_void_p]
+    if L.nmpc_debug_sstamps_rowpar(sb) == 0:
+        ss = np.frombuffer(sb, dtype=np.uint64).reshape(256, 64, 16).astype(np.int64)[:min(B, 256)]
+        S_ = plan[2]
+        m_ = 0 if os.environ.get("SEQM") else S_ // 2
+        steps = list(range(S_ - 2, m_ - 1, -1))  # the backward sweep's boundaries, in order
+        rows = []
+        for r in range(ss.shape[0]):
+            for i in range(int(it[r])):
+                t0 = ms[r, i, 0]
+                prev, d = t0, []
+                for b in steps:
+                    d.append(ss[r, i, b] - prev)
+                    prev = ss[r, i, b]
+                rows.append(d)
+        if rows:
+            a = np.array(rows)
+            print("  backward sweep per step (boundary order %s): mean %s" % (steps, np.round(a.mean(axis=0)).astype(int).tolist()))
+        dsteps = list(range(1, m_)) if m_ <= 8 else []
+        drows = []
+        for r in range(ss.shape[0]):
+            for i in range(int(it[r])):
+                prev, d = ms[r, i, 0], []
+                for b in dsteps:
+                    d.append(ss[r, i, 8 + b] - prev)
+                    prev = ss[r, i, 8 + b]
+                drows.append(d)
+        if dsteps and drows:
+            a = np.array(drows)
+            print("  dual sweep per step (boundary order %s): mean %s" % (dsteps, np.round(a.mean(axis=0)).astype(int).tolist()))
