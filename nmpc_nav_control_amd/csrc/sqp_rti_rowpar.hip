@@ -72,8 +72,8 @@ struct SegLayout {
         CS = QS + 2 * S * NX * NX;          // [S][NX] double
         PHS = CS + 2 * S * NX;              // [S][NX] double
         LT = PHS + 2 * S * NX;              // [2][NX][NX] double: the master rows' transpose scratch
-        XA = LT + 4 * NX * NX;              // [2][NX + 1][NX] double: Phat_m, phat_m / Shat_m, shat_m for the join
-        SL = XA + 4 * (NX + 1) * NX;        // [S + 1][2][NX]: s_q, lam_q
+        XA = LT + 4 * NX * NX;              // [2][NX + 1][NX] + [NX] double: Phat_m, phat_m / Shat_m, shat_m; lam_m
+        SL = XA + 4 * (NX + 1) * NX + 2 * NX;  // [S + 1][2][NX]: s_q, lam_q
         ZL = SL + (S + 1) * 2 * NX;         // [N + 1][NU][NXP]
     }
     __host__ __device__ size_t floats(int N) const { return (size_t)ZL + (size_t)(N + 1) * NU * NXP; }
@@ -143,11 +143,6 @@ __device__ unsigned long long g_rp_sstamps[256][kRpIts][16];
     do {                                                                                                         \
         if (tid == 0 && inst < 256 && it < kRpIts && (i) < 16) g_rp_sstamps[inst][it][(i)] = __builtin_amdgcn_s_memtime(); \
     } while (0)
-// the dual sweep's steps (lane 64 * kDW): slot 8 + i after step i (i <= 7)
-#define RP_DSTAMP(i)                                                                                            \
-    do {                                                                                                         \
-        if ((tid & 63) == 0 && tid > 0 && inst < 256 && it < kRpIts && (i) < 8) g_rp_sstamps[inst][it][8 + (i)] = __builtin_amdgcn_s_memtime(); \
-    } while (0)
 extern "C" int nmpc_debug_sstamps_rowpar(unsigned long long* host)
 {
     return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_rp_sstamps), sizeof(g_rp_sstamps), 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -2;
@@ -156,7 +151,6 @@ extern "C" int nmpc_debug_sstamps_rowpar(unsigned long long* host)
 #define RP_STAMP(slot) ((void)0)
 #define RP_MSTAMP(slot, lane) ((void)0)
 #define RP_SSTAMP(i) ((void)0)
-#define RP_DSTAMP(i) ((void)0)
 #endif
 
 namespace {
@@ -919,224 +913,152 @@ __global__ __launch_bounds__(64 * W, (SEG && M::NX < 10) ? 2 : 1) void k_sqp_rti
             // ---- master (fp64): the two-point recursion over the segment boundaries,
             //   s_{i+1} = Phi_i' s_i + Gam_i lam_{i+1} + t_i,   lam_i = P_i s_i + pbar_i + Phi_i lam_{i+1}   (s_0 = 0),
             // solved from both ends at once and joined at boundary m = S / 2 (round 5: the chain of factorisations
-            // falls from S - 1 boundary steps to max(S - 1 - m, m - 1) + 1, e.g. 7 -> 4 at N = 80, S = 8, 3 -> 2 at S = 4):
+            // falls from S - 1 boundary steps to max(S - 1 - m, m - 1) + 1, e.g. 7 -> 4 at N = 80, S = 8):
             //  - row 0 of wave 0, the backward sweep lam_i = Phat_i s_i + phat_i (Phat_{S-1} = P_{S-1}) down to m, with
             //    Q_i = Phat_{i+1} (I - Gam_i Phat_{i+1})^-1, Phat_i = P_i + Phi_i Q_i Phi_i', c_i = t_i + Gam_i phat_{i+1},
             //    phat_i = pbar_i + Phi_i (Q_i c_i + phat_{i+1});
-            //  - row 0 of wave 1 (wave 0 after the backward sweep when the block has one wave), the dual sweep
-            //    s_i = -Shat_i lam_i + shat_i (Shat_1 = -Gam_0, shat_1 = t_0) up to m, with Q'_i = (I + Shat_i P_i)^-1 Shat_i,
-            //    Shat_{i+1} = -Gam_i + Phi_i' Q'_i Phi_i, u_i = shat_i - Q'_i (pbar_i + P_i shat_i), shat_{i+1} = t_i + Phi_i' u_i;
-            //  - the join (row 0 of wave 0): lam_m = Q_j (shat_m - Shat_m phat_m) + phat_m with Q_j = Phat_m (I + Shat_m
-            //    Phat_m)^-1, s_m = shat_m - Shat_m lam_m;
-            //  - then wave 0 propagates s, lam forward to S - 1 (lam_{i+1} = Q_i (Phi_i' s_i + c_i) + phat_{i+1}, s_{i+1} =
-            //    Phi_i' s_i + Gam_i lam_{i+1} + t_i) while the dual row propagates them back to 1 (s_i = u_i - Q'_i Phi_i
-            //    lam_{i+1}, lam_i = P_i s_i + pbar_i + Phi_i lam_{i+1}).
-            // Every Q (Q_i, Q'_i, Q_j) is A (I + C A)^-1 = L (I + L' C L)^-1 L' with C >= 0, formed through the factor
-            // L L' = A (pivots below 1e-13 of their diagonal entry dropped) as Y Y', Y = L R^-T, R R' = K = I + L' C L (K >= I:
-            // Cholesky without pivoting; positive semidefinite by construction; the Woodbury form and a factor of -Gam
-            // both failed numerically, tools/seg_case_study.py). Lane NU + r holds row r of every matrix and element r of
-            // every vector (the fused-DPP blocks of team_asm_gen.hpp); segment data come from LDS
+            //  - row 1 of wave 0, the dual sweep s_i = -Shat_i lam_i + shat_i (Shat_1 = -Gam_0, shat_1 = t_0) up to m,
+            //    Q'_i = (I + Shat_i P_i)^-1 Shat_i, Shat_{i+1} = -Gam_i + Phi_i' Q'_i Phi_i,
+            //    u_i = shat_i - Q'_i (pbar_i + P_i shat_i), shat_{i+1} = t_i + Phi_i' u_i;
+            //  - the join (row 0): lam_m = Q_j (shat_m - Shat_m phat_m) + phat_m, Q_j = Phat_m (I + Shat_m Phat_m)^-1,
+            //    s_m = shat_m - Shat_m lam_m;
+            //  - row 0 propagates s, lam forward to S - 1 (lam_{i+1} = Q_i (Phi_i' s_i + c_i) + phat_{i+1},
+            //    s_{i+1} = Phi_i' s_i + Gam_i lam_{i+1} + t_i) while row 1 propagates them back to 1
+            //    (s_i = u_i - Q'_i Phi_i lam_{i+1}, lam_i = P_i s_i + pbar_i + Phi_i lam_{i+1}).
+            // Both sweeps are one instruction stream: a step is the same sequence of fused-DPP blocks on the two rows,
+            // each row addressing its own operands (backward: C = -Gam_i, D = P_i, F = Phi_i; dual: C = P_i,
+            // D = -Gam_i, F = Phi_i'), so they cost one step's issue; on two waves of a CU they slowed each other
+            // down by half (profiles/r05/stamps/). Every Q (Q_i, Q'_i, Q_j) is A (I + C A)^-1 = L (I + L' C L)^-1 L'
+            // with C >= 0 (mst_qform). Lane NU + r of a row holds row r of every matrix and element r of every vector.
 #ifdef NMPC_SEQ_MASTER
             constexpr bool kSeqM = true;  // A/B only: the round-4 master (backward over all S - 1 boundaries, then forward)
 #else
             constexpr bool kSeqM = false;
 #endif
             const int mj = kSeqM ? 0 : Sg / 2;        // the join boundary (1 <= m <= S - 1)
+            const int nbw = Sg - 1 - mj;              // backward-sweep steps (boundaries S - 2 .. m)
+            const int ndu = kSeqM ? 0 : mj - 1;       // dual-sweep steps (boundaries 1 .. m - 1)
             const bool mrow0 = tid < 16;              // backward sweep, join, forward propagation
-#ifndef NMPC_DUAL_WAVE
-#define NMPC_DUAL_WAVE 1  // (A/B: the wave of the dual sweep when the block has more than one)
-#endif
-            constexpr int kDW = (W > NMPC_DUAL_WAVE) ? NMPC_DUAL_WAVE : 1;
-            const bool mrowd = (W > 1) ? (tid >= 64 * kDW && tid < 64 * kDW + 16) : (tid < 16);  // the dual sweep
-            if (Sg > 1 && (mrow0 || mrowd)) {
+            const bool bwr = mrow0;                   // (row 1 of wave 0: the dual side)
+            float* const sl = seg_lds + SegL.SL;
+            if (Sg > 1 && wave == 0 && tid < 32) {
                 const double* const sP = reinterpret_cast<const double*>(seg_lds + SegL.SUM_P);
+                const double* const sG = reinterpret_cast<const double*>(seg_lds + SegL.SUM_GAM);
                 double* const sQ = reinterpret_cast<double*>(seg_lds + SegL.QS);
                 double* const sCv = reinterpret_cast<double*>(seg_lds + SegL.CS);
                 double* const sPh = reinterpret_cast<double*>(seg_lds + SegL.PHS);
-                double* const sLt = reinterpret_cast<double*>(seg_lds + SegL.LT) + (wave > 0 ? NX * NX : 0);
+                double* const sLt = reinterpret_cast<double*>(seg_lds + SegL.LT) + (bwr ? 0 : NX * NX);
                 double* const sXa = reinterpret_cast<double*>(seg_lds + SegL.XA);
-                auto ldrow = [&](int i, int off, double (&v)[NX]) {  // row xi of segment i's fp32 matrix at off
+                double* const sXo = sXa + (bwr ? 0 : (NX + 1) * NX);  // this row's final (X, x): Phat_m / Shat_m
+                const double sgn = bwr ? -1.0 : 1.0;
+                // per-row operands of boundary i: C (sign sgn) and D (sign -sgn) rows, the F row (Phi_i row or
+                // column) and the vector terms a0 (t_i / pbar_i) and a1 (pbar_i / t_i)
+                const double* const pC = bwr ? sG : sP;
+                const double* const pD = bwr ? sP : sG;
+                const int fs1 = bwr ? NX : 1, fs2 = bwr ? 1 : NX;  // F element c: Phi[i][xi * fs1 + c * fs2]
+                const int a0off = bwr ? SegL.SUM_T : SegL.SUM_PB, a1off = bwr ? SegL.SUM_PB : SegL.SUM_T;
+                double X[NX], x;
+                {  // Phat_{S-1} = P_{S-1}, phat_{S-1} = pbar_{S-1} / Shat_1 = -Gam_0, shat_1 = t_0
+                    const int i0 = bwr ? Sg - 1 : 0;
 #pragma unroll
-                    for (int c = 0; c < NX; c++) v[c] = (double)seg_lds[off + (i * NX + xi) * NX + c];
-                };
-                auto ldgam = [&](int i, double (&v)[NX]) {  // row xi of Gam_i (fp64)
+                    for (int c = 0; c < NX; c++) X[c] = -sgn * pD[((size_t)i0 * NX + xi) * NX + c];
+                    x = (double)seg_lds[(bwr ? SegL.SUM_PB : SegL.SUM_T) + i0 * NX + xi];
+                }
+                if (is_x) {
 #pragma unroll
-                    for (int c = 0; c < NX; c++) v[c] = reinterpret_cast<const double*>(seg_lds + SegL.SUM_GAM)[(i * NX + xi) * NX + c];
-                };
-                auto ldcol = [&](int i, int off, double (&v)[NX]) {  // column xi (row xi of the transpose)
-#pragma unroll
-                    for (int c = 0; c < NX; c++) v[c] = (double)seg_lds[off + (i * NX + c) * NX + xi];
-                };
-                auto qform = [&](const double (&Ar)[NX], const double (&Cr)[NX], double (&Q)[NX]) {
-                    mst_qform<NX, NU>(Ar, Cr, Q, sLt, xi, is_x);
-                };
-                auto backward = [&]() {
-                    double Ph[NX], ph;
-#pragma unroll
-                    for (int c = 0; c < NX; c++) Ph[c] = sP[((size_t)(Sg - 1) * NX + xi) * NX + c];
-                    ph = (double)seg_lds[SegL.SUM_PB + (Sg - 1) * NX + xi];
-                    for (int i = Sg - 2; i >= mj; i--) {
-                        double Gn[NX], Q[NX];
-                        ldgam(i, Gn);
-#pragma unroll
-                        for (int c = 0; c < NX; c++) Gn[c] = -Gn[c];
-                        qform(Ph, Gn, Q);  // Q_i = Phat_{i+1} (I - Gam_i Phat_{i+1})^-1
-                        double Fr[NX], Gr[NX];
-                        ldrow(i, SegL.SUM_PHI, Fr);
-                        ldgam(i, Gr);
-                        const double cv = mst_vdot<NX, NU>((double)seg_lds[SegL.SUM_T + i * NX + xi], ph, Gr);
-                        if (is_x) {
-#pragma unroll
-                            for (int c = 0; c < NX; c++) sQ[((size_t)i * NX + xi) * NX + c] = Q[c];
-                            sCv[i * NX + xi] = cv;
-                            sPh[i * NX + xi] = ph;
-                        }
-                        // Phat_i = P_i + Phi_i Q_i Phi_i',  phat_i = pbar_i + Phi_i (Q_i c_i + phat_{i+1})
-                        double T[NX];
-#pragma unroll
-                        for (int c = 0; c < NX; c++) {
-                            T[c] = 0.0;
-                            Ph[c] = sP[((size_t)i * NX + xi) * NX + c];
-                        }
-                        mst_rowdot<NX, NU>(T, Q, Fr);   // T = Q Phi'
-                        mst_rowmul<NX, NU>(Ph, Fr, T);  // Phat_i = P_i + Phi T
-                        const double w = mst_vdot<NX, NU>(ph, cv, Q);
-                        ph = mst_vdot<NX, NU>((double)seg_lds[SegL.SUM_PB + i * NX + xi], w, Fr);
-                        RP_SSTAMP(i);
-                    }
-                    if (is_x) {  // Phat_m, phat_m for the join
-#pragma unroll
-                        for (int c = 0; c < NX; c++) sXa[xi * NX + c] = Ph[c];
-                        sXa[NX * NX + xi] = ph;
-                    }
-                };
-                auto dual = [&]() {
-                    double Sh[NX], sh;
-                    ldgam(0, Sh);
-#pragma unroll
-                    for (int c = 0; c < NX; c++) Sh[c] = -Sh[c];  // Shat_1 = -Gam_0
-                    sh = (double)seg_lds[SegL.SUM_T + xi];        // shat_1 = t_0
-                    for (int i = 1; i < mj; i++) {
-                        double Pr[NX], Q[NX];
-#pragma unroll
-                        for (int c = 0; c < NX; c++) Pr[c] = sP[((size_t)i * NX + xi) * NX + c];
-                        qform(Sh, Pr, Q);  // Q'_i = (I + Shat_i P_i)^-1 Shat_i
-                        const double e = mst_vdot<NX, NU>((double)seg_lds[SegL.SUM_PB + i * NX + xi], sh, Pr);
-                        const double u = mst_vdot<NX, NU>(sh, -e, Q);  // u_i = shat_i - Q'_i (pbar_i + P_i shat_i)
-                        if (is_x) {
-#pragma unroll
-                            for (int c = 0; c < NX; c++) sQ[((size_t)i * NX + xi) * NX + c] = Q[c];
-                            sCv[i * NX + xi] = u;
-                        }
-                        // Shat_{i+1} = -Gam_i + Phi_i' Q'_i Phi_i,  shat_{i+1} = t_i + Phi_i' u_i
-                        double Fc[NX], T[NX];
-                        ldcol(i, SegL.SUM_PHI, Fc);
-                        ldgam(i, Sh);
-#pragma unroll
-                        for (int c = 0; c < NX; c++) {
-                            T[c] = 0.0;
-                            Sh[c] = -Sh[c];
-                        }
-                        mst_rowdot<NX, NU>(T, Q, Fc);   // T = Q' Phi
-                        mst_rowmul<NX, NU>(Sh, Fc, T);  // Shat_{i+1} = -Gam_i + Phi' T
-                        sh = mst_vdot<NX, NU>((double)seg_lds[SegL.SUM_T + i * NX + xi], u, Fc);
-                        RP_DSTAMP(i);
-                    }
-                    if (is_x) {  // Shat_m, shat_m for the join
-#pragma unroll
-                        for (int c = 0; c < NX; c++) sXa[(NX + 1 + xi) * NX + c] = Sh[c];
-                        sXa[(2 * NX + 1) * NX + xi] = sh;
-                    }
-                };
+                    for (int c = 0; c < NX; c++) sXo[xi * NX + c] = X[c];
+                    sXo[NX * NX + xi] = x;
+                }
                 RP_MSTAMP(0, 0);
-                if (kSeqM) {
-                    if (wave == 0 && mrow0) backward();
-                } else if (W > 1) {
-                    if (wave == 0) {  // (wave-uniform branches: neither wave issues the other's sweep under a zero mask)
-                        if (mrow0) backward();
-                    } else if (wave == kDW) {
-                        if (mrowd) dual();
+                const int ns = nbw > ndu ? nbw : ndu;
+                for (int j = 0; j < ns; j++) {
+                    const bool act = bwr ? (j < nbw) : (j < ndu);
+                    const int i = act ? (bwr ? Sg - 2 - j : 1 + j) : 1;  // (an idle row reads boundary 1, stores nothing)
+                    double Cm[NX], Q[NX];
+#pragma unroll
+                    for (int c = 0; c < NX; c++) Cm[c] = sgn * pC[((size_t)i * NX + xi) * NX + c];
+                    mst_qform<NX, NU>(X, Cm, Q, sLt, xi, is_x);
+                    // v = a0 + R x (R = Gam_i / P_i = sgn C): c_i / e_i;  w = x + sQ Q v (sQ = -sgn): phat + Q c / u_i
+                    const double v = mst_vdot<NX, NU>((double)seg_lds[a0off + i * NX + xi], sgn * x, Cm);
+                    const double w = mst_vdot<NX, NU>(x, -sgn * v, Q);
+                    if (act && is_x) {
+#pragma unroll
+                        for (int c = 0; c < NX; c++) sQ[((size_t)i * NX + xi) * NX + c] = Q[c];
+                        sCv[i * NX + xi] = bwr ? v : w;
+                        if (bwr) sPh[i * NX + xi] = x;
                     }
-                } else {
-                    backward();
-                    dual();
+                    // X' = D + F Q F', x' = a1 + F w
+                    double Fr[NX], T[NX];
+#pragma unroll
+                    for (int c = 0; c < NX; c++) {
+                        Fr[c] = (double)seg_lds[SegL.SUM_PHI + i * NX * NX + xi * fs1 + c * fs2];
+                        T[c] = 0.0;
+                        X[c] = -sgn * pD[((size_t)i * NX + xi) * NX + c];
+                    }
+                    mst_rowdot<NX, NU>(T, Q, Fr);
+                    mst_rowmul<NX, NU>(X, Fr, T);
+                    x = mst_vdot<NX, NU>((double)seg_lds[a1off + i * NX + xi], w, Fr);
+                    if (act && is_x) {
+#pragma unroll
+                        for (int c = 0; c < NX; c++) sXo[xi * NX + c] = X[c];
+                        sXo[NX * NX + xi] = x;
+                    }
+                    if (bwr) RP_SSTAMP(i);
                 }
+                lds_fence();  // (Q_i, c_i, u_i, phat, and both rows' final X, x in LDS)
                 RP_MSTAMP(1, 0);
-                RP_MSTAMP(2, 64 * kDW);
-            }
-            __syncthreads();  // Phat_m, phat_m and Shat_m, shat_m in LDS
-            RP_MSTAMP(3, 0);
-            float* const sl = seg_lds + SegL.SL;
-            if (Sg > 1 && wave == 0 && mrow0) {
-                const double* const sXa = reinterpret_cast<const double*>(seg_lds + SegL.XA);
-                const double* const sQ = reinterpret_cast<const double*>(seg_lds + SegL.QS);
-                const double* const sCv = reinterpret_cast<const double*>(seg_lds + SegL.CS);
-                const double* const sPh = reinterpret_cast<const double*>(seg_lds + SegL.PHS);
-                double* const sLt = reinterpret_cast<double*>(seg_lds + SegL.LT);
-                double Sr[NX], Q[NX];
+                // the join (row 0): lam_m, s_m
+                double sv = 0.0, lam_m = 0.0;
+                if (!kSeqM && bwr) {
+                    double Pm[NX], Sr[NX], Q[NX];
 #pragma unroll
-                for (int c = 0; c < NX; c++) Sr[c] = sXa[(NX + 1 + xi) * NX + c];
-                if (!kSeqM) {  // Q_j = L (I + L' Shat_m L)^-1 L', L L' = Phat_m
-                    double Pm[NX];
-#pragma unroll
-                    for (int c = 0; c < NX; c++) Pm[c] = sXa[xi * NX + c];
+                    for (int c = 0; c < NX; c++) {
+                        Pm[c] = sXa[xi * NX + c];
+                        Sr[c] = sXa[(NX + 1 + xi) * NX + c];
+                    }
                     mst_qform<NX, NU>(Pm, Sr, Q, sLt, xi, is_x);
+                    const double ph = sXa[NX * NX + xi], shm = sXa[(2 * NX + 1) * NX + xi];
+                    const double v1 = mst_vdot<NX, NU>(shm, -ph, Sr);  // shat_m - Shat_m phat_m
+                    lam_m = mst_vdot<NX, NU>(ph, v1, Q);
+                    sv = mst_vdot<NX, NU>(shm, -lam_m, Sr);           // s_m = shat_m - Shat_m lam_m
+                    if (is_x) {
+                        sl[mj * 2 * NX + xi] = (float)sv;
+                        sl[mj * 2 * NX + NX + xi] = (float)lam_m;
+                        sXa[2 * (NX + 1) * NX + xi] = lam_m;  // (full precision for row 1)
+                    }
                 }
-                const double ph = sXa[NX * NX + xi], shm = sXa[(2 * NX + 1) * NX + xi];
-                const double v1 = mst_vdot<NX, NU>(shm, -ph, Sr);   // shat_m - Shat_m phat_m
-                const double lam_m = mst_vdot<NX, NU>(ph, v1, Q);  // lam_m
-                double sv = kSeqM ? 0.0 : mst_vdot<NX, NU>(shm, -lam_m, Sr);  // s_m = shat_m - Shat_m lam_m
-                if (is_x && !kSeqM) {
-                    sl[mj * 2 * NX + xi] = (float)sv;
-                    sl[mj * 2 * NX + NX + xi] = (float)lam_m;
-                    reinterpret_cast<double*>(seg_lds + SegL.XA)[xi] = lam_m;  // (full precision for the dual row)
-                }
+                lds_fence();
                 RP_MSTAMP(4, 0);
-                if (W == 1) lds_fence();
-                // forward from m: lam_{i+1} = Q_i (Phi_i' s_i + c_i) + phat_{i+1}, s_{i+1} = Phi_i' s_i + Gam_i lam_{i+1} + t_i
-                for (int i = mj; i <= Sg - 2; i++) {
-                    double Fc[NX], Gr[NX], Qr[NX];
+                // outward propagation, both rows as one stream: z = s_i (row 0, i = m .. S - 2) / lam_{i+1} (row 1,
+                // i = m - 1 .. 1);  y = F z (F = Phi_i' / Phi_i);  o = b0 + sO Q_i (y + alpha) (lam_{i+1} / s_i);
+                // z' = y + beta + R o (s_{i+1} / lam_i), R = Gam_i / P_i
+                double z = bwr ? sv : (kSeqM ? 0.0 : sXa[2 * (NX + 1) * NX + xi]);
+                const int nfw = Sg - 1 - mj, nbp = kSeqM ? 0 : mj - 1;
+                const int no = nfw > nbp ? nfw : nbp;
+                const int gs1 = bwr ? 1 : NX, gs2 = bwr ? NX : 1;  // (the transposed F of the sweep)
+                for (int j = 0; j < no; j++) {
+                    const bool act = bwr ? (j < nfw) : (j < nbp);
+                    const int i = act ? (bwr ? mj + j : mj - 1 - j) : 1;
+                    double Fr[NX], Qr[NX], Rr[NX];
 #pragma unroll
                     for (int l = 0; l < NX; l++) {
-                        Fc[l] = (double)seg_lds[SegL.SUM_PHI + (i * NX + l) * NX + xi];
+                        Fr[l] = (double)seg_lds[SegL.SUM_PHI + i * NX * NX + xi * gs1 + l * gs2];
                         Qr[l] = sQ[((size_t)i * NX + xi) * NX + l];
-                        Gr[l] = reinterpret_cast<const double*>(seg_lds + SegL.SUM_GAM)[(i * NX + xi) * NX + l];
+                        Rr[l] = pC[((size_t)i * NX + xi) * NX + l];
                     }
-                    const double fs = mst_vdot<NX, NU>(0.0, sv, Fc);
-                    const double v = fs + sCv[i * NX + xi];
-                    const double lam = mst_vdot<NX, NU>(sPh[i * NX + xi], v, Qr);
-                    sv = mst_vdot<NX, NU>(fs + (double)seg_lds[SegL.SUM_T + i * NX + xi], lam, Gr);
-                    if (is_x) {
-                        sl[(i + 1) * 2 * NX + xi] = (float)sv;
-                        sl[(i + 1) * 2 * NX + NX + xi] = (float)lam;
+                    const double y = mst_vdot<NX, NU>(0.0, z, Fr);
+                    const double cw = sCv[i * NX + xi];  // c_i (row 0) / u_i (row 1)
+                    const double b0 = bwr ? sPh[i * NX + xi] : cw;
+                    const double o = mst_vdot<NX, NU>(b0, bwr ? y + cw : -y, Qr);
+                    const double z2 = mst_vdot<NX, NU>(y + (double)seg_lds[a0off + i * NX + xi], o, Rr);
+                    if (act && is_x) {
+                        const int slot = bwr ? i + 1 : i;
+                        sl[slot * 2 * NX + xi] = (float)(bwr ? z2 : o);
+                        sl[slot * 2 * NX + NX + xi] = (float)(bwr ? o : z2);
                     }
+                    z = z2;
                 }
                 RP_MSTAMP(5, 0);
-            }
-            if (W > 1) __syncthreads();  // lam_m for the dual row
-            if (Sg > 1 && wave == (W > 1 ? kDW : 0) && mrowd) {
-                // back from m: s_i = u_i - Q'_i Phi_i lam_{i+1}, lam_i = P_i s_i + pbar_i + Phi_i lam_{i+1}
-                const double* const sP = reinterpret_cast<const double*>(seg_lds + SegL.SUM_P);
-                const double* const sQ = reinterpret_cast<const double*>(seg_lds + SegL.QS);
-                const double* const sCv = reinterpret_cast<const double*>(seg_lds + SegL.CS);
-                double lv_ = reinterpret_cast<const double*>(seg_lds + SegL.XA)[xi];  // lam_m
-                for (int i = mj - 1; i >= 1; i--) {
-                    double Fr[NX], Qr[NX], Pr[NX];
-#pragma unroll
-                    for (int l = 0; l < NX; l++) {
-                        Fr[l] = (double)seg_lds[SegL.SUM_PHI + (i * NX + xi) * NX + l];
-                        Qr[l] = sQ[((size_t)i * NX + xi) * NX + l];
-                        Pr[l] = sP[((size_t)i * NX + xi) * NX + l];
-                    }
-                    const double fl = mst_vdot<NX, NU>(0.0, lv_, Fr);               // Phi_i lam_{i+1}
-                    const double si = mst_vdot<NX, NU>(sCv[i * NX + xi], -fl, Qr);  // u_i - Q'_i Phi_i lam_{i+1}
-                    lv_ = mst_vdot<NX, NU>((double)seg_lds[SegL.SUM_PB + i * NX + xi] + fl, si, Pr);
-                    if (is_x) {
-                        sl[i * 2 * NX + xi] = (float)si;
-                        sl[i * 2 * NX + NX + xi] = (float)lv_;
-                    }
-                }
-                RP_MSTAMP(6, 64 * kDW);
             }
             __syncthreads();  // the boundary states and costates
             RP_MSTAMP(7, 0);

@@ -93,15 +93,3 @@ if seg and hasattr(L, "nmpc_debug_sstamps_rowpar") and hasattr(L, "nmpc_debug_ms
         if rows:
             a = np.array(rows)
             print("  backward sweep per step (boundary order %s): mean %s" % (steps, np.round(a.mean(axis=0)).astype(int).tolist()))
-        dsteps = list(range(1, m_)) if m_ <= 8 else []
-        drows = []
-        for r in range(ss.shape[0]):
-            for i in range(int(it[r])):
-                prev, d = ms[r, i, 0], []
-                for b in dsteps:
-                    d.append(ss[r, i, 8 + b] - prev)
-                    prev = ss[r, i, 8 + b]
-                drows.append(d)
-        if dsteps and drows:
-            a = np.array(drows)
-            print("  dual sweep per step (boundary order %s): mean %s" % (dsteps, np.round(a.mean(axis=0)).astype(int).tolist()))
