@@ -455,15 +455,20 @@ __global__ __launch_bounds__(64 * W, (SEG && M::NX < 10) ? 2 : 1) void k_sqp_rti
                 dx = is_x ? nx_ + cur.b : 0.0f;
             }
         };
-        Stg ca, cb;  // two buffers used in turn (no copies: a copy waits for the LDS read in flight)
-        lds_ld(0, ca);
-        for (int k = 0;; k += 2) {
-            lds_ld(k + 1, cb);
-            step(k, ca);
+        // three buffers used in turn, loads two stages ahead (no copies: a copy waits for the LDS read in flight)
+        Stg c0, c1, c2;
+        lds_ld(0, c0);
+        lds_ld(1, c1);
+        for (int k = 0;; k += 3) {
+            lds_ld(k + 2, c2);
+            step(k, c0);
             if (k == N) break;
-            lds_ld(k + 2, ca);
-            step(k + 1, cb);
+            lds_ld(k + 3, c0);
+            step(k + 1, c1);
             if (k + 1 == N) break;
+            lds_ld(k + 4, c1);
+            step(k + 2, c2);
+            if (k + 2 == N) break;
         }
     }
     __syncthreads();
