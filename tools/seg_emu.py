@@ -210,10 +210,15 @@ def kkt_res(G, H, g, nx, nu, N, us, xs):
     return worst
 
 
-def riccati_segmented(G, H, g, nx, nu, N, S, sens_dtype=np.float64, chol_master=False):
+def riccati_segmented(G, H, g, nx, nu, N, S, sens_dtype=np.float64, chol_master=False, master_fn=None):
+    """master_fn(segs, nx) -> (s, lam): another master form (the default: `master`, or `master_chol`)."""
     bnd = np.linspace(0, N + 1, S + 1).round().astype(int)
     segs = [seg_backward(G, H, g, nx, nu, N, bnd[i], bnd[i + 1], sens_dtype) for i in range(S)]
-    s, lam, Xs = (master_chol if chol_master else master)(segs, nx)
+    if master_fn is not None:
+        s, lam = master_fn(segs, nx)
+        Xs = [np.eye(nx)]
+    else:
+        s, lam, Xs = (master_chol if chol_master else master)(segs, nx)
     us, xs = np.zeros((N, nu)), np.zeros((N + 1, nx))
     gap = 0.0
     for i in range(S):
