@@ -125,9 +125,8 @@ extern "C" int nmpc_debug_stamps_rowpar(unsigned long long* host)
 {
     return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_rp_stamps), sizeof(g_rp_stamps), 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -2;
 }
-// the segment master's parts, per IPM iteration: [0] start (lane 0), [1] backward sweep done (lane 0), [2] dual
-// sweep done (lane 64), [3] after the first barrier, [4] join done, [5] forward propagation done (lane 0),
-// [6] backward propagation done (lane 64), [7] after the last barrier
+// the segment master's parts, per IPM iteration (lane 0): [0] start, [1] both sweeps done, [4] join done,
+// [5] both propagations done, [7] after the block barrier (slots 2, 3, 6: unused since the one-stream master)
 __device__ unsigned long long g_rp_mstamps[256][kRpIts][8];
 #define RP_MSTAMP(slot, lane)                                                                                    \
     do {                                                                                                         \

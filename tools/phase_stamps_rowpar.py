@@ -64,8 +64,8 @@ if seg and hasattr(L, "nmpc_debug_mstamps_rowpar"):
     L.nmpc_debug_mstamps_rowpar.argtypes = [ctypes.c_void_p]
     if L.nmpc_debug_mstamps_rowpar(mb) == 0:
         ms = np.frombuffer(mb, dtype=np.uint64).reshape(256, 64, 8).astype(np.int64)[:min(B, 256)]
-        parts = {"backward sweep (w0)": (0, 1), "dual sweep (w1)": (0, 2), "barrier 1": (1, 3), "join": (3, 4),
-                 "forward prop (w0)": (4, 5), "backward prop (w1)": (4, 6), "to last barrier": (5, 7), "total": (0, 7)}
+        parts = {"sweeps (rows 0 / 1)": (0, 1), "join": (1, 4), "propagations": (4, 5), "to the barrier": (5, 7),
+                 "total": (0, 7)}
         for name, (a, b) in parts.items():
             v = np.array([ms[r, i, b] - ms[r, i, a] for r in range(ms.shape[0]) for i in range(int(it[r]))
                           if ms[r, i, a] > 0 and ms[r, i, b] > 0])
