@@ -601,7 +601,7 @@ __global__ __launch_bounds__(64 * W, (SEG && M::NX < 10) ? 2 : 1) void k_sqp_rti
             ld_range<F0, F1, RS, QM>(tbase + (size_t)k * KS, v);
             dzv = it_rd(k, IT::DZ);
         };
-        float ra[RS], rb[RS], da, db;
+        float ra[RS], rb[RS], da, db;  // (two rounds ahead measured slower: profiles/r05/ab/spar_prefetch.txt)
         load(0, ra, da);
         for (int j = 0;; j += 2) {
             load(j + 1 < NR ? j + 1 : NR - 1, rb, db);
