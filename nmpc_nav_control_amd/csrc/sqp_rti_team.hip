@@ -800,6 +800,13 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a)
                 } else {
                     mrow_pg_block<NX, NU>(Lr, pivot, pg, Gd);  // the row form (NX x NV broadcast FMAs)
                     STAMPF(4);
+#ifdef NMPC_ROW_PIV2
+                    if constexpr (NU == 2) {  // A/B: both input pivots up front with the row form too
+                        const double m11 = bc64<1>(Lr[1]), m10 = bc64<1>(Lr[0]);
+                        chol_input_2<NX>(Lr, pivot, m11, m10, r, fail);
+                        seq_pivots = false;
+                    }
+#endif
                 }
                 if (seq_pivots) sfor<0, NU>([&](auto jc) {
                     constexpr int j = decltype(jc)::value;
