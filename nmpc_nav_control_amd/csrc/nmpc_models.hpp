@@ -55,9 +55,10 @@ struct Diff2 {
     // rows >= NGV of the discrete Jacobian [B A] do not depend on the state or input (theta, wheel and
     // ref rows are linear): they are computed once per launch (checked by tests/test_oracle.py)
     static constexpr int NGV = 2;
-    // team kernel M block: the row form (NX x NV broadcast FMAs); the column form measured 1.5 % slower on the
-    // metric config (profiles/r05/ab/mcol.txt)
-    static constexpr bool kMcolForm = false;
+    // team kernel M block: the column form, with the input pivots one after the other (up front they cost the
+    // metric config 4.4 %: profiles/r05/ab/mcol_pivots.txt)
+    static constexpr bool kMcolForm = true;
+    static constexpr bool kPivotsUpFront = false;
     // constant rows th, vl, vr, vl_ref, vr_ref over columns [dvl_ref dvr_ref | x y th vl vr vl_ref vr_ref]
     __host__ __device__ static constexpr unsigned gmask(int i)
     {
@@ -120,6 +121,7 @@ struct Omni4 {
     static constexpr int ID = kOmni4, NX = 11, NU = 4, NBX = 4, NBU = 4, NP = 2, NY = 15;
     static constexpr int NGV = 2;  // x, y rows vary; theta / wheel / ref rows are linear
     static constexpr bool kMcolForm = true;  // column-form M block: +6 % (profiles/r05/ab/mcol.txt)
+    static constexpr bool kPivotsUpFront = false;  // (NU = 4: chol_input_2 is for two inputs)
     // constant rows th, v1..v4, v1_ref..v4_ref over columns [dv1_ref..dv4_ref | x y th v1..v4 v1_ref..v4_ref]
     __host__ __device__ static constexpr unsigned gmask(int i)
     {
@@ -191,6 +193,7 @@ struct Tric3 {
     static constexpr int ID = kTric, NX = 7, NU = 2, NBX = 2, NBU = 2, NP = 3, NY = 9;
     static constexpr int NGV = 3;  // x, y, theta rows vary; v / alpha / ref rows are linear
     static constexpr bool kMcolForm = true;  // column-form M block: +5 % (profiles/r05/ab/mcol.txt)
+    static constexpr bool kPivotsUpFront = true;  // both input pivots from the 2 x 2 block: +1.2 % (mcol_pivots.txt)
     // constant rows v, alpha, v_ref, alpha_ref over columns [dv_ref dalpha_ref | x y th v alpha v_ref alpha_ref]
     __host__ __device__ static constexpr unsigned gmask(int i)
     {

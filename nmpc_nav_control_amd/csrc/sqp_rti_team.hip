@@ -578,6 +578,8 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a)
     for (int i = 0; i < NX; i++) gcol64[i] = (double)gcol[i];
 #ifdef NMPC_MROW
     constexpr bool kMcol = false;  // A/B: the row form for every model
+#elif defined(NMPC_MCOL_ALL)
+    constexpr bool kMcol = true;  // A/B: the column form for every model
 #else
     constexpr bool kMcol = M::kMcolForm;  // per model (nmpc_models.hpp)
 #endif
@@ -791,12 +793,18 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a)
                     double m11, m10;
                     m_block<M>(Lr, pivot, m11, m10, pg, Gd, gcs);  // column form: uniform constant rows + 3 broadcast rows
                     STAMPF(4);
-#ifndef NMPC_SEQ_PIVOTS
-                    if constexpr (NU == 2) {
+#ifdef NMPC_SEQ_PIVOTS
+                    constexpr bool kPiv2 = false;  // A/B: the pivots one after the other for every model
+#else
+                    constexpr bool kPiv2 = M::kPivotsUpFront;
+#endif
+                    if constexpr (NU == 2 && kPiv2) {
                         chol_input_2<NX>(Lr, pivot, m11, m10, r, fail);  // both pivots up front
                         seq_pivots = false;
+                    } else {
+                        (void)m11;
+                        (void)m10;
                     }
-#endif
                 } else {
                     mrow_pg_block<NX, NU>(Lr, pivot, pg, Gd);  // the row form (NX x NV broadcast FMAs)
                     STAMPF(4);
