@@ -40,6 +40,14 @@ int ocp_nlp_constraints_model_set(ocp_nlp_config* config, ocp_nlp_dims* dims, oc
 /* fields: "W" (col-major NY x NY at stages < N, NYN x NYN at N; must be diagonal), "yref" (NY / NYN). */
 int ocp_nlp_cost_model_set(ocp_nlp_config* config, ocp_nlp_dims* dims, ocp_nlp_in* in, int stage,
                            const char* field, void* value);
+/* Read back what the setters above stored (acados' ocp_nlp_constraints_model_get / ocp_nlp_cost_model_get):
+ * the same fields and sizes ("W" as the full col-major block). Returns 0, or < 0 on a bad field or stage. Not
+ * called by the reference's wrappers; tests/test_reference_wrappers.py reads the x0, yref and W_e the
+ * reference's own run() set (NMPCNavControlDiff.cpp:96-139) through them. */
+int ocp_nlp_constraints_model_get(ocp_nlp_config* config, ocp_nlp_dims* dims, ocp_nlp_in* in, int stage,
+                                  const char* field, void* value);
+int ocp_nlp_cost_model_get(ocp_nlp_config* config, ocp_nlp_dims* dims, ocp_nlp_in* in, int stage,
+                           const char* field, void* value);
 /* fields: "x" (NX doubles), "u" (NU doubles) of the current iterate. */
 void ocp_nlp_out_get(ocp_nlp_config* config, ocp_nlp_dims* dims, ocp_nlp_out* out, int stage, const char* field,
                      void* value);

@@ -187,7 +187,12 @@ int nmpc_batch_forget_warm(nmpc_batch* b, int B, const unsigned char* mask, void
  * the record layout its multipliers were stored in (NMPC_WARM_TAG_*): a solve reads them only when its launch uses
  * the same layout, so a robot whose launches change kernel or layout (e.g. a handle whose batch crosses the
  * row-parallel kernel's limit) starts cold on its own, and no other robot is touched. With nmpc_batch_state this
- * is everything a solve reads from the handle, e.g. to checkpoint a fleet or to replay a tick bit for bit. */
+ * is everything a solve reads from the handle, e.g. to checkpoint a fleet or to replay a tick bit for bit.
+ * Checkpoints of this state are tied to the library version that wrote them: before round 5 a flag of 1 meant
+ * "succeeded", whatever the layout, and now reads as NMPC_WARM_TAG_WIDE (a tric team-kernel record written then
+ * was split-layout). After restoring a warm state saved by an older build, call nmpc_batch_forget_warm on the
+ * restored robots: their first solve then starts cold (wrong warm multipliers would only be clamped, costing
+ * IPM iterations, never a wrong solution). */
 #define NMPC_WARM_TAG_WIDE 1     /* single-direction field order, one record per lane (team / row-parallel) */
 #define NMPC_WARM_TAG_SPLIT 2    /* the team kernel's split core / bound planes */
 #define NMPC_WARM_TAG_MEHROTRA 3 /* the Mehrotra rule's field order (NMPC_IPM_MEHROTRA) */

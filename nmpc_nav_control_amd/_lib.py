@@ -92,8 +92,9 @@ REC_LAYOUTS = {"auto": -1, "wide": 0, "split": 1}
 PLAN_MODES = {"solve": 0, "run": 1, "run_path": 2}
 WARM_TAGS = {1: "wide", 2: "split", 3: "mehrotra"}
 SCHEDULES = {"off": 0, "auto": 1, "sorted": 2, "interleaved": 3, "spread": 4}
-NLP_SYMBOLS = ["ocp_nlp_constraints_model_set", "ocp_nlp_cost_model_set", "ocp_nlp_out_get", "ocp_nlp_out_set",
-               "ocp_nlp_get", "ocp_nlp_solver_opts_set", "ocp_nlp_dims_get_from_attr"]
+NLP_SYMBOLS = ["ocp_nlp_constraints_model_set", "ocp_nlp_cost_model_set", "ocp_nlp_constraints_model_get",
+               "ocp_nlp_cost_model_get", "ocp_nlp_out_get", "ocp_nlp_out_set", "ocp_nlp_get", "ocp_nlp_solver_opts_set",
+               "ocp_nlp_dims_get_from_attr"]
 CAPSULE_SUFFIXES = ["create_capsule", "free_capsule", "create", "create_with_discretization", "reset",
                     "update_params", "solve", "batch_solve", "free", "print_stats", "get_nlp_in", "get_nlp_out",
                     "get_nlp_solver", "get_nlp_config", "get_nlp_opts", "get_nlp_dims"]

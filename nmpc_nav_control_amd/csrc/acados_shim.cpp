@@ -148,8 +148,9 @@ void codegen_defaults(nmpc_capsule_impl* c, const nmpc_codegen_desc& d)
     // mean count (kappa 0.01; the batch default for diff, 0.2, is tuned for the slowest robot of a fleet)
     c->prm.qp_warm_kappa = 0.01;
     // acados' default, which the reference's OCP keeps (scripts/diff/generate_c_code.py:68-74 sets no
-    // qp_warm_start): HPIPM starts every QP cold. ocp_nlp_solver_opts_set(.., "qp_warm_start", 1) opts in to the
-    // capsule's multiplier warm start (INTEGRATION.md "Capsule semantics")
+    // qp_warm_start): HPIPM starts every QP cold. ocp_nlp_solver_opts_set(.., "qp_warm_start", 2) opts in to the
+    // capsule's multiplier warm start (INTEGRATION.md "Capsule semantics"; 1, acados' primal-only warm start, starts
+    // cold here)
     c->prm.qp_warm_start = 0;
     // HPIPM has no infeasibility exit: a hard QP runs to qp_iter_max and acados' RTI accepts the result
     // (SURVEY Appendix B.6), so the drop-in never turns a stiff but feasible QP into the wrapper's exception
@@ -589,6 +590,52 @@ int ocp_nlp_cost_model_set(ocp_nlp_config* config, ocp_nlp_dims* dims, ocp_nlp_i
     return -1;
 }
 
+int ocp_nlp_constraints_model_get(ocp_nlp_config* config, ocp_nlp_dims* dims, ocp_nlp_in* in, int stage,
+                                  const char* field, void* value)
+{
+    (void)config; (void)dims;
+    nmpc_capsule_impl* c = in ? impl_of(in->impl) : nullptr;
+    if (!c || !c->created || !field || !value) return -1;
+    if (!stage_ok(c, stage, "ocp_nlp_constraints_model_get", field)) return -1;
+    double* v = static_cast<double*>(value);
+    const int nx = c->nx;
+    if (!std::strcmp(field, "lbx") || !std::strcmp(field, "ubx")) {
+        const std::vector<double>& src = (field[0] == 'l') ? c->lbx : c->ubx;
+        const int n = (stage == 0) ? nx : c->nbx;
+        for (int i = 0; i < n; i++) v[i] = src[(size_t)stage * nx + i];
+        return 0;
+    }
+    if ((!std::strcmp(field, "lbu") || !std::strcmp(field, "ubu")) && stage < c->N) {
+        const std::vector<double>& src = (field[0] == 'l') ? c->lbu : c->ubu;
+        for (int i = 0; i < c->nbu; i++) v[i] = src[(size_t)stage * c->nbu + i];
+        return 0;
+    }
+    log_err("ocp_nlp_constraints_model_get", std::string("unsupported field ") + field);
+    return -1;
+}
+
+int ocp_nlp_cost_model_get(ocp_nlp_config* config, ocp_nlp_dims* dims, ocp_nlp_in* in, int stage,
+                           const char* field, void* value)
+{
+    (void)config; (void)dims;
+    nmpc_capsule_impl* c = in ? impl_of(in->impl) : nullptr;
+    if (!c || !c->created || !field || !value) return -1;
+    if (!stage_ok(c, stage, "ocp_nlp_cost_model_get", field)) return -1;
+    double* v = static_cast<double*>(value);
+    const int n = (stage == c->N) ? c->nx : c->ny;
+    if (!std::strcmp(field, "W")) {
+        const double* W = c->W.data() + (size_t)stage * c->ny * c->ny;
+        for (int i = 0; i < n * n; i++) v[i] = W[i];
+        return 0;
+    }
+    if (!std::strcmp(field, "yref")) {
+        for (int i = 0; i < n; i++) v[i] = c->yref[(size_t)stage * c->ny + i];
+        return 0;
+    }
+    log_err("ocp_nlp_cost_model_get", std::string("unsupported field ") + field);
+    return -1;
+}
+
 void ocp_nlp_out_get(ocp_nlp_config* config, ocp_nlp_dims* dims, ocp_nlp_out* out, int stage, const char* field,
                      void* value)
 {
@@ -647,6 +694,10 @@ void ocp_nlp_solver_opts_set(ocp_nlp_config* config, void* opts_, const char* fi
         // warm start), so 0 and 1 both start cold and only 2 warm-starts the bound multipliers
         c->prm.qp_warm_start = (v == 2) ? 1 : 0;
         if (v != 2) c->warm_ok = false;
+        static std::atomic<bool> told{false};
+        if (v == 1 && !told.exchange(true))  // until round 5, 1 selected the multiplier warm start
+            log_err("ocp_nlp_solver_opts_set", "qp_warm_start 1 (primal only) starts the QP cold here; 2 warm-starts "
+                                               "the bound multipliers");
     } else if (!std::strcmp(field, "qp_iter_max") && v >= 1) {
         c->prm.qp_iter_max = v;
     } else {

@@ -26,6 +26,8 @@ struct nmpc_batch {
     float* scratch = nullptr;
     int sched = NMPC_SCHED_AUTO;
     int n_simd = 1024;           // SIMDs of the device (4 per CU)
+    int n_cu = 256;              // CUs of the device and LDS bytes per CU (MI355X: 256, 160 KiB; read at create)
+    size_t lds_per_cu = 163840;
     int split_max = 256;         // team-kernel launches of at most this many robots run one block per robot (split)
     // launches of at most this many robots (single-direction IPM, not run_path) run k_sqp_rti_rowpar (DESIGN.md
     // section 4): four waves per robot up to 256 robots; above, rowpar_w waves per robot and there only with
@@ -163,8 +165,6 @@ inline int seg_count(int N, int rows)
     return best;
 }
 
-// LDS a row-parallel launch of B robots may give each block: the CU's 160 KiB shared by the ceil(B / 256) robots
-// each CU holds (one block per robot on 256 CUs), so that every robot of the launch is resident at once
 // waves per robot of a row-parallel launch of B robots (eight waves per robot up to 64 robots measured no faster:
 // the one-robot phases are chains, not rounds; profiles/r05/ab/w8_rowchol2.txt)
 inline int rowpar_waves(const nmpc_batch* b, int B)
@@ -172,10 +172,14 @@ inline int rowpar_waves(const nmpc_batch* b, int B)
     return B <= 256 ? 4 : b->rowpar_w;
 }
 
-inline size_t rowpar_lds_cap(int B)
+// LDS a row-parallel launch of B robots may give each block: one CU's LDS shared by the ceil(B / CUs) robots each
+// CU holds (one block per robot), so that every robot of the launch is resident at once. The CU count and the LDS
+// per CU are the device's (hipDeviceProp_t at create: a CU-partitioned GPU has fewer CUs)
+inline size_t rowpar_lds_cap(const nmpc_batch* b, int B)
 {
-    const int per_cu = (B + 255) / 256;
-    return (size_t)163840 / (size_t)(per_cu > 0 ? per_cu : 1);
+    const int n_cu = b->n_cu > 0 ? b->n_cu : 1;
+    const int per_cu = (B + n_cu - 1) / n_cu;
+    return b->lds_per_cu / (size_t)(per_cu > 0 ? per_cu : 1);
 }
 
 template <class M>
@@ -183,7 +187,7 @@ bool rowpar_ok(const nmpc_batch* b, KArgs& a, int mode)
 {
     if (b->kp.ipm != NMPC_IPM_SINGLE || a.segs || a.B > b->rowpar_max) return false;
     const int rows = a.B <= 256 ? 16 : b->seg_rows;  // segments: any row up to 256 robots, the first wave's above
-    const size_t cap = rowpar_lds_cap(a.B);
+    const size_t cap = rowpar_lds_cap(b, a.B);
     int S = b->seg >= 0 ? b->seg : seg_count(b->prm.N, rows);
     if (S > rows || S > kSegMax || (S > 0 && b->prm.N % S)) S = 0;
     if (S > 0 && rowpar_lds_bytes<M>(b->prm.N, mode, S) > cap) S = 0;
@@ -504,8 +508,11 @@ int nmpc_batch_create(const nmpc_model_params* prm, int capacity, nmpc_batch** o
     int dev = 0;
     hipDeviceProp_t props;
     if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&props, dev) == hipSuccess &&
-        props.multiProcessorCount > 0)
+        props.multiProcessorCount > 0) {
         b->n_simd = 4 * props.multiProcessorCount;
+        b->n_cu = props.multiProcessorCount;
+        if (props.maxSharedMemoryPerMultiProcessor > 0) b->lds_per_cu = props.maxSharedMemoryPerMultiProcessor;
+    }
 #ifdef NMPC_HYBRID
     if ((e = hipMalloc(&b->hyb_n, sizeof(int))) != hipSuccess || (e = hipMemset(b->hyb_n, 0, sizeof(int))) != hipSuccess) {
         nmpc_batch_destroy(b);

@@ -14,6 +14,11 @@
 namespace nmpc {
 
 // Uniform (per-launch) parameters: model parameters, bounds, stage weights, QP options.
+// INVARIANT the team kernel relies on: dt and the model parameters p are the same for every robot of a launch, so the
+// state-independent rows of [B A] (rows >= NGV of each model, Model::gmask) are bit-identical for every robot; the
+// column-form M block (gconst_load, team_common.hpp) reads them from each wave's first team and applies them to all
+// four. Per-robot model parameters would break this and need the row form (-DNMPC_MROW) or per-team constants;
+// tests/test_gpu_split.py::test_constant_rows_per_launch checks the column form against that build.
 struct KParams {
     int N;
     float dt, dt_ctrl;

@@ -527,8 +527,9 @@ __global__ __launch_bounds__(64 * W, (SEG && M::NX < 10) ? 2 : 1) void k_sqp_rti
     }
 
 #ifdef NMPC_ROWPAR_MCOL
-    // A/B only: the column-form M block needs 20 more registers, which pushes the segmented kernels past the 256
-    // that two waves per SIMD allow (diff 250 -> 256 + 14 AGPRs; tests/test_reg_usage.py), so the row form stays
+    // A/B only: the column-form M block needs about 20 more registers, which pushes the segmented kernels past the
+    // 256 that two waves per SIMD allow (tests/test_reg_usage.py), so the row form stays; tests/test_codegen.py
+    // compiles this variant so that it keeps building
     GConst<M> gcs;  // the constant rows of [B A] as uniform operands of the M block (m_block)
     gconst_load<M>(gcs, gcol);
 #endif
@@ -796,7 +797,10 @@ __global__ __launch_bounds__(64 * W, (SEG && M::NX < 10) ? 2 : 1) void k_sqp_rti
                     for (int jj = 0; jj < NV; jj++) Lr[jj] = (r == jj) ? dg : 0.0;
                     double pivot;
 #ifdef NMPC_ROWPAR_MCOL
-                    m_block<M>(Lr, pivot, pg, Gd, gcs);
+                    double m11, m10;  // the 2x2 input block for up-front pivots (unused: pivots in turn below)
+                    m_block<M>(Lr, pivot, m11, m10, pg, Gd, gcs);
+                    (void)m11;
+                    (void)m10;
 #else
                     mrow_pg_block<NX, NU>(Lr, pivot, pg, Gd);
 #endif
@@ -1178,7 +1182,10 @@ __global__ __launch_bounds__(64 * W, (SEG && M::NX < 10) ? 2 : 1) void k_sqp_rti
                         for (int j = 0; j < NV; j++) Lr[j] = (r == j) ? dg : 0.0;
                         double pivot;
 #ifdef NMPC_ROWPAR_MCOL
-                        m_block<M>(Lr, pivot, pg, Gd, gcs);
+                        double m11, m10;  // unused: pivots in turn below
+                        m_block<M>(Lr, pivot, m11, m10, pg, Gd, gcs);
+                        (void)m11;
+                        (void)m10;
 #else
                         mrow_pg_block<NX, NU>(Lr, pivot, pg, Gd);
 #endif

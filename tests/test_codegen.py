@@ -185,3 +185,27 @@ def test_team_asm_header_is_generated():
     spec.loader.exec_module(gen)
     with open(gen.OUT) as fh:
         assert fh.read() == gen.generate(), "team_asm_gen.hpp differs from tools/gen_team_asm.py: regenerate it"
+
+
+# A/B-only build options (each decided by a same-box A/B run) keep compiling: the product library leaves
+# them out, so nothing else would notice when a change of the shared blocks breaks one (the
+# -DNMPC_ROWPAR_MCOL call of m_block had kept an old signature). Syntax and template instantiation only (-fsyntax-only,
+# device and host), a few seconds each.
+AB_VARIANTS = [("sqp_rti_rowpar.hip", "-DNMPC_ROWPAR_MCOL"), ("sqp_rti_rowpar.hip", "-DNMPC_SEQ_MASTER"),
+               ("sqp_rti_rowpar.hip", "-DNMPC_STAMPS"), ("sqp_rti_team.hip", "-DNMPC_MROW"),
+               ("sqp_rti_team.hip", "-DNMPC_MCOL_ALL"), ("sqp_rti_team.hip", "-DNMPC_SEQ_PIVOTS"),
+               ("sqp_rti_team.hip", "-DNMPC_ROW_PIV2"), ("sqp_rti_team.hip", "-DNMPC_STAMPS"),
+               ("sqp_rti_team.hip", "-DP1_MASKED_STORE"), ("sqp_rti_team.hip", "-DNMPC_REC_FULL"),
+               ("sqp_rti_team.hip", "-DNMPC_RSS_FULL"), ("sqp_rti_team.hip", "-DNMPC_HYBRID"),
+               ("sqp_rti_rowpar.hip", "-DNMPC_HYBRID"), ("nmpc_batch.cpp", "-DNMPC_HYBRID")]
+
+
+@pytest.mark.parametrize("src,flag", AB_VARIANTS, ids=[f"{s.split('.')[0]}{f[2:].lower()}" for s, f in AB_VARIANTS])
+def test_ab_variant_compiles(src, flag):
+    csrc = os.path.join(ROOT, "nmpc_nav_control_amd", "csrc")
+    cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-std=c++17", "-fsyntax-only", "-Wno-unused-command-line-argument",
+           "-I", os.path.join(ROOT, "include"), "-I", csrc, flag]
+    if src.endswith(".cpp"):
+        cmd += ["-x", "hip"]
+    r = subprocess.run(cmd + [os.path.join(csrc, src)], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-4000:]

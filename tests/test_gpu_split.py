@@ -207,3 +207,43 @@ def test_rowpar_run_matches_team(built, monkeypatch):
             assert close(ca[:, :B], cb[:, :B]) <= TOL_RP, (tick, j)
         # the two team layouts: the same arithmetic on differently placed records, bit for bit
         assert torch.equal(res[1]["u0"], res[2]["u0"]) and torch.equal(res[1]["cmd"], res[2]["cmd"]), tick
+
+
+# ---- the column-form M block's per-launch constant rows ------------------------------------------------
+# gconst_load (team_common.hpp) takes the state-independent rows of [B A] (rows >= NGV: the theta, wheel and
+# reference rows, functions of dt and the model parameters only, which are per launch: KParams) from the lanes of
+# each wave's FIRST team and uses them for all four teams of the wave. The checker build lib/mrow/ (Makefile: the row
+# form for every model, every row read from the robot's own lanes) solves the same fleet; robots in different
+# states in every wave must give the product's results to fp32 rounding.
+
+@pytest.mark.parametrize("model", ["diff", "omni4", "tric"])
+def test_constant_rows_per_launch(built, tmp_path, model):
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    mrow = os.path.join(root, "nmpc_nav_control_amd", "lib", "mrow", "libnmpc_amd.so")
+    assert os.path.exists(mrow), "lib/mrow/libnmpc_amd.so is built by the csrc Makefile (all)"
+    N, B = 40, 64
+    layout = "split" if model == "tric" else "wide"
+    outs = {}
+    for name, lib in (("product", None), ("mrow", mrow)):
+        env = dict(os.environ)
+        env.pop("NMPC_AMD_LIB", None)
+        if lib:
+            env["NMPC_AMD_LIB"] = lib
+        out = str(tmp_path / f"{name}.npz")
+        r = subprocess.run([sys.executable, os.path.join(root, "tests", "team_probe.py"), model, str(N), str(B), "6",
+                            layout, out], env=env, capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stderr[-3000:]
+        outs[name] = np.load(out)
+    a, b = outs["product"], outs["mrow"]
+    assert str(b["lib"]).endswith("mrow/libnmpc_amd.so")
+    assert (a["status"] == 0).all() and (b["status"] == 0).all()
+    # robots in different states share each wave (the oracle closed loop's fleet after 6 ticks)
+    x0 = a["xtraj"][:3]
+    assert np.unique(np.round(x0, 3), axis=1).shape[1] == B
+    du = float(np.abs(a["utraj"] - b["utraj"]).max())
+    dx = float(np.abs(a["xtraj"] - b["xtraj"]).max())
+    print(f"{model}: column form vs row form: u {du:.2e} x {dx:.2e}")
+    assert du <= 3e-4 and dx <= 3e-4, (du, dx)

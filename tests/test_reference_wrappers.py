@@ -17,6 +17,7 @@ destroys it: host-only capsule code, so it runs here and must log no shim error.
 import os
 import subprocess
 
+import numpy as np
 import pytest
 
 from nmpc_nav_control_amd import _lib
@@ -105,3 +106,44 @@ def test_reference_wrappers_compile_link_and_construct(built, tmp_path):
     # the shipped codegen yaml bakes N = ceil(2.0 s * 40 Hz) = 80 for all three models (scripts/*/common.py:5-9)
     assert r.stdout.split() == ["80", "80", "80", "1", "1", "1"], r.stdout
     assert "[nmpc_amd]" not in r.stderr, r.stderr
+
+
+# ---- the reference's run() executed: oracle/ref_driver.cpp ------------------------------------
+
+@pytest.fixture(scope="module")
+def ref_driver(built):
+    """oracle/_ref/ref_wrappers_{oracle,device}: the reference's wrappers compiled in place (build() makes them)."""
+    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "ref"], check=True)
+    return True
+
+
+@pytest.mark.parametrize("model", ["diff", "omni4", "tric"])
+def test_reference_run_matches_the_oracle_restatement(ref_driver, model):
+    """The reference's own run() (NMPCNavControl{Diff,Omni4,Tric}.cpp:82-175 / :96-174 / :93-178), with the fp64
+    oracle as its solver, over closed-loop ticks and the edge cases of tests/ref_wrappers.py: everything it sets
+    before the solve (x0, yref of every stage, W_e), the iterate the solve starts from, the solve, and the command and
+    carried references after it equal the oracle's restatement (oc_prepare, oc_sqp_rti, oc_post) bit for bit."""
+    import ref_wrappers as rw
+    o = rw.oracle(model)
+    robots = rw.closed_loop_robots(o, robots=3, ticks=12) + rw.edge_robots(o)
+    recs, stderr = rw.run_driver("oracle", o, robots)
+    assert "[nmpc_amd]" not in stderr, stderr
+    for seq, rc in zip(robots, recs):
+        rw.check_robot(o, seq, rc)
+    # the branches were taken: padded lists, the diff hack both ways, +-pi unwraps
+    We_scale = {rc["We"][0] / o.prm.W[0] for r in recs for rc in r}
+    assert (We_scale == {1.0, 100.0}) if model == "diff" else (We_scale == {1.0}), We_scale
+    th = np.concatenate([rc["yref"].reshape(rw.N + 1, o.ny)[:, 2] for r in recs for rc in r])
+    assert th.max() > np.pi and th.min() < -np.pi, (th.min(), th.max())
+
+
+def test_reference_run_detects_a_changed_restatement(ref_driver):
+    """The bit-for-bit check is sharp: a one-ulp change of the oracle's control time step (oc_post's carry
+    x_ref + u0 dt) is caught in the command."""
+    import ref_wrappers as rw
+    o = rw.oracle("diff")
+    robots = rw.closed_loop_robots(o, robots=1, ticks=3)
+    recs, _ = rw.run_driver("oracle", o, robots)
+    o.prm.dt_ctrl = np.nextafter(o.prm.dt_ctrl, 1.0)
+    with pytest.raises(AssertionError):
+        rw.check_robot(o, robots[0], recs[0])

@@ -34,9 +34,13 @@ def main():
     for t in range(dump):
         torch.cuda.synchronize()
         sn = f.snapshot()
-        rec = sv.to_tensor()[0, :B * (N + 1) * 16 * RS].reshape(B, N + 1, 16, RS)
-        keep[f"t{t}_lam"] = rec[:, :, :nv, LL:LL + 2].cpu().numpy()
-        keep[f"t{t}_warm"] = wv.to_tensor()[0, :B].cpu().numpy()
+        if f.solver.plan_ex(B)["record_layout"] == "wide":
+            rec = sv.to_tensor()[0, :B * (N + 1) * 16 * RS].reshape(B, N + 1, 16, RS)
+            keep[f"t{t}_lam"] = rec[:, :, :nv, LL:LL + 2].cpu().numpy()
+            keep[f"t{t}_warm"] = wv.to_tensor()[0, :B].cpu().numpy()
+        else:  # split record planes (tric): no multipliers dumped, every robot replayed cold
+            keep[f"t{t}_lam"] = np.zeros((B, N + 1, nv, 2), np.float32)
+            keep[f"t{t}_warm"] = np.zeros(B, np.uint8)
         f.solve()
         torch.cuda.synchronize()
         keep[f"t{t}_gpu_iter"] = f.qp_iter.cpu().numpy()
