@@ -583,8 +583,23 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a)
 #else
     constexpr bool kMcol = M::kMcolForm;  // per model (nmpc_models.hpp)
 #endif
+    // -DNMPC_F32_FACTOR (A/B build): the single-direction rule factors in fp32 with the bounded states' barrier
+    // weights split off (team_common.hpp chol_split_f32). As accurate as the fp64 factor (same IPM counts in the
+    // closed loop, every full-batch replay green) but slower on every config, 3-10 % (profiles/r06/ab/fp32_factor.txt,
+    // DESIGN.md section 5), so the product keeps the fp64 factorisation
+#ifdef NMPC_F32_FACTOR
+    constexpr bool kF32 = SD && kMcol;
+#else
+    constexpr bool kF32 = false;
+#endif
+    using FT = std::conditional_t<kF32, float, double>;
     GConst<M> gcs;  // the constant rows of [B A] as uniform operands of the column-form M block (m_block)
-    if constexpr (kMcol) gconst_load<M>(gcs, gcol);
+    GConstF<M> gcf;  // the same in fp32 (m_block_f32, chol_split_f32)
+    if constexpr (kF32) gconst_load_f<M>(gcf, gcol);
+    else if constexpr (kMcol) gconst_load<M>(gcs, gcol);
+    // fp32 factor: a bounded state's barrier weight stays out of P_k (lane NU + idxbx(c), c = cx); s_next carries it
+    // from stage k's body to stage k - 1's pivot of input c
+    const bool split_lane = kF32 && is_x && cx >= 0;
 
     STAMP(1);
     // infeasibility threshold of this robot: qp_infeas_lambda scaled by its largest weight (terminal hack included)
@@ -688,9 +703,10 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a)
     for (int it = 0;; it++) {
         // P1 (backward): apply the previous step, residuals, adjoint, fp64 classic Riccati factorisation,
         // predictor rhs
-        double Lrow[NV];  // lane NU+i: row i of P_{k+1} (the state block of the previous stage's M after its pivots)
+        FT Lrow[NV];  // lane NU+i: row i of P_{k+1} (the state block of the previous stage's M after its pivots)
 #pragma unroll
         for (int j = 0; j < NV; j++) Lrow[j] = 0.0;
+        float s_next = 0.0f;  // fp32 factor: the split lane's barrier weight of stage k + 1 (0 elsewhere)
         float pv = 0.0f, piv = 0.0f;
         float res_stat = 0.0f, res_ineq = 0.0f, sum_c = 0.0f, max_c = 0.0f, stat_scale = 1.0f, nanf_ = 0.0f;
         float lam_max = 0.0f;
@@ -764,11 +780,47 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a)
             const float pi_new = vx ? base : 0.0f;
             if (ghat != ghat || sig != sig) nanf_ = 1.0f;
             if (k == N) {
-                // terminal: P_N = diag(W_e + Sigma) on the state lanes
-                const double d = is_x ? (double)fmaxf(we_lane + sig, 0.0f) : 0.0;
+                // terminal: P_N = diag(W_e + Sigma) on the state lanes (fp32 factor: Sigma of a bounded state in
+                // s_next instead)
+                const FT d = is_x ? (FT)fmaxf(we_lane + (split_lane ? 0.0f : sig), 0.0f) : (FT)0.0;
 #pragma unroll
-                for (int j = 0; j < NV; j++) Lrow[j] = (is_x && j == r) ? d : 0.0;
+                for (int j = 0; j < NV; j++) Lrow[j] = (is_x && j == r) ? d : (FT)0.0;
+                s_next = split_lane ? sig : 0.0f;
                 pv = is_x ? ghat : 0.0f;
+            } else if constexpr (kF32) {
+                // fp32 split-sigma factorisation: M~ = D~ + G' P~ G with the bounded states' barrier weights out of
+                // D~ and P~ (team_common.hpp chol_split_f32 enters those of stage k + 1 at their inputs' pivots)
+                float pg[NX];
+#pragma unroll
+                for (int i = 0; i < NX; i++) pg[i] = 0.0f;
+                STAMPF(2);
+                pg_block_f<NX, NU>(pg, Lrow, Gc);
+                STAMPF(3);
+                const float dg = valid ? h_stage + (split_lane ? 0.0f : sig) : 1.0f;
+                float Lr[NV];
+#pragma unroll
+                for (int j = 0; j < NV; j++) Lr[j] = (j == r) ? dg : 0.0f;
+                float pivot;  // = M[0][0]
+                m_block_f<M>(Lr, pivot, pg, Gc, gcf);
+                STAMPF(4);
+                chol_split_f32<M>(Lr, pivot, s_next, gcf, r, fail);
+                s_next = (split_lane && vx) ? sig : 0.0f;
+                STAMPF(5);
+#pragma unroll
+                for (int q = 0; q < NU; q++) rc[R::LM + q] = Lr[q];
+                // rhs: w = g^ + G' p_{k+1}; forward substitution over the input block (fp32)
+                float y = dot_x<NX, NU>(ghat, pv, Gc);
+                float my_lr = 0.0f;
+                sfor<0, NU>([&](auto jc) {
+                    constexpr int j = decltype(jc)::value;
+                    const float lrj = bc<j>(y * frcp(Lr[j]));  // (y_j / L_jj) from lane j
+                    if (r == j) my_lr = lrj;
+                    y -= Lr[j] * lrj;
+                });
+                rc[R::LR] = my_lr;
+                pv = is_x ? y : 0.0f;
+#pragma unroll
+                for (int j = 0; j < NV; j++) Lrow[j] = Lr[j];
             } else {
                 double Gd[NX];
 #pragma unroll

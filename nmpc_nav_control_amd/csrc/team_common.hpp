@@ -182,6 +182,104 @@ __device__ __forceinline__ void m_block(double (&Lr)[M::NX + M::NU], double& piv
     }
 }
 
+// ---- fp32 split-sigma factorisation (single-direction team kernel) ---------------------------
+// The fp64 factor above exists because a bounded state's barrier weight s (up to ~1e12 near the solution) enters
+// P_{k+1} and cancels in the Schur complement P_k = Qxx - Qxu Quu^-1 Qux, which fp32 cannot hold. Every bounded state
+// of the three models is a reference integrator: row idxbx(c) of [B A] is g = h e_{u_c} + gam e_{x_idxbx(c)} (h = dt,
+// gam = 1; static_assert below), so s enters stage k as s g g'. Kept out of P (P = P~ + sum_c s_c e e'), it is added
+// at the pivot of input c -- the pivot gets h^2 s, entry (x, u_c) h gam s -- and the one Schur update that cancels s,
+// the diagonal (x, x), is evaluated in closed form from the s-free entries a = M[c][c], b = M[x][c], e = M[x][x]:
+//     e + gam^2 s - (b + h gam s)^2 / (a + h^2 s) = [s (gam^2 a - 2 h gam b + h^2 e) + (a e - b^2)] / (a + h^2 s)
+// (exact algebra, no s - s). tools/fp32_factor_study.py (variant splitsig) on 12288 dumped metric QPs:
+// profiles/r06/ab/fp32_factor_study_metric.txt; the same recursion fully in fp32 leaves u0 errors up to 1.2e-3.
+template <class M>
+struct GConstF {
+    float v[M::NX][M::NX + M::NU];
+};
+template <class M>
+__device__ __forceinline__ void gconst_load_f(GConstF<M>& gc, const float (&gcol)[M::NX])
+{
+    constexpr int NX = M::NX, NV = M::NX + M::NU;
+    sfor<mcol_nbc<M>(), NX>([&](auto ic) {
+        constexpr int i = decltype(ic)::value;
+        sfor<0, NV>([&](auto rc) {
+            constexpr int r = decltype(rc)::value;
+            if constexpr ((M::gmask(i) >> r) & 1u)
+                gc.v[i][r] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(gcol[i]), r));
+            else
+                gc.v[i][r] = 0.0f;
+        });
+    });
+}
+template <int NX, int NU>
+__device__ __forceinline__ void pg_block_f(float (&acc)[NX], const float (&prow)[NX + NU], const float (&gd)[NX])
+{
+    if constexpr (NX == 7 && NU == 2) pg_block_f32_7_2(acc, prow, gd);
+    else pg_block_f32_11_4(acc, prow, gd);
+}
+// m_block in fp32 (column form; pivot = M[0][0])
+template <class M>
+__device__ __forceinline__ void m_block_f(float (&Lr)[M::NX + M::NU], float& pivot, const float (&pg)[M::NX],
+                                          const float (&gd)[M::NX], const GConstF<M>& gc)
+{
+    constexpr int NX = M::NX, NU = M::NU, NV = NX + NU;
+    static_assert(mcol_nbc<M>() == 3, "generated broadcast blocks cover three rows");
+    sfor<mcol_nbc<M>(), NX>([&](auto ic) {
+        constexpr int i = decltype(ic)::value;
+        sfor<0, NV>([&](auto rc) {
+            constexpr int r = decltype(rc)::value;
+            if constexpr ((M::gmask(i) >> r) & 1u) Lr[r] = __builtin_fmaf(gc.v[i][r], pg[i], Lr[r]);
+        });
+    });
+    if constexpr (NX == 7 && NU == 2) mcol_var_block_f32_7_2_3(Lr, pivot, pg, gd);
+    else mcol_var_block_f32_11_4_3(Lr, pivot, pg, gd);
+}
+template <int NX, int NU, int J>
+__device__ __forceinline__ void chol_update_f(float (&lr)[NX + NU], float lj, float& piv)
+{
+    if constexpr (NX == 7 && NU == 2) chol_update_f32_7_2<J>(lr, lj, piv);
+    else chol_update_f32_11_4<J>(lr, lj, piv);
+}
+// The input pivots of M = M~ + sum_c s_c g_c g_c' (row-distributed, lane r holds row r of M~ in Lr; pivot = M~[0][0]
+// broadcast), pivots in turn. s_own: the barrier weight s_c of x_{k+1, idxbx(c)} on that state's lane (0 elsewhere).
+// Leaves the input columns of the factor in Lr[0..NU) and the Schur complement P~_k in the state block. fail: a
+// pivot <= 0 (or NaN).
+template <class M>
+__device__ __forceinline__ void chol_split_f32(float (&Lr)[M::NX + M::NU], float pivot, float s_own,
+                                               const GConstF<M>& gc, int r, bool& fail)
+{
+    constexpr int NX = M::NX, NU = M::NU;
+    sfor<0, NU>([&](auto jc) {
+        constexpr int j = decltype(jc)::value;
+        constexpr bool kB = j < M::NBX;
+        constexpr int ib = kB ? M::idxbx(j) : 0;  // the state input j drives
+        constexpr int xl = NU + ib;                // its lane
+        static_assert(!kB || M::gmask(ib) == ((1u << j) | (1u << xl)), "bounded state = integrator of its input");
+        float s = 0.0f, h = 0.0f, gam = 0.0f, a = 0.0f, b = 0.0f, e = 0.0f;
+        if constexpr (kB) {
+            h = gc.v[ib][j];
+            gam = gc.v[ib][xl];
+            s = bc<xl>(s_own);
+            a = pivot;  // s-free entries (after the previous pivots' updates)
+            b = Lr[j];  // lane xl: M[xl][j]
+            e = Lr[xl]; // lane xl: M[xl][xl]
+            const float hs = h * s;
+            pivot = __builtin_fmaf(h, hs, pivot);
+            Lr[j] += (r == j) ? h * hs : ((r == xl) ? gam * hs : 0.0f);
+        }
+        if (!(pivot > 0.0f)) fail = true;
+        const float rd = __builtin_amdgcn_rsqf(fmaxf(pivot, 1e-30f));
+        const float lj = (r >= j) ? Lr[j] * rd : 0.0f;
+        Lr[j] = lj;
+        chol_update_f<NX, NU, j>(Lr, lj, pivot);
+        if constexpr (kB) {
+            const float num = __builtin_fmaf(s, gam * gam * a - 2.0f * h * gam * b + h * h * e, a * e - b * b);
+            const float den = __builtin_fmaf(h * h, s, a);
+            if (r == xl) Lr[xl] = num * frcp(den);
+        }
+    });
+}
+
 // Right-looking Cholesky of a 2 x 2 input block held row-wise (lane r: Lr = row r of M, m00 / m11 / m10 its
 // entries broadcast to every lane), leaving the Schur complement in the state block. Both pivots come from the
 // block up front -- d0 = M00, d1 = M11 - M10^2 / M00 = det / M00 with det = M00 M11 - M10^2, so

@@ -24,18 +24,25 @@ VAR_ROWS = {(7, 2): (3,), (11, 4): (3,)}
 M = " row_mask:0xf bank_mask:0xf"
 
 
-def pg_block(nx, nu):
+# fp64 (the default factorisation) or fp32 (the split-sigma fp32 factorisation of the single-direction team kernel,
+# DESIGN.md section 5): instruction, C type and function-name suffix
+TYPES = {"f64": ("v_fmac_f64_dpp", "v_mov_b64_dpp", "double", ""),
+         "f32": ("v_fmac_f32_dpp", "v_mov_b32_dpp", "float", "_f32")}
+
+
+def pg_block(nx, nu, t="f64"):
     # classic Riccati: pg[i] += bcast_{nu+i}(Prow[nu+l]) * Gd[l] (column v of P_{k+1} [B A]); lane nu+i holds row i
     # of P_{k+1}; operands: acc 0..nx-1 (+v), Prow x-part nx.., Gd 2nx..
+    fma, _, ct, sfx = TYPES[t]
     lines = ["s_nop 1"]
     for l in range(nx):
         for i in range(nx):
-            lines.append(f"v_fmac_f64_dpp %{i}, %{nx + l}, %{2 * nx + l} row_newbcast:{nu + i}{M}")
+            lines.append(f"{fma} %{i}, %{nx + l}, %{2 * nx + l} row_newbcast:{nu + i}{M}")
     outs = ", ".join(f'"+v"(acc[{i}])' for i in range(nx))
     ins = ", ".join([f'"v"(prow[{nu + l}])' for l in range(nx)] + [f'"v"(gd[{l}])' for l in range(nx)])
     body = "\\n\\t".join(lines)
-    return (f"__device__ __forceinline__ void pg_block_{nx}_{nu}(double (&acc)[{nx}], const double (&prow)[{nx + nu}],"
-            f" const double (&gd)[{nx}])\n{{\n    asm(\"{body}\"\n        : {outs}\n        : {ins});\n}}\n")
+    return (f"__device__ __forceinline__ void pg_block{sfx}_{nx}_{nu}({ct} (&acc)[{nx}], const {ct} (&prow)[{nx + nu}],"
+            f" const {ct} (&gd)[{nx}])\n{{\n    asm(\"{body}\"\n        : {outs}\n        : {ins});\n}}\n")
 
 
 def mrow_pg_block(nx, nu):
@@ -56,55 +63,63 @@ def mrow_pg_block(nx, nu):
             f"        : {ins});\n}}\n")
 
 
-def mcol_var_block(nx, nu, ngv):
+def mcol_var_block(nx, nu, ngv, t="f64"):
     # classic Riccati, column form of M = D + [B A]' P [B A] on lane j: acc[r] += bcast_r(Gd[i]) * pg[i] over the
     # ngv state-dependent rows i of [B A] (lane r holds column r of [B A], lane j column j of P [B A]); the constant
     # rows are the caller's uniform-operand FMAs (team_common.hpp m_block). Then md0 = bcast_0(acc[0]), the first
     # pivot. M is symmetric, so lane j's column j is its row j. Operands: acc 0..nv-1 (+v), md0 (=v), Gd.., pg..
-    # NU = 2 also broadcasts M[1][1] and M[0][1] (m11, m10): both input pivots then come from the 2 x 2 block at
-    # once (the second as det / M00), so their rsq chains run side by side (sqp_rti_team.hip P1)
+    # fp64 NU = 2 also broadcasts M[1][1] and M[0][1] (m11, m10): both input pivots then come from the 2 x 2 block at
+    # once (the second as det / M00), so their rsq chains run side by side (sqp_rti_team.hip P1); the fp32 form takes
+    # its pivots in turn (each may carry a bounded state's barrier weight, team_common.hpp chol_split_f32)
+    fma, mov, ct, sfx = TYPES[t]
     nv = nx + nu
-    npv = 3 if nu == 2 else 1
+    npv = 3 if (nu == 2 and t == "f64") else 1
     lines = ["s_nop 1"]
     for i in range(ngv):
         for r in range(nv):
-            lines.append(f"v_fmac_f64_dpp %{r}, %{nv + npv + i}, %{nv + npv + ngv + i} row_newbcast:{r}{M}")
+            lines.append(f"{fma} %{r}, %{nv + npv + i}, %{nv + npv + ngv + i} row_newbcast:{r}{M}")
     lines.append("s_nop 1")
-    lines.append(f"v_mov_b64_dpp %{nv}, %0 row_newbcast:0{M}")
+    lines.append(f"{mov} %{nv}, %0 row_newbcast:0{M}")
     if npv == 3:
-        lines.append(f"v_mov_b64_dpp %{nv + 1}, %1 row_newbcast:1{M}")
-        lines.append(f"v_mov_b64_dpp %{nv + 2}, %0 row_newbcast:1{M}")
+        lines.append(f"{mov} %{nv + 1}, %1 row_newbcast:1{M}")
+        lines.append(f"{mov} %{nv + 2}, %0 row_newbcast:1{M}")
     outs = ", ".join([f'"+v"(acc[{r}])' for r in range(nv)] + ['"=&v"(md0)'] +
                      (['"=&v"(m11)', '"=&v"(m10)'] if npv == 3 else []))
     ins = ", ".join([f'"v"(gd[{i}])' for i in range(ngv)] + [f'"v"(pg[{i}])' for i in range(ngv)])
     body = "\\n\\t".join(lines)
-    extra = ", double& m11, double& m10" if npv == 3 else ""
-    return (f"__device__ __forceinline__ void mcol_var_block_{nx}_{nu}_{ngv}(double (&acc)[{nv}], double& md0{extra},"
-            f" const double (&pg)[{nx}], const double (&gd)[{nx}])\n{{\n    asm(\"{body}\"\n        : {outs}\n"
+    extra = f", {ct}& m11, {ct}& m10" if npv == 3 else ""
+    return (f"__device__ __forceinline__ void mcol_var_block{sfx}_{nx}_{nu}_{ngv}({ct} (&acc)[{nv}], {ct}& md0{extra},"
+            f" const {ct} (&pg)[{nx}], const {ct} (&gd)[{nx}])\n{{\n    asm(\"{body}\"\n        : {outs}\n"
             f"        : {ins});\n}}\n")
 
 
-def chol_update(nx, nu):
+def chol_update(nx, nu, t="f64"):
     # column j done: Lr[jp] -= bcast_jp(lj) * lj for jp > j, then pivot of column j+1 = bcast_{j+1}(Lr[j+1])
+    fma, mov, ct, sfx = TYPES[t]
     nv = nx + nu
     out = []
-    for j in range(nv - 1):
+    for j in range(nv - 1 if t == "f64" else nu):  # fp32: the input columns only (the split-sigma factor's pivots)
         lines = ["s_nop 1"]
         k = 0
         ops = []
         for jp in range(j + 1, nv):
-            lines.append(f"v_fmac_f64_dpp %{k}, -%{nv - j - 1 + 1}, %{nv - j - 1 + 1} row_newbcast:{jp}{M}")
+            lines.append(f"{fma} %{k}, -%{nv - j - 1 + 1}, %{nv - j - 1 + 1} row_newbcast:{jp}{M}")
             ops.append(f'"+v"(lr[{jp}])')
             k += 1
         n = nv - j - 1
         # the pivot broadcast reads lr[j+1], written by the first FMA: two more VALU ops must separate them
         if n < 3:
             lines.append("s_nop 1")
-        lines.append(f"v_mov_b64_dpp %{n}, %0 row_newbcast:{j + 1}{M}")
+        lines.append(f"{mov} %{n}, %0 row_newbcast:{j + 1}{M}")
         outs = ", ".join(ops + ['"=&v"(piv)'])
         body = "\\n\\t".join(lines)
-        out.append(f"__device__ __forceinline__ void chol_update_{nx}_{nu}_{j}(double (&lr)[{nv}], double lj, double& piv)\n"
+        out.append(f"__device__ __forceinline__ void chol_update{sfx}_{nx}_{nu}_{j}({ct} (&lr)[{nv}], {ct} lj, {ct}& piv)\n"
                    f"{{\n    asm(\"{body}\"\n        : {outs}\n        : \"v\"(lj));\n}}\n")
+    if t == "f32":
+        cases = "\n".join(f"    if constexpr (J == {j}) chol_update_f32_{nx}_{nu}_{j}(lr, lj, piv);" for j in range(nu))
+        out.append(f"template <int J>\n__device__ __forceinline__ void chol_update_f32_{nx}_{nu}(float (&lr)[{nv}], float lj,"
+                   f" float& piv)\n{{\n{cases}\n}}\n")
+        return "\n".join(out)
     # the same updates without the next pivot's broadcast (input columns j < nu, when the pivots are known up front)
     for j in range(nu):
         lines = ["s_nop 1"]
@@ -245,6 +260,8 @@ def generate():
     for nx, nu in SHAPES:
         nv = nx + nu
         parts += [pg_block(nx, nu), mrow_pg_block(nx, nu)] + [mcol_var_block(nx, nu, g) for g in VAR_ROWS[(nx, nu)]]
+        parts += [pg_block(nx, nu, "f32"), mcol_var_block(nx, nu, VAR_ROWS[(nx, nu)][0], "f32"),
+                  chol_update(nx, nu, "f32")]
         parts += [chol_update(nx, nu),
                   dot_f32(nx, nu, f"dot_x_{nx}_{nu}"), dot_f32(nv, 0, f"dot_v_{nx}_{nu}"),
                   mst_rowmul(nx, nu), mst_rowmul_lt(nx, nu), mst_rowdot(nx, nu), mst_chol(nx, nu), mst_trsv(nx, nu), mst_vdot(nx, nu)]
