@@ -229,13 +229,16 @@ def cpu_baseline(fleets, sample, ticks, nthreads):
     """Replay `ticks` closed-loop GPU ticks for the first `sample` robots (0: all) of each fleet through the
     fp64 oracle. Every tick the oracle starts from exactly the GPU's pre-tick state (iterate, carried refs,
     measurements, references), so the u0 error is the per-solve fp32-vs-fp64 error, not the divergence of
-    two closed loops. Returns (CPU instance-iterations/s, u0 max-abs err, failed, solves, 1-core rate)."""
+    two closed loops. The timed replay runs the oracle's "batched" exit rule (the batched API's); the same inputs
+    go through its "acados" rule too (HPIPM: no infeasibility exit), untimed, for the second error figure. Returns
+    (CPU instance-iterations/s, u0 max-abs err, failed, solves, 1-core rate, u0 max-abs err on the acados rule)."""
     from oracle.oracle import Oracle
     total_time, total_solves, err, fails = 0.0, 0, 0.0, 0
-    time_1, solves_1 = 0.0, 0
+    time_1, solves_1, err_a = 0.0, 0, 0.0
     for f in fleets:
         S = f.B if sample <= 0 else min(sample, f.B)
         o = Oracle(f.model, f.N, rule="batched")
+        oa = Oracle(f.model, f.N, rule="acados")
         for _ in range(ticks):
             torch.cuda.synchronize()
             sn = f.snapshot()
@@ -251,17 +254,24 @@ def cpu_baseline(fleets, sample, ticks, nthreads):
             o.batch_tick(*a1, *s1, nthreads=1)
             time_1 += time.perf_counter() - t0
             solves_1 += S1
+            sa = [np.array(a) for a in state]  # batch_tick updates the iterate in place
             t0 = time.perf_counter()
             nf, cmd_o, u0_o, st_o, _ = o.batch_tick(*args, *state, nthreads=nthreads)
             total_time += time.perf_counter() - t0
             total_solves += S
+            _, _, u0_a, st_a, _ = oa.batch_tick(*args, *sa, nthreads=nthreads)
             torch.cuda.synchronize()
-            ok = (st_o == 0) & (f.status[:S].cpu().numpy() == 0)
+            st_g = f.status[:S].cpu().numpy()
+            u0_g = f.u0[:, :S].cpu().numpy().T
+            ok = (st_o == 0) & (st_g == 0)
             fails += int((~ok).sum())
             if ok.any():
-                err = max(err, float(np.abs(f.u0[:, :S].cpu().numpy().T[ok] - u0_o[ok]).max()))
+                err = max(err, float(np.abs(u0_g[ok] - u0_o[ok]).max()))
+            ok_a = (st_a == 0) & (st_g == 0)
+            if ok_a.any():
+                err_a = max(err_a, float(np.abs(u0_g[ok_a] - u0_a[ok_a]).max()))
             f.advance()
-    return total_solves / total_time, err, fails, total_solves, solves_1 / time_1
+    return total_solves / total_time, err, fails, total_solves, solves_1 / time_1, err_a
 
 
 class LaunchTimer:
@@ -305,13 +315,35 @@ def launch_ranks(n, argv):
     return subprocess.run(cmd, env=env).returncode
 
 
-def _factory(spec):
-    """--test-solver MODULE:ATTR -> the solver class FleetNode builds its fleets with (default: BatchSolver)."""
-    if not spec:
-        return None
-    import importlib
-    mod, attr = spec.split(":")
-    return getattr(importlib.import_module(mod), attr)
+# --ipm-rules acados: HPIPM's defaults for the batched API (the reference's OCP sets none of
+# them, scripts/diff/generate_c_code.py:68-74): no infeasibility exit, slack floor thr0 0.5 (the oracle's), every QP
+# started cold. The product's own rules (nmpc_model_params_default) differ in exactly these three (DESIGN.md section
+# 5); this line states what they are worth
+ACADOS_RULES = dict(qp_infeas_lambda=0.0, qp_thr0=0.5, qp_warm_start=0)
+
+
+def _factory(spec, ipm_rules="product", qp=None):
+    """--test-solver MODULE:ATTR -> the solver class FleetNode builds its fleets with (default: BatchSolver);
+    --ipm-rules acados -> BatchSolver with ACADOS_RULES; --qp k=v,... (A/B runs) -> nmpc_model_params overrides."""
+    if spec:
+        import importlib
+        mod, attr = spec.split(":")
+        return getattr(importlib.import_module(mod), attr)
+    over = dict(ACADOS_RULES) if ipm_rules == "acados" else {}
+    for kv in (qp.split(",") if qp else []):
+        k, v = kv.split("=")
+        over[k] = float(v)
+    if over:
+        from nmpc_nav_control_amd._lib import default_params
+        from nmpc_nav_control_amd.batch import BatchSolver
+
+        def make(model, N, B, device=None):
+            prm = default_params(model, N)
+            for k, v in over.items():
+                setattr(prm, k, type(getattr(prm, k))(v))
+            return BatchSolver(model, N, B, params=prm, device=device)
+        return make
+    return None
 
 
 def main():
@@ -342,6 +374,10 @@ def main():
     ap.add_argument("--batch-per-gpu", type=int, default=None,
                     help="robots per rank (default: the config's; mixed splits them over the three models)")
     # test hooks of the launch path (tests/test_bench_launch.py): CPU ranks over gloo with a CPU solver class
+    ap.add_argument("--ipm-rules", default="product", choices=["product", "acados"],
+                    help="acados: the batched solve with HPIPM's defaults (no infeasibility exit, thr0 0.5, cold QP "
+                         "starts) instead of the product's IPM rules; not the headline")
+    ap.add_argument("--qp", default=None, help=argparse.SUPPRESS)  # A/B: nmpc_model_params overrides k=v,...
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"], help=argparse.SUPPRESS)
     ap.add_argument("--test-solver", default=None, help=argparse.SUPPRESS)
     args = ap.parse_args()
@@ -385,7 +421,7 @@ def main():
     groups = cfg.get("groups", 1) if args.groups is None else args.groups
     node = FleetNode(models, cfg["N"], DEFAULT_SEED + cfg["idx"], dev, rank=rank, world=world, gather=gather,
                      groups=groups, decoupled=False if args.joined else None, renew=not args.no_renew,
-                     solver_factory=_factory(args.test_solver))
+                     solver_factory=_factory(args.test_solver, args.ipm_rules, args.qp))
     fleets = node.fleets
     if not cpu:
         torch.cuda.synchronize()
@@ -423,9 +459,11 @@ def main():
         u0_err = None
         if not args.no_cpu_baseline and world == 1 and not cpu:
             nthreads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
-            cpu_rate, u0_err, nf, ns, rate_1 = cpu_baseline(fleets, args.cpu_sample, args.cpu_ticks, nthreads)
+            cpu_rate, u0_err, nf, ns, rate_1, u0_err_acados = cpu_baseline(fleets, args.cpu_sample, args.cpu_ticks,
+                                                                           nthreads)
             cpu_base = {"value": round(cpu_rate, 1), "unit": "SQP-RTI iterations/sec", "cores": nthreads,
                         "kind": "port", "oracle_rule": "batched (the batched API's IPM exit rule; oracle/oracle.py RULES)",
+                        "u0_max_abs_err_acados_rule": u0_err_acados,
                         "sample": f"{ns} instance-iterations: {'all' if args.cpu_sample <= 0 else args.cpu_sample} robots of each model x "
                                   f"{args.cpu_ticks} closed-loop ticks after the timed region, fp64 oracle/nmpc_oracle.c, "
                                   f"OpenMP {nthreads} threads, identical inputs", "failed": nf,
@@ -446,7 +484,8 @@ def main():
                        "ranks": ranks, "backend": backend,
                        "launcher": os.environ.get("NMPC_BENCH_LAUNCHER",
                                                   "torchrun" if "WORLD_SIZE" in os.environ else "single process"),
-                       "closed_loop_warmup_ticks": args.closed_loop_warmup, "rccl_gather": gather},
+                       "closed_loop_warmup_ticks": args.closed_loop_warmup, "rccl_gather": gather,
+                       "ipm_rules": args.ipm_rules + (f" + {args.qp}" if args.qp else "")},
             "u0_max_abs_err": u0_err, "qp_iter_mean": round(k_mean, 3), "qp_iter_max": int(node.iters_max.max().item()),
             "qp_iter": {k: (round(v, 3) if isinstance(v, float) else v) for k, v in its.items()},
             "failed_solves": int(node.fail_cnt.sum().item()), "roofline": roof, "cpu_baseline": cpu_base,

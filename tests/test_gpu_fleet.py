@@ -44,23 +44,33 @@ def replay_and_compare(fleet, oracle, tick_fn):
     return eu, max(ex, 0.0), ec, st, st_o, after["xbar"]
 
 
-@pytest.mark.parametrize("model,N,B,idx,layout", [("diff", 40, 4096, 1, "wide"), ("diff", 40, 4096, 1, "split"),
-                                                  ("diff", 40, 1024, 1, None), ("omni4", 40, 4096, 2, "wide"),
-                                                  ("tric", 60, 8192, 3, "split")])
-def test_bench_config_full_batch_replay(built, model, N, B, idx, layout):
+@pytest.mark.parametrize("model,N,B,idx,layout,rules", [("diff", 40, 4096, 1, "wide", "product"),
+                                                        ("diff", 40, 4096, 1, "split", "product"),
+                                                        ("diff", 40, 4096, 1, "wide", "acados"),
+                                                        ("diff", 40, 1024, 1, None, "product"),
+                                                        ("omni4", 40, 4096, 2, "wide", "product"),
+                                                        ("tric", 60, 8192, 3, "split", "product")])
+def test_bench_config_full_batch_replay(built, model, N, B, idx, layout, rules):
     """BASELINE configs at full batch (the bench's own fleets): 20 closed-loop ticks with no failed solve, then
     two ticks on which EVERY robot is replayed through the fp64 oracle. The metric config runs once per record
     layout of diff's team kernel (wide: its own default alone on the device, what bench.py's metric line runs;
     split: the mixed fleet's), and the layout the launches took is asserted. tric: >= 10 % of
     the robots have their steering reference alpha_ref on its 45 deg bound somewhere on the horizon (SURVEY 8d
-    config 4; NMPCNavControlTric.cpp:24-29, scripts/tric/generate_c_code.py:47-57)."""
-    f = Fleet(model, B, N, SEED + idx, DEV, record_layout=layout if model == "diff" else None)
+    config 4; NMPCNavControlTric.cpp:24-29, scripts/tric/generate_c_code.py:47-57). rules "acados": the metric
+    fleet with HPIPM's defaults instead of the product's IPM rules (bench.py ACADOS_RULES: no infeasibility exit,
+    thr0 0.5, cold QP starts), replayed through the oracle's acados rule."""
+    import bench
+    f = Fleet(model, B, N, SEED + idx, DEV, record_layout=layout if model == "diff" else None,
+              solver_factory=bench._factory(None, rules))
     plan = f.solver.plan_ex(B, "run")
     if layout is None:
         assert plan["kernel"] == "rowpar", plan  # diff1024: the segmented row-parallel kernel
     else:
         assert plan["kernel"] == "team" and plan["record_layout"] == layout, plan
-    o = Oracle(model, N, rule="batched")
+    if rules == "acados":
+        prm = f.solver.params
+        assert prm.qp_infeas_lambda == 0.0 and prm.qp_thr0 == 0.5 and prm.qp_warm_start == 0
+    o = Oracle(model, N, rule="batched" if rules == "product" else "acados")
     for tick in range(20):
         f.tick()
         if tick % 5 == 4:
@@ -75,7 +85,8 @@ def test_bench_config_full_batch_replay(built, model, N, B, idx, layout):
             on_bound = (np.abs(xb[:, 1:, 6]) >= np.pi / 4 - 1e-3).any(axis=1)
             assert on_bound.mean() >= 0.10, on_bound.mean()
         f.advance()
-    print(f"\n{model} N={N} B={B}: all robots, 2 ticks: u0 err {worst_u:.2e}, x err {worst_x:.2e}, cmd {worst_c:.2e}")
+    print(f"\n{model} N={N} B={B} {rules}: all robots, 2 ticks: u0 err {worst_u:.2e}, x err {worst_x:.2e}, "
+          f"cmd {worst_c:.2e}")
     assert worst_u <= TOL_U, worst_u
     assert worst_x <= TOL_X, worst_x
     assert worst_c <= TOL_U, worst_c
