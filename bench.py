@@ -51,7 +51,7 @@ MODEL_FLOPS = {"diff": dict(nx=7, nu=2, nbx=2, nbu=2, nnz_jx=12, nnz_ju=2, c_f=2
                "tric": dict(nx=7, nu=2, nbx=2, nbu=2, nnz_jx=12, nnz_ju=2, c_f=24)}
 FP32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 vector (and FP32-input MFMA) peak
 FP64_PEAK_SPEC_TFLOPS = 78.6  # AMD spec FP64 vector (half the FP32 rate; the guide gives no FP64 figure)
-PROFILE_ROUND = "r05"
+PROFILE_ROUND = "r06"
 HBM_PEAK_GBS = 8000.0
 
 
