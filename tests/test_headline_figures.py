@@ -5,6 +5,7 @@ profiles/<ROUND>/ and a format (the table below). The test formats the record's 
 the marker to start with it, so a figure cannot go stale without this test failing. Every key
 must be quoted at least once across the three documents, and every marker must name a known key.
 """
+import csv
 import json
 import os
 import re
@@ -12,7 +13,7 @@ import re
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-ROUND = "r05"
+ROUND = "r06"
 PROF = os.path.join(ROOT, "profiles", ROUND)
 DOCS = ("README.md", "DESIGN.md", "INTEGRATION.md")
 CONFIGS = ("metric", "diff1024", "omni4", "tric", "mixed")
@@ -37,7 +38,32 @@ def _sources():
         out[f"{c}_ms"] = f"{b['ms_per_step']:.2f}"
         out[f"{c}_u0err"] = f"{b['u0_max_abs_err']:.1e}"
         out[f"{c}_frac"] = f"{100.0 * b['roofline']['frac']:.1f} %"
+    for c in CONFIGS:
+        b = _bench(c)
+        out[f"{c}_iters"] = f"{b['qp_iter_mean']:.1f} / {b['qp_iter_max']}"
     out["metric_launch_ms"] = f"{_bench('metric')['roofline']['kernel_ms_mean']:.3f}"
+    # the rocprofv3 record and the PMC counters the prose cites (figures citing
+    # profiles/<round>/*trace* and pmc/ are checked like the bench figures)
+    with open(os.path.join(PROF, "bench_metric_kernel_trace_timed.json")) as fh:
+        tr = json.load(fh)
+    out["metric_trace_ms"] = f"{tr['mean_ms']:.3f}"
+    with open(os.path.join(PROF, "bench_metric_kernel_stats.csv")) as fh:
+        row = next(r for r in csv.DictReader(fh) if "k_sqp_rti" in r["Name"])
+    out["metric_stats_ms"] = f"{float(row['AverageNs']) * 1e-6:.3f}"
+    out["metric_stats_calls"] = row["Calls"]
+    for c, key in (("metric", "diff_N40_B4096"), ("diff1024", "diff_N40_B1024")):
+        with open(os.path.join(PROF, "pmc", f"pmc_{key}.json")) as fh:
+            pm = json.load(fh)
+        out[f"{c}_pmc_traffic_gb"] = f"{pm['l2_fabric_bytes_per_launch'] / 1e9:.2f} GB"
+        out[f"{c}_pmc_issue"] = f"{pm['valu_issue_frac']:.2f}"
+        out[f"{c}_pmc_wait"] = f"{pm['wait_frac']:.2f}"
+        out[f"{c}_pmc_active"] = f"{pm['active_frac']:.2f}"
+        out[f"{c}_pmc_hit"] = f"{100 * pm['tcc_hit_rate']:.0f} %"
+        out[f"{c}_pmc_write_gb"] = f"{pm['write_size_kb'] * 1024 / 1e9:.2f} GB"
+    mr = _bench("metric")["roofline"]
+    ex = mr["executed_flops"]
+    out["metric_exec64_ratio"] = f"{ex['fp64_per_step'] / mr['fp64']['flop_per_step']:.2f}"
+    out["metric_exec32_ratio"] = f"{ex['fp32_per_step'] / mr['fp32']['flop_per_step']:.2f}"
     out["metric_cpu_its"] = f"{_bench('metric')['cpu_baseline']['value'] / 1e3:.0f} k"
     for m in ("cold", "warm"):
         out[f"capsule_{m}_ms"] = f"{_capsule(m)['run_wall_ms_mean']:.3f}"

@@ -13,7 +13,7 @@ import re
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-ROUND = "r05"
+ROUND = "r06"
 PROF = os.path.join(ROOT, "profiles", ROUND)
 CONFIGS = ["metric", "diff1024", "omni4", "tric", "mixed"]
 
