@@ -187,8 +187,18 @@ __device__ __forceinline__ float wave_min_rows(float v)
 // boundaries (DESIGN.md "Segmented Riccati"); a robot's serial chain shrinks from N + 1 stage steps to L + 1 plus S - 1
 // master steps. The rhs is built in absolute form (no adjoint), so the stationarity residual of the stopping rule is
 // evaluated by its own serial adjoint pass, only when the rest of the exit test already holds.
+// Register bound of the segmented diff / tric instantiations: two waves per SIMD for W <= 2 (launches above 256
+// robots put two robots' waves on each SIMD, tests/test_reg_usage.py), one for W = 4 (launches of at most 256 robots,
+// one block per CU). Bounding the four-wave kernel to 256 registers as well (round 5) made the compiler serialise the
+// master step's LDS operand loads through one register; without it the one-robot capsule takes 0.260 instead of
+// 0.279 ms cold (same box, profiles/r06/ab/p0b_w4.txt). -DNMPC_W4_BOUND2 keeps round 5's bound for A/B runs.
+#ifdef NMPC_W4_BOUND2
+constexpr int kRowparW2Max = 4;
+#else
+constexpr int kRowparW2Max = 2;
+#endif
 template <class M, int W, bool SEG>
-__global__ __launch_bounds__(64 * W, (SEG && M::NX < 10) ? 2 : 1) void k_sqp_rti_rowpar(KParams P, KArgs a, int mode)
+__global__ __launch_bounds__(64 * W, (SEG && M::NX < 10 && W <= kRowparW2Max) ? 2 : 1) void k_sqp_rti_rowpar(KParams P, KArgs a, int mode)
 {
     using R = RowRec<M>;
     constexpr int NX = M::NX, NU = M::NU, NV = R::NV, NGV = R::NGV, RS = R::RS, RSS = R::RSS;
@@ -410,11 +420,92 @@ __global__ __launch_bounds__(64 * W, (SEG && M::NX < 10) ? 2 : 1) void k_sqp_rti
     __syncthreads();  // the stage inputs of every row are in LDS
     RP_STAMP(1);
 
-    // ---- P0b (serial, wave 0): the dynamics-feasible initial iterate dx_{k+1} = A_k dx_k + b_k and, in run mode,
-    // the reference unwrap / padding (NMPCNavControlDiff.cpp:104-118), both recursions over the stages; dx_k and
-    // the stage's reference pose go to LDS for P0c ----------------------------------------------------------------
+    // ---- P0b (serial): the dynamics-feasible initial iterate dx_{k+1} = A_k dx_k + b_k on wave 0 and, in run mode,
+    // the reference unwrap / padding (NMPCNavControlDiff.cpp:104-118) on the last wave, two recursions over the
+    // stages; dx_k and the stage's reference pose go to LDS for P0c. Each loop body is branch-free: round 5's one
+    // loop for both recursions tested the mode, the horizon end and the reference lanes in every stage (about 15
+    // scalar branches per stage, 575 cycles per stage step at one robot; profiles/r06/ab/p0b_w4.txt)
     float* const s_dx = s_red + 32;                  // [N+1][16]
     float* const s_ref = s_dx + (size_t)(N + 1) * 16;  // [N+1][3]
+#ifndef NMPC_P0_SERIAL
+    if (w0) {
+        struct Stg {
+            float b, g[NGV];
+        };
+        auto lds_ld = [&](int k, Stg& o) {
+            const int kk = k <= N ? k : N;
+            const float* const st = s_stg + (size_t)kk * SF * 16 + r;
+            o.b = st[64];
+#pragma unroll
+            for (int i = 0; i < NGV; i++) o.g[i] = st[(5 + i) * 16];
+        };
+        // store dx_k, then dx_{k+1} (every LDS store unconditional; rows 1-3 of wave 0 write row 0's identical values)
+        float dx = is_x ? x0_lane - XB(0, xi) : 0.0f;
+        auto step = [&](int k, const Stg& cur) {
+            s_dx[k * 16 + r] = dx;
+            const float dzd = is_x ? dx : 0.0f;
+            float nx_ = dot_v<NX, NU>(0.0f, dzd, grow);
+#pragma unroll
+            for (int i = 0; i < NGV; i++) {
+                const float sr = row_sum16(lv ? cur.g[i] * dzd : 0.0f);
+                if (xi == i) nx_ = sr;
+            }
+            dx = is_x ? nx_ + cur.b : 0.0f;
+        };
+        // three buffers used in turn, loads two stages ahead (no copies: a copy waits for the LDS read in flight)
+        Stg c0, c1, c2;
+        lds_ld(0, c0);
+        lds_ld(1, c1);
+        for (int k = 0;; k += 3) {  // stages 0 .. N - 1
+            lds_ld(k + 2, c2);
+            step(k, c0);
+            if (k + 1 == N) break;
+            lds_ld(k + 3, c0);
+            step(k + 1, c1);
+            if (k + 2 == N) break;
+            lds_ld(k + 4, c1);
+            step(k + 2, c2);
+            if (k + 3 == N) break;
+        }
+        s_dx[N * 16 + r] = dx;
+    }
+    if (mode == kModeRun && wave == W - 1) {
+        // (rows of the wave compute the same values; lanes 0-2 of each row store them, the rest store to a pad)
+        float ref_x = 0.0f, ref_y = 0.0f, ref_t = pose_th;
+        auto ld_t = [&](int k, float (&t)[3]) {
+            const int kk = k <= N ? k : N;
+#pragma unroll
+            for (int j = 0; j < 3; j++) t[j] = my_traj[kk * 3 + j];
+        };
+        auto uw = [&](int k, const float (&t)[3]) {
+            const bool in = k < len;
+            const float th = t[2], d = th - ref_t;
+            const float thu = (d > kPi) ? th - 2.0f * kPi : ((d < -kPi) ? th + 2.0f * kPi : th);
+            ref_x = in ? t[0] : ref_x;
+            ref_y = in ? t[1] : ref_y;
+            ref_t = in ? thu : ref_t;
+            float v = ref_t;
+            v = (r == 1) ? ref_y : v;
+            v = (r == 0) ? ref_x : v;
+            *(r < 3 ? s_ref + k * 3 + r : lpad) = v;
+        };
+        float t0[3], t1[3], t2[3];
+        ld_t(0, t0);
+        ld_t(1, t1);
+        for (int k = 0;; k += 3) {  // stages 0 .. N
+            ld_t(k + 2, t2);
+            uw(k, t0);
+            if (k == N) break;
+            ld_t(k + 3, t0);
+            uw(k + 1, t1);
+            if (k + 1 == N) break;
+            ld_t(k + 4, t1);
+            uw(k + 2, t2);
+            if (k + 2 == N) break;
+        }
+    }
+#else
+    // A/B only (-DNMPC_P0_SERIAL): round 5's single loop over both recursions on wave 0
     if (w0) {
         float dx = is_x ? x0_lane - XB(0, xi) : 0.0f;
         float ref_x = 0.0f, ref_y = 0.0f, ref_t = pose_th;
@@ -470,6 +561,7 @@ __global__ __launch_bounds__(64 * W, (SEG && M::NX < 10) ? 2 : 1) void k_sqp_rti
             if (k + 2 == N) break;
         }
     }
+#endif
     __syncthreads();
     RP_STAMP(2);
 
