@@ -30,6 +30,7 @@ using nmpc::TraceRange;
 
 #include "nmpc_amd/nmpc_batch.h"
 #include "nmpc_amd/nmpc_capsule.h"
+#include "nmpc_kernels.hpp"  // nmpc_batch_solve_iterate_staged (library-internal)
 
 struct nmpc_capsule_impl {
     int model = 0, N = 0;
@@ -101,6 +102,7 @@ struct Engine {
     nmpc_batch* batch = nullptr;
     int cap = 0;
     float *dio = nullptr, *hio = nullptr;  // the device I/O block, sized for cap capsules, and its pinned twin
+    float* hio_dev = nullptr;  // hio as the device addresses it (staged one-capsule solves)
     unsigned char *dwarm = nullptr, *hwarm = nullptr;  // the handle's warm flags; pinned staging for them
     std::vector<std::uint64_t> owner;
     std::vector<unsigned char> dev_warm;
@@ -110,7 +112,7 @@ struct Engine {
         nmpc_batch_destroy(batch);
         batch = nullptr;
         (void)hipFree(dio); (void)hipHostFree(hio); (void)hipHostFree(hwarm);
-        dio = hio = nullptr;
+        dio = hio = hio_dev = nullptr;
         dwarm = hwarm = nullptr;
         owner.clear();
         dev_warm.clear();
@@ -360,6 +362,7 @@ int ensure_engine(Engine& e, const nmpc_model_params& prm, int n, std::string& w
         e.release();
         return -1;
     }
+    if ((r = hipHostGetDevicePointer(reinterpret_cast<void**>(&e.hio_dev), e.hio, 0)) != hipSuccess) e.hio_dev = nullptr;
     nmpc_batch_warm_state(e.batch, &e.dwarm, nullptr, nullptr);
     e.owner.assign(cap, 0);
     e.dev_warm.assign(cap, 0);  // nmpc_batch_create zeroes the flags
@@ -423,24 +426,44 @@ void solve_group(std::vector<nmpc_capsule_impl*>& cs, std::vector<Packed>& ps, c
         e.hwarm[q] = (e.owner[q] == c->uid && c->warm_ok) ? c->warm_tag : 0;
         flags_differ |= e.hwarm[q] != e.dev_warm[q];
     }
+    nmpc_launch_plan plan{};
+    nmpc_batch_plan_ex(e.batch, n, NMPC_PLAN_SOLVE, &plan);  // the kernel of this launch, and the tag it leaves
+    // One capsule on the row-parallel kernel (the reference node's case): the kernel reads the pinned input block and
+    // writes the output block back itself, so the solve is one launch instead of a copy, the kernel and a copy, each
+    // behind the previous one's completion (same box: profiles/r06/ab/capsule_staged.txt). NMPC_AMD_CAPSULE_STAGE=0
+    // keeps the copies (A/B).
+    static const bool stage_ok_env = [] {
+        const char* v = std::getenv("NMPC_AMD_CAPSULE_STAGE");
+        return !(v && std::atoi(v) == 0);
+    }();
+    const bool staged = n == 1 && plan.kernel == 1 && e.hio_dev && stage_ok_env;
     {
         const TraceRange tr("capsule.h2d");
         if (flags_differ && (r = hipMemcpyAsync(e.dwarm, e.hwarm, (size_t)n, hipMemcpyHostToDevice, st)) != hipSuccess)
             return fail_all(hipGetErrorString(r));
-        if ((r = hipMemcpyAsync(dio, e.hio, sizeof(float) * bl.in_floats, hipMemcpyHostToDevice, st)) != hipSuccess)
+        if (!staged &&
+            (r = hipMemcpyAsync(dio, e.hio, sizeof(float) * bl.in_floats, hipMemcpyHostToDevice, st)) != hipSuccess)
             return fail_all(hipGetErrorString(r));
     }
     const auto t1 = std::chrono::steady_clock::now();
-    if (nmpc_batch_solve_iterate(e.batch, n, dio + bl.x0, dio + bl.yref, ny, dio + bl.We, nullptr, dio + bl.xb,
-                                 dio + bl.ub, n, reinterpret_cast<int*>(dio + bl.ost),
-                                 reinterpret_cast<int*>(dio + bl.oit), dio + bl.ores, st) != NMPC_OK)
+    if (staged) {
+        const nmpc_stage_io io{e.hio_dev, dio, (int)bl.in_floats, e.hio_dev + bl.xb, dio + bl.xb,
+                               (int)(bl.io_words - bl.xb)};
+        if (nmpc_batch_solve_iterate_staged(e.batch, dio + bl.x0, dio + bl.yref, ny, dio + bl.We, dio + bl.xb,
+                                            dio + bl.ub, reinterpret_cast<int*>(dio + bl.ost),
+                                            reinterpret_cast<int*>(dio + bl.oit), dio + bl.ores, st, &io) != NMPC_OK)
+            return fail_all(nmpc_last_error());
+    } else if (nmpc_batch_solve_iterate(e.batch, n, dio + bl.x0, dio + bl.yref, ny, dio + bl.We, nullptr,
+                                        dio + bl.xb, dio + bl.ub, n, reinterpret_cast<int*>(dio + bl.ost),
+                                        reinterpret_cast<int*>(dio + bl.oit), dio + bl.ores, st) != NMPC_OK) {
         return fail_all(nmpc_last_error());
+    }
     {
         const TraceRange tr("capsule.d2h_sync");  // the output copy queued behind the kernel, and the wait
-        if ((r = hipMemcpyAsync(e.hio + bl.xb, dio + bl.xb, sizeof(float) * (bl.io_words - bl.xb),
-                                hipMemcpyDeviceToHost, st)) != hipSuccess ||
-            (r = hipStreamSynchronize(st)) != hipSuccess)
+        if (!staged && (r = hipMemcpyAsync(e.hio + bl.xb, dio + bl.xb, sizeof(float) * (bl.io_words - bl.xb),
+                                           hipMemcpyDeviceToHost, st)) != hipSuccess)
             return fail_all(hipGetErrorString(r));
+        if ((r = hipStreamSynchronize(st)) != hipSuccess) return fail_all(hipGetErrorString(r));
     }
     const float* const hres = e.hio + bl.ores;
     const int* const hst = reinterpret_cast<const int*>(e.hio + bl.ost);
@@ -455,8 +478,6 @@ void solve_group(std::vector<nmpc_capsule_impl*>& cs, std::vector<Packed>& ps, c
                      std::chrono::duration<double>(t1 - tb).count() * 1e3, tq * 1e3);
     int rule_warm = 0, rule_wmax = 0, rule_imax = 0;
     nmpc_batch_warm_rule(e.batch, &rule_warm, &rule_wmax, &rule_imax);
-    nmpc_launch_plan plan{};
-    nmpc_batch_plan_ex(e.batch, n, NMPC_PLAN_SOLVE, &plan);  // the tag this launch left in the flags
     std::vector<double*> xbs(n), ubs(n);  // failed solves keep their iterate (nullptr: skipped)
     for (int q = 0; q < n; q++) {
         nmpc_capsule_impl* c = cs[idx[q]];

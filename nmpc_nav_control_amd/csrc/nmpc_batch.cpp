@@ -143,6 +143,7 @@ template <class M>
 hipError_t launch_m(nmpc_batch* b, const KArgs& a, int mode, hipStream_t s)
 {
     if (a.rowpar) return launch_sqp_rti_rowpar<M>(b->kp, a, mode, s);
+    if (a.stage_in_n > 0 || a.stage_out_n > 0) return hipErrorInvalidValue;  // (only the row-parallel kernel stages)
     return launch_sqp_rti_team<M>(b->kp, a, mode, s);
 }
 
@@ -630,11 +631,11 @@ int nmpc_batch_solve(nmpc_batch* b, int B, const float* x0, const float* yref, i
     return hip_err(launch(b, a, kModeSolve, (hipStream_t)stream), "solve launch");
 }
 
-int nmpc_batch_solve_iterate(nmpc_batch* b, int B, const float* x0, const float* yref, int ny_in, const float* We,
-                             const unsigned char* reset, float* xbar, float* ubar, int ld, int* status, int* qp_iter,
-                             float* qp_res, void* stream)
+namespace {
+int solve_iterate(nmpc_batch* b, int B, const float* x0, const float* yref, int ny_in, const float* We,
+                  const unsigned char* reset, float* xbar, float* ubar, int ld, int* status, int* qp_iter,
+                  float* qp_res, void* stream, const nmpc_stage_io* io)
 {
-    const TraceRange trace("nmpc_batch_solve_iterate");
     if (!b) return set_err(NMPC_ERR_ARG, "batch is NULL");
     if (B < 0 || B > b->capacity) return set_err(NMPC_ERR_ARG, "B out of range [0, capacity]");
     if (B == 0) return NMPC_OK;
@@ -658,7 +659,39 @@ int nmpc_batch_solve_iterate(nmpc_batch* b, int B, const float* x0, const float*
     a.status = status;
     a.qp_iter = qp_iter;
     a.qp_res = qp_res;
+    if (io) {
+        // one robot on the row-parallel kernel only (the team kernel does not stage)
+        nmpc_launch_plan plan{};
+        nmpc_batch_plan_ex(b, B, NMPC_PLAN_SOLVE, &plan);
+        if (B != 1 || plan.kernel != 1)
+            return set_err(NMPC_ERR_ARG, "staged I/O needs a one-robot row-parallel launch");
+        a.stage_in_h = io->in_h;
+        a.stage_in_d = io->in_d;
+        a.stage_in_n = io->in_n;
+        a.stage_out_h = io->out_h;
+        a.stage_out_d = io->out_d;
+        a.stage_out_n = io->out_n;
+    }
     return hip_err(launch(b, a, kModeSolve, (hipStream_t)stream), "solve launch");
+}
+}  // namespace
+
+int nmpc_batch_solve_iterate(nmpc_batch* b, int B, const float* x0, const float* yref, int ny_in, const float* We,
+                             const unsigned char* reset, float* xbar, float* ubar, int ld, int* status, int* qp_iter,
+                             float* qp_res, void* stream)
+{
+    const TraceRange trace("nmpc_batch_solve_iterate");
+    return solve_iterate(b, B, x0, yref, ny_in, We, reset, xbar, ubar, ld, status, qp_iter, qp_res, stream, nullptr);
+}
+
+int nmpc_batch_solve_iterate_staged(nmpc_batch* b, const float* x0, const float* yref, int ny_in, const float* We,
+                                    float* xbar, float* ubar, int* status, int* qp_iter, float* qp_res, void* stream,
+                                    const nmpc_stage_io* io)
+{
+    const TraceRange trace("nmpc_batch_solve_iterate_staged");
+    if (!io || !io->in_h || !io->in_d || !io->out_h || !io->out_d || io->in_n < 0 || io->out_n < 0)
+        return set_err(NMPC_ERR_ARG, "staged I/O: host and device blocks are required");
+    return solve_iterate(b, 1, x0, yref, ny_in, We, nullptr, xbar, ubar, 1, status, qp_iter, qp_res, stream, io);
 }
 
 int nmpc_batch_run(nmpc_batch* b, int B, const float* pose, const float* vel, const float* steer,

@@ -8,6 +8,22 @@
 #include "nmpc_amd/nmpc_path.h"
 #include "nmpc_models.hpp"
 
+// Internal to the library (acados_shim.cpp -> nmpc_batch.cpp, not part of the public ABI): nmpc_batch_solve_iterate
+// for one robot whose I/O block the row-parallel kernel stages itself (KArgs::stage_*): it reads [in_d, in_d + in_n)
+// from the host-mapped in_h at its start and writes [out_d, out_d + out_n) to the host-mapped out_h at its end.
+// NMPC_ERR_ARG when the launch would not run the row-parallel kernel.
+struct nmpc_stage_io {
+    const float* in_h;
+    float* in_d;
+    int in_n;
+    float* out_h;
+    const float* out_d;
+    int out_n;
+};
+extern "C" int nmpc_batch_solve_iterate_staged(nmpc_batch* b, const float* x0, const float* yref, int ny_in,
+                                               const float* We, float* xbar, float* ubar, int* status, int* qp_iter,
+                                               float* qp_res, void* stream, const nmpc_stage_io* io);
+
 namespace nmpc {
 
 constexpr float kPi = 3.14159265358979323846f;
@@ -69,6 +85,15 @@ struct KArgs {
     // hyb_cap blocks), the rest the team kernel (role 1, team slot t -> order[hyb_n[0] + t]); role 0: a plain launch
     const int* hyb_n;
     int hyb_role, hyb_cap;
+    // one-robot capsule solves (acados_shim.cpp, k_sqp_rti_rowpar only): the kernel copies the capsule's input block
+    // from host-mapped memory into the device block at its start and the output block back at its end, in place of a
+    // copy launch on each side (stage_in_n / stage_out_n = 0: nothing staged)
+    const float* stage_in_h;
+    float* stage_in_d;
+    int stage_in_n;
+    float* stage_out_h;
+    const float* stage_out_d;
+    int stage_out_n;
 };
 
 template <class M>

@@ -252,6 +252,27 @@ __global__ __launch_bounds__(64 * W, (SEG && M::NX < 10 && W <= kRowparW2Max) ? 
 #define XB(k, j) a.xbar[((size_t)(k) * NX + (j)) * S + inst]
 #define UBAR(k, j) a.ubar[((size_t)(k) * NU + (j)) * S + inst]
 
+    // ---- staged capsule input (one robot): host-mapped block -> device block, every thread's loads in flight
+    // together (one round trip of host memory instead of a copy launch and its dispatch gap before this kernel)
+    if (a.stage_in_n > 0) {
+        constexpr int T = 64 * W, U = 8;
+        for (int e0 = 0; e0 < a.stage_in_n; e0 += T * U) {
+            float v[U];
+#pragma unroll
+            for (int j = 0; j < U; j++) {
+                const int e = e0 + j * T + tid;
+                v[j] = a.stage_in_h[e < a.stage_in_n ? e : 0];
+            }
+#pragma unroll
+            for (int j = 0; j < U; j++) {
+                const int e = e0 + j * T + tid;
+                if (e < a.stage_in_n) a.stage_in_d[e] = v[j];
+            }
+        }
+        __threadfence_block();
+        __syncthreads();
+    }
+
     // ---- reset ({name}_acados_reset: zero iterate) ----------------------------------------------------------
     if (a.reset && a.reset[inst]) {
         for (int e = tid; e < (N + 1) * NX; e += 64 * W) XB(e / NX, e % NX) = 0.0f;
@@ -1498,6 +1519,12 @@ __global__ __launch_bounds__(64 * W, (SEG && M::NX < 10 && W <= kRowparW2Max) ? 
 #pragma unroll
             for (int j = 0; j < 3; j++) a.cmd[(size_t)j * Bn + inst] = 0.0f;
         }
+    }
+    // ---- staged capsule output: device block -> host-mapped block once every output above is stored
+    if (a.stage_out_n > 0) {
+        __threadfence_block();
+        __syncthreads();
+        for (int e = tid; e < a.stage_out_n; e += 64 * W) a.stage_out_h[e] = a.stage_out_d[e];
     }
 #undef XB
 #undef UBAR
