@@ -390,53 +390,61 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a)
             ref_y = in ? trk[1] : ref_y;
             ref_t = in ? thu : ref_t;
             if (k == N - 1) { prv_x = ref_x; prv_y = ref_y; prv_t = ref_t; }
-            yr = (is_x && xi == 0) ? ref_x : ((is_x && xi == 1) ? ref_y : ((is_x && xi == 2) ? ref_t : 0.0f));
+            // (one select per value: the nested conditional compiled to lane-mask branches)
+            float v = 0.0f;
+            v = (is_x && xi == 2) ? ref_t : v;
+            v = (is_x && xi == 1) ? ref_y : v;
+            v = (is_x && xi == 0) ? ref_x : v;
+            yr = v;
         }
         float rec[RS];
 #pragma unroll
         for (int f = 0; f < RS; f++) rec[f] = 0.0f;
         const bool vu = is_u && k < N, vx = is_x && k >= 1;
         const bool valid = vu || vx;
-        // gradient of the Gauss-Newton cost (stage weights scaled by dt, terminal weight unscaled)
-        if (vu) rec[R::GR] = sc * w_lane * (zbar - yr);
-        if (vx) {
-            float w = sc * w_lane;
-            if (k == N) {
-                w = we_lane;
-                if (mode == kModeRun && P.terminal_hack && xi < 3) {  // NMPCNavControlDiff.cpp:127-139
-                    const bool eq = (ref_x == prv_x) && (ref_y == prv_y) && (ref_t == prv_t);
-                    w = (eq ? 100.0f : 1.0f) * w_lane;
-                    we_lane = w;
-                }
+        // gradient of the Gauss-Newton cost (stage weights scaled by dt, terminal weight unscaled). Every per-lane
+        // condition of this body is a select: as lane-mask branches they cost P0 about 14 branch regions per stage
+        float w = sc * w_lane;
+        if (k == N) {  // (k is wave-uniform)
+            float wt = we_lane;
+            if (mode == kModeRun && P.terminal_hack) {  // NMPCNavControlDiff.cpp:127-139
+                const bool eq = (ref_x == prv_x) && (ref_y == prv_y) && (ref_t == prv_t);
+                const float wh = (eq ? 100.0f : 1.0f) * w_lane;
+                const bool hk = is_x && xi < 3;
+                wt = hk ? wh : wt;
+                we_lane = hk ? wh : we_lane;
             }
-            rec[R::GR] = w * (zbar - yr);
+            w = vx ? wt : w;
         }
+        rec[R::GR] = valid ? w * (zbar - yr) : 0.0f;
         // iterate, bounds, slacks, multipliers
         const float z = vx ? dx : 0.0f;
         rec[R::Z] = z;
         // slots without a bound (or outside their stage range) get a sentinel bound at +-kFar with slack kFar
         // and zero multipliers: every bounded-variable expression of the sweeps then vanishes on them (r = 0,
         // Sigma = 0, no step bound), so the sweeps need no per-lane branches
-        rec[R::TL] = kFar;
-        rec[R::TU] = kFar;
-        rec[R::LB] = -kFar;
-        rec[R::UB] = kFar;
-        if (valid && has_b) {
+        {
+            const bool bd = valid && has_b;
             const float lb = lo_b - zbar, ubd = hi_b - zbar;
             const float tl = fmaxf(z - lb, P.thr0), tu = fmaxf(ubd - z, P.thr0);
-            rec[R::LB] = lb;
-            rec[R::UB] = ubd;
-            rec[R::TL] = tl;
-            rec[R::TU] = tu;
             // cold: t lambda = mu0; warm: the previous multipliers, floored at kappa / t
             // (previous multipliers capped at kWarmLambdaCap: a feasible QP of this OCP ends with multipliers of
             // the size of its weights, < 1e2; a runaway value from a struggling solve would start the IPM at a huge
             // complementarity)
-            const float ll0 = warm ? fmaxf(fminf(lp.x, kWarmLambdaCap), P.warm_kappa / tl) : P.mu0 / tl;
-            const float lu0 = warm ? fmaxf(fminf(lp.y, kWarmLambdaCap), P.warm_kappa / tu) : P.mu0 / tu;
-            rec[R::LL] = ll0;
-            rec[R::LU] = lu0;
-            sum_c0 += ll0 * tl + lu0 * tu;
+            // (one division per slack: with one per branch of the warm flag, a per-team value, the compiler split
+            // the lanes around two division sequences)
+            const float num = warm ? P.warm_kappa : P.mu0;
+            const float ql = num / tl, qu = num / tu;
+            const float ll0 = warm ? fmaxf(fminf(lp.x, kWarmLambdaCap), ql) : ql;
+            const float lu0 = warm ? fmaxf(fminf(lp.y, kWarmLambdaCap), qu) : qu;
+            rec[R::LB] = bd ? lb : -kFar;
+            rec[R::UB] = bd ? ubd : kFar;
+            rec[R::TL] = bd ? tl : kFar;
+            rec[R::TU] = bd ? tu : kFar;
+            rec[R::LL] = bd ? ll0 : 0.0f;
+            rec[R::LU] = bd ? lu0 : 0.0f;
+            const float c0 = ll0 * tl + lu0 * tu;
+            sum_c0 += bd ? c0 : 0.0f;
         }
 #pragma unroll
         for (int i = 0; i < NGV; i++) rec[R::GV + i] = (k < N && lv) ? g[i] : 0.0f;
@@ -1153,9 +1161,13 @@ __global__ __launch_bounds__(256, 1) void k_sqp_rti_team(KParams P, KArgs a)
         // entry -- idle slots, u at stage N -- read and write the dummy record): under lane masks every wait in
         // this loop was a vmcnt(0), one memory round trip per stage
         // this lane's entry of stage k (clamped: stages past N repeat stage N's, read-only below)
+        // (both candidate addresses computed for every lane, then selected: as a pointer choice per lane class the
+        // compiler branched around each address computation, two lane-mask regions per stage)
         auto entry = [&](int k) -> float* {
             const int kk = k <= N ? k : N;
-            return is_x ? &XB(kk, xi) : ((is_u && kk < N) ? &UBAR(kk, r) : tdummy);
+            float* const px = &XB(kk, xi);
+            float* const pu = &UBAR(kk < N ? kk : N - 1, is_u ? r : 0);
+            return is_x ? px : ((is_u && kk < N) ? pu : tdummy);
         };
         constexpr int EC = 8;  // stages per batch: EC loads of each kind in flight, then EC stores
         for (int k0 = 0; k0 <= N; k0 += EC) {
