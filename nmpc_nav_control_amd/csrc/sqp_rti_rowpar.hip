@@ -345,7 +345,38 @@ __global__ __launch_bounds__(64 * W, (SEG && M::NX < 10 && W <= kRowparW2Max) ? 
     const int rv = lv ? r : 0;
     auto it_rd = [&](int k, int f) -> float { return it_lds[((size_t)k * IT::NF + f) * NV + rv]; };
     auto it_wr = [&](int k, int f, bool w) -> float* { return w ? it_lds + ((size_t)k * IT::NF + f) * NV + r : lpad; };
-    {
+    // Four waves, segmented: wave 0 runs P0b's initial-iterate pass while waves 1-3 integrate the stages (P0a, rounds
+    // of 12 stages), taking each round as soon as its three waves have stored it: s_cnt counts the finished
+    // wave-rounds (an LDS word the block reductions leave unused). Otherwise every row integrates and P0b follows a
+    // block barrier. -DNMPC_P0_NO_OVERLAP keeps the barrier for A/B runs.
+#if defined(NMPC_P0_SERIAL) || defined(NMPC_P0_NO_OVERLAP)
+    constexpr bool kP0Ov = false;
+#else
+    constexpr bool kP0Ov = W == 4 && SEG;
+#endif
+    constexpr int PW = kP0Ov ? 1 : 0;           // waves that skip P0a
+    constexpr int PROWS = ROWS - 4 * PW;        // rows of P0a
+    const int prow = q - 4 * PW;                // this row among them (wave 0: negative, unused)
+    const int pnr = (N + 1 + PROWS - 1) / PROWS;  // rounds of P0a
+    unsigned int* const s_cnt = reinterpret_cast<unsigned int*>(s_red + 7);
+    if constexpr (kP0Ov) {
+        if (tid == 0) *s_cnt = 0u;
+        __syncthreads();
+    }
+    // (wave 0, and the unwrap's wave) wait until the round holding stage k is in LDS; bounded, never a hang
+    unsigned int seen = 0;
+    auto wait_stage = [&](int k) {
+        if constexpr (kP0Ov) {
+            const int kk = k <= N ? k : N;
+            const unsigned int need = (unsigned int)(W - 1) * (unsigned int)(kk / PROWS + 1);
+            for (int g = 0; seen < need && g < (1 << 24); g++) {
+                seen = __builtin_amdgcn_readfirstlane(
+                    __hip_atomic_load(s_cnt, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
+                if (seen < need) __builtin_amdgcn_s_sleep(1);
+            }
+        }
+    };
+    if (!kP0Ov || !w0) {
         struct In {
             float x[NX], u[NU], y, xnext, tq;
             float2 l;
@@ -376,7 +407,7 @@ __global__ __launch_bounds__(64 * W, (SEG && M::NX < 10 && W <= kRowparW2Max) ? 
         // rounds j = 0 .. NR-1 (row q: stage j ROWS + q) with the next round's inputs in flight (two buffers used in
         // turn: a copy between them would wait for the load still in flight)
         auto round = [&](int j, const In& cur) {
-            const int k = j * ROWS + q;
+            const int k = j * PROWS + prow;
             const bool kv = k <= N;
             if (mode == kModeRun) *((r < 3 && kv) ? my_traj + k * 3 + r : lpad) = cur.tq;
             float xn[NX], g[NX];
@@ -405,15 +436,26 @@ __global__ __launch_bounds__(64 * W, (SEG && M::NX < 10 && W <= kRowparW2Max) ? 
 #pragma unroll
             for (int i = 0; i < NGV; i++) *(kv ? st + (5 + i) * 16 : lpad) = g[i];
         };
+        // (overlap: this wave's stores of the round are in LDS, then its count)
+        auto signal = [&]() {
+            if constexpr (kP0Ov) {
+                // LDS completes in order per wave: waiting for this wave's LDS operations is the release (a
+                // workgroup-scope fence would also wait for the next round's global loads in flight)
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                if ((tid & 63) == 0) __hip_atomic_fetch_add(s_cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+        };
         In ca, cb;
-        ld(q, ca);
+        ld(prow, ca);
         for (int j = 0;; j += 2) {
-            ld((j + 1) * ROWS + q, cb);
+            ld((j + 1) * PROWS + prow, cb);
             round(j, ca);
-            if (j + 1 >= NR) break;
-            ld((j + 2) * ROWS + q, ca);
+            signal();
+            if (j + 1 >= pnr) break;
+            ld((j + 2) * PROWS + prow, ca);
             round(j + 1, cb);
-            if (j + 2 >= NR) break;
+            signal();
+            if (j + 2 >= pnr) break;
         }
     }
     // constant rows of [B A] (rows >= NGV) from stage 0 (every row, identically)
@@ -438,7 +480,7 @@ __global__ __launch_bounds__(64 * W, (SEG && M::NX < 10 && W <= kRowparW2Max) ? 
             grow[v] = sv;
         });
     }
-    __syncthreads();  // the stage inputs of every row are in LDS
+    if constexpr (!kP0Ov) __syncthreads();  // the stage inputs of every row are in LDS
     RP_STAMP(1);
 
     // ---- P0b (serial): the dynamics-feasible initial iterate dx_{k+1} = A_k dx_k + b_k on wave 0 and, in run mode,
@@ -475,15 +517,19 @@ __global__ __launch_bounds__(64 * W, (SEG && M::NX < 10 && W <= kRowparW2Max) ? 
         };
         // three buffers used in turn, loads two stages ahead (no copies: a copy waits for the LDS read in flight)
         Stg c0, c1, c2;
+        wait_stage(1);
         lds_ld(0, c0);
         lds_ld(1, c1);
         for (int k = 0;; k += 3) {  // stages 0 .. N - 1
+            wait_stage(k + 2);
             lds_ld(k + 2, c2);
             step(k, c0);
             if (k + 1 == N) break;
+            wait_stage(k + 3);
             lds_ld(k + 3, c0);
             step(k + 1, c1);
             if (k + 2 == N) break;
+            wait_stage(k + 4);
             lds_ld(k + 4, c1);
             step(k + 2, c2);
             if (k + 3 == N) break;
@@ -492,6 +538,7 @@ __global__ __launch_bounds__(64 * W, (SEG && M::NX < 10 && W <= kRowparW2Max) ? 
     }
     if (mode == kModeRun && wave == W - 1) {
         // (rows of the wave compute the same values; lanes 0-2 of each row store them, the rest store to a pad)
+        wait_stage(N);  // (overlap: every round's reference poses)
         float ref_x = 0.0f, ref_y = 0.0f, ref_t = pose_th;
         auto ld_t = [&](int k, float (&t)[3]) {
             const int kk = k <= N ? k : N;
