@@ -359,8 +359,12 @@ __global__ __launch_bounds__(64 * W, (SEG && M::NX < 10 && W <= kRowparW2Max) ? 
     const int prow = q - 4 * PW;                // this row among them (wave 0: negative, unused)
     const int pnr = (N + 1 + PROWS - 1) / PROWS;  // rounds of P0a
     unsigned int* const s_cnt = reinterpret_cast<unsigned int*>(s_red + 7);
-    if constexpr (kP0Ov) {
-        if (tid == 0) *s_cnt = 0u;
+    if constexpr (W >= 2 && SEG) {  // (and phase B's counts of finished factorisation stages, s_red[15], s_red[23])
+        if (tid == 0) {
+            *s_cnt = 0u;
+            reinterpret_cast<unsigned int*>(s_red)[15] = 0u;
+            if constexpr (W == 4) reinterpret_cast<unsigned int*>(s_red)[23] = 0u;
+        }
         __syncthreads();
     }
     // (wave 0, and the unwrap's wave) wait until the round holding stage k is in LDS; bounded, never a hang
@@ -800,6 +804,7 @@ __global__ __launch_bounds__(64 * W, (SEG && M::NX < 10 && W <= kRowparW2Max) ? 
     float exit_res[3] = {0.0f, 0.0f, 0.0f};
     float alpha = 0.0f, sigma_mu = 0.0f, mu_prev = 3.0e38f;
     float tg_rhs = P.sd_hi * sum_c0 * inv_m2;
+    int bseg_runs = 0;  // (SEG) executions of phase B so far
     for (int it = 0;; it++) {
         // phase A (stage-parallel): apply the previous step, residuals, barrier weight, rhs terms
         const float a_upd = (it > 0) ? alpha : 0.0f;
@@ -912,6 +917,19 @@ __global__ __launch_bounds__(64 * W, (SEG && M::NX < 10 && W <= kRowparW2Max) ? 
             // j = 0 initialises: the last row with the terminal P_N, p_N; the others with P = 0, p = 0, Phi = I
             const int Sg = a.seg, Ls = N / Sg;
             const bool srow = q < Sg, slast = q == Sg - 1;
+            // Two or four waves and at most 4 W / 2 segments: the lam sensitivities (Phi, Z, Gam, t) of segment q run
+            // on row q + 2 W (the second half of the waves), one stage behind its factorisation on row q (the first
+            // half), from the factor columns LR / LM the factorisation leaves in LDS (a count per factor wave of its
+            // finished stages); the factorisation's chain loses the sensitivities' ~130 instructions per stage (same
+            // box: capsule -5 %, diff1024 +3.7 %, profiles/r06/ab/sens_split.txt). Otherwise each row does both.
+            // -DNMPC_SENS_FUSED keeps them together for A/B runs.
+#ifdef NMPC_SENS_FUSED
+            constexpr bool kSensSplit = false;
+#else
+            constexpr bool kSensSplit = W >= 2;
+#endif
+            constexpr int SW = W / 2, SOFF = 4 * SW;  // factor waves [0, SW), sensitivity rows q + SOFF
+            const bool ssplit = kSensSplit && Sg <= SOFF;
             double Lrow[NV];
             float pv = 0.0f, Phi[NX], tt = 0.0f, nanb = 0.0f;
             double Gam[NX];  // fp64 sum of exact fp32 products (an fp32 sum broke the dual sweep's factor of -Gam_0)
@@ -923,6 +941,62 @@ __global__ __launch_bounds__(64 * W, (SEG && M::NX < 10 && W <= kRowparW2Max) ? 
                 Gam[c] = 0.0;
             }
             bool fail = false;
+            // one stage of the sensitivities: column c of Y = G' Phi_{k+1}, Z = L^-1 Y_u (uniform over the row), and
+            // Phi_k = Y_x - LM Z; the value's lam terms Gam -= Z'Z, t -= Z' LR; Z to LDS for phase C
+            // (column by column: the fused all-column block held 7 more accumulators live and pushed the
+            // kernel past 256 registers, one wave per SIMD: diff1024 1.65 -> 1.11 M it/s)
+            auto sens_step = [&](int k, bool srw, const float (&Gc)[NX], const float (&Lm)[NU], const float (&rLm)[NU],
+                                 const float (&lrv)[NU]) {
+                float zc[NU][NX];
+                sfor<0, NX>([&](auto cc) {
+                    constexpr int c = decltype(cc)::value;
+                    float yc = dot_x<NX, NU>(0.0f, Phi[c], Gc);
+                    sfor<0, NU>([&](auto jc) {
+                        constexpr int j2 = decltype(jc)::value;
+                        const float z = bc<j2>(yc * rLm[j2]);
+                        zc[j2][c] = z;
+                        yc -= Lm[j2] * z;
+                    });
+                    Phi[c] = is_x ? yc : 0.0f;
+                });
+                float zi[NU], zr[NX];
+#pragma unroll
+                for (int j2 = 0; j2 < NU; j2++) {
+                    float s = 0.0f;
+#pragma unroll
+                    for (int c = 0; c < NX; c++) s = (xi == c) ? zc[j2][c] : s;
+                    zi[j2] = s;
+                }
+#pragma unroll
+                for (int c = 0; c < NX; c++) {
+                    double g = Gam[c];
+#pragma unroll
+                    for (int j2 = 0; j2 < NU; j2++) g -= (double)zi[j2] * (double)zc[j2][c];
+                    Gam[c] = g;
+                    float s = zc[0][c];
+#pragma unroll
+                    for (int j2 = 1; j2 < NU; j2++) s = (r == j2) ? zc[j2][c] : s;
+                    zr[c] = s;  // input lane j: row j of Z
+                }
+#pragma unroll
+                for (int j2 = 0; j2 < NU; j2++) tt -= zi[j2] * lrv[j2];
+                if (srw && is_u) {
+                    float* const zp = seg_lds + SegL.ZL + ((size_t)k * NU + r) * SegLayout<M>::NXP;
+#pragma unroll
+                    for (int c = 0; c < NX; c++) zp[c] = zr[c];
+                }
+            };
+            // the segment's sensitivity summary for the master (state lanes: row xi of segment qq)
+            auto store_sens = [&](int qq) {
+                seg_lds[SegL.SUM_T + qq * NX + xi] = tt;
+#pragma unroll
+                for (int c = 0; c < NX; c++) {
+                    seg_lds[SegL.SUM_PHI + (qq * NX + xi) * NX + c] = Phi[c];
+                    reinterpret_cast<double*>(seg_lds + SegL.SUM_GAM)[(qq * NX + xi) * NX + c] = Gam[c];
+                }
+            };
+            // finished factorisation stages of factor wave w (waves 0-1), counted over the whole launch
+            unsigned int* const b_cnt = reinterpret_cast<unsigned int*>(s_red + 15);  // [w * 8]
             if (4 * wave < Sg) {  // (wave-uniform) the wave holds a segment
                 auto kof = [&](int j) { return srow ? (q + 1) * Ls - j : N; };
                 auto bseg = [&](int j, float (&rc)[RS]) {
@@ -991,51 +1065,16 @@ __global__ __launch_bounds__(64 * W, (SEG && M::NX < 10 && W <= kRowparW2Max) ? 
                     });
                     rc[R::LR] = my_lr;
                     pv = is_x ? y : 0.0f;
-                    // lam sensitivities: column c of Y = G' Phi_{k+1}, Z = L^-1 Y_u (uniform over the row), and
-                    // Phi_k = Y_x - LM Z; the value's lam terms Gam -= Z'Z, t -= Z' LR
-                    // (column by column: the fused all-column block held 7 more accumulators live and pushed the
-                    // kernel past 256 registers, one wave per SIMD: diff1024 1.65 -> 1.11 M it/s)
-                    float zc[NU][NX];
-                    sfor<0, NX>([&](auto cc) {
-                        constexpr int c = decltype(cc)::value;
-                        float yc = dot_x<NX, NU>(0.0f, Phi[c], Gc);
-                        sfor<0, NU>([&](auto jc) {
-                            constexpr int j2 = decltype(jc)::value;
-                            const float z = bc<j2>(yc * rLm[j2]);
-                            zc[j2][c] = z;
-                            yc -= Lm[j2] * z;
-                        });
-                        Phi[c] = is_x ? yc : 0.0f;
-                    });
-                    float zi[NU], zr[NX];
-#pragma unroll
-                    for (int j2 = 0; j2 < NU; j2++) {
-                        float s = 0.0f;
-#pragma unroll
-                        for (int c = 0; c < NX; c++) s = (xi == c) ? zc[j2][c] : s;
-                        zi[j2] = s;
-                    }
-#pragma unroll
-                    for (int c = 0; c < NX; c++) {
-                        double g = Gam[c];
-#pragma unroll
-                        for (int j2 = 0; j2 < NU; j2++) g -= (double)zi[j2] * (double)zc[j2][c];
-                        Gam[c] = g;
-                        float s = zc[0][c];
-#pragma unroll
-                        for (int j2 = 1; j2 < NU; j2++) s = (r == j2) ? zc[j2][c] : s;
-                        zr[c] = s;  // input lane j: row j of Z
-                    }
-#pragma unroll
-                    for (int j2 = 0; j2 < NU; j2++) tt -= zi[j2] * lrv[j2];
-                    if (srow && is_u) {
-                        float* const zp = seg_lds + SegL.ZL + ((size_t)k * NU + r) * SegLayout<M>::NXP;
-#pragma unroll
-                        for (int c = 0; c < NX; c++) zp[c] = zr[c];
-                    }
+                    if (!ssplit) sens_step(k, srow, Gc, Lm, rLm, lrv);
 #pragma unroll
                     for (int jj = 0; jj < NV; jj++) Lrow[jj] = Lr[jj];
                     st_lrlm(k, rc, lv && srow);
+                    if (ssplit) {
+                        // this stage's LR / LM are in LDS (LDS completes in order per wave), then its count
+                        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                        if ((tid & 63) == 0)
+                            __hip_atomic_fetch_add(b_cnt + wave * 8, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    }
                 };
                 auto load = [&](int j, float (&v)[RS]) { ld_bfields(kof(j), v); };
                 float ra[RS], rb[RS];
@@ -1054,14 +1093,55 @@ __global__ __launch_bounds__(64 * W, (SEG && M::NX < 10 && W <= kRowparW2Max) ? 
 #pragma unroll
                     for (int l = 0; l < NX; l++) sp[l] = Lrow[NU + l];
                     seg_lds[SegL.SUM_PB + q * NX + xi] = pv;
-                    seg_lds[SegL.SUM_T + q * NX + xi] = tt;
-#pragma unroll
-                    for (int c = 0; c < NX; c++) {
-                        seg_lds[SegL.SUM_PHI + (q * NX + xi) * NX + c] = Phi[c];
-                        reinterpret_cast<double*>(seg_lds + SegL.SUM_GAM)[(q * NX + xi) * NX + c] = Gam[c];
-                    }
+                    if (!ssplit) store_sens(q);
                 }
+            } else if (ssplit && wave >= SW && 4 * (wave - SW) < Sg) {
+                // the sensitivity rows: segment qs = q - SOFF, stage after stage as factor wave wave - SW finishes them
+                const int qs = q - SOFF;
+                const bool srs = qs < Sg, slast_s = qs == Sg - 1;
+                auto kos = [&](int j) { return srs ? (qs + 1) * Ls - j : N; };
+#pragma unroll
+                for (int c = 0; c < NX; c++) Phi[c] = (srs && !slast_s && is_x && xi == c) ? 1.0f : 0.0f;
+                const unsigned int base = (unsigned int)bseg_runs * (unsigned int)Ls;
+                unsigned int done_f = 0;
+                auto wait_f = [&](int j) {
+                    const unsigned int need = base + (unsigned int)j;
+                    for (int g = 0; done_f < need && g < (1 << 24); g++) {
+                        done_f = __builtin_amdgcn_readfirstlane(
+                            __hip_atomic_load(b_cnt + (wave - SW) * 8, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
+                        if (done_f < need) __builtin_amdgcn_s_sleep(1);
+                    }
+                };
+                auto sload = [&](int j, float (&v)[RS]) {
+                    ld_range<R::GV, R::GV + NGV, RS, QM>(tbase + (size_t)kos(j) * KS, v);
+                };
+                auto sstep = [&](int j, float (&rc)[RS]) {
+                    const int k = kos(j);
+                    wait_f(j);
+                    float Gc[NX];
+                    column(rc, Gc);
+                    float Lm[NU], rLm[NU], lrv[NU];
+#pragma unroll
+                    for (int qq = 0; qq < NU; qq++) {
+                        Lm[qq] = it_rd(k, IT::LM + qq);
+                        rLm[qq] = frcp(Lm[qq]);
+                        lrv[qq] = it_lds[((size_t)k * IT::NF + IT::LR) * NV + qq];  // (the LR of input lane qq)
+                    }
+                    sens_step(k, srs, Gc, Lm, rLm, lrv);
+                };
+                float ra[RS], rb[RS];
+                sload(1, ra);
+                for (int j = 1;; j += 2) {
+                    sload(j + 1 <= Ls ? j + 1 : Ls, rb);
+                    sstep(j, ra);
+                    if (j == Ls) break;
+                    sload(j + 2 <= Ls ? j + 2 : Ls, ra);
+                    sstep(j + 1, rb);
+                    if (j + 1 == Ls) break;
+                }
+                if (srs && is_x) store_sens(qs);
             }
+            bseg_runs++;
             {
                 float v[6] = {wave_max_rows(row_max16(fail ? 1.0f : 0.0f)), wave_max_rows(row_max16(nanb)), 0.0f,
                               0.0f, 0.0f, 0.0f};
