@@ -74,7 +74,10 @@ def run_pair(monkeypatch, model, N, B, seg, ticks=3, cap=64, rowpar_max=None):
 
 
 @pytest.mark.parametrize("model", ["diff", "omni4", "tric"])
-@pytest.mark.parametrize("N,seg", [(80, 5), (80, 8), (80, 2), (40, 4), (40, 1), (20, 4), (2, 2), (1, 1)])
+# (S <= 8 on four waves: the sensitivities on waves 2-3 beside the factorisation; S = 10, 16: on the factorisation's
+# own rows, DESIGN.md "Segmented Riccati")
+@pytest.mark.parametrize("N,seg", [(80, 5), (80, 8), (80, 2), (80, 10), (80, 16), (40, 4), (40, 1), (20, 4), (2, 2),
+                                   (1, 1)])
 def test_seg_matches_serial_and_oracle(built, monkeypatch, model, N, seg):
     B = 9
     out, u0_o = run_pair(monkeypatch, model, N, B, seg)
