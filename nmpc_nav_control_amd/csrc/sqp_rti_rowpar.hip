@@ -874,6 +874,34 @@ __global__ __launch_bounds__(64 * W, (SEG && M::NX < 10 && W <= kRowparW2Max) ? 
         const float mu = sum_c * inv_m2;
         RP_STAMP(3 + 4 * it);
 
+        // phase D's terms of stage k on this lane (kv: the stage is this row's): bound directions, the
+        // fraction-to-boundary step bound and the complementarity polynomial. SEG: accumulated inside phase C as each
+        // row's forward recursion produces the direction of a stage (its record fields loaded with C's), so phase D
+        // is only the block reduction; -DNMPC_D_SEPARATE keeps the separate stage-parallel pass for A/B runs
+#ifdef NMPC_D_SEPARATE
+        constexpr bool kDinC = false;
+#else
+        constexpr bool kDinC = SEG;
+#endif
+        float amax = 1e30f, s1 = 0.0f, s2 = 0.0f;
+        auto dterm = [&](int k, bool kv, const float (&rc)[RS], float dz) {
+            const bool valid = kv && ((is_u && k < N) || (is_x && k >= 1));
+            const bool bnd = valid && has_b;
+            const float z = rc[R::Z];
+            const float tl = rc[R::TL], tu = rc[R::TU], ll = rc[R::LL], lu = rc[R::LU];
+            const float rl = z - rc[R::LB] - tl, rr = rc[R::UB] - z - tu;
+            const float itl = frcp(tl), itu = frcp(tu);
+            const BoundDir d = bound_dir(dz, rl, rr, tl, tu, ll, lu, itl, itu, sigma_mu, sigma_mu);
+            if (kv) {
+                amax = step_bound_r(amax, tl, d.dtl);
+                amax = step_bound_r(amax, tu, d.dtu);
+                amax = step_bound_r(amax, ll, d.dll);
+                amax = step_bound_r(amax, lu, d.dlu);
+            }
+            s1 += bnd ? ll * d.dtl + tl * d.dll + lu * d.dtu + tu * d.dlu : 0.0f;
+            s2 += bnd ? d.dll * d.dtl + d.dlu * d.dtu : 0.0f;
+        };
+
         if constexpr (SEG) {
             // ---- stopping rule first (phase A's sums); the stationarity residual needs the exact adjoint, a serial
             // pass run only when the rest of the first exit clause holds (typically the last one or two iterations)
@@ -1315,6 +1343,43 @@ __global__ __launch_bounds__(64 * W, (SEG && M::NX < 10 && W <= kRowparW2Max) ? 
             // ---- phase C (segments in parallel, 0 -> N): row q starts at x_{qL} = s_q and takes the stored
             // factor with LR + Z lam_{q+1}; rows other than the last stop before the next segment's first stage
             sigma_mu = tg_rhs;
+            // LR_k + Z_k lam_{q+1} of every stage of a segment with a free end costate, before the chain, over the
+            // block's lanes. Two waves: inside phase C's chain its seven LDS operand loads serialised through one
+            // register under the two-wave register bound (four dependent LDS round trips per stage in the ISA); the
+            // pass takes diff1024 1.83 -> 1.88 M it/s same-box. Four waves (one per SIMD, no such bound) lose with it
+            // (capsule 0.240 -> 0.248 ms cold: the chain's loads were already batched, the pass and its barrier are
+            // extra), so they keep the update in the chain (profiles/r06/ab/lr_pre.txt). -DNMPC_LR_IN_C: in the
+            // chain everywhere, for A/B runs
+#ifdef NMPC_LR_IN_C
+            constexpr bool kLrPre = false;
+#else
+            constexpr bool kLrPre = W == 2;
+#endif
+            if constexpr (kLrPre) {
+                // segment by segment (0 .. S - 2), one (stage, input) pair of the segment per lane of the block
+#pragma unroll 1
+                for (int qs = 0; qs < Sg - 1; qs++) {
+                    // lam_{qs+1} is block-uniform: scalar registers (the VGPRs are at the two-wave bound)
+                    float lam[NX];
+#pragma unroll
+                    for (int c = 0; c < NX; c++)
+                        lam[c] = __int_as_float(__builtin_amdgcn_readfirstlane(
+                            __float_as_int(seg_lds[SegL.SL + (qs + 1) * 2 * NX + NX + c])));
+#pragma unroll 1
+                    for (int p0 = 0; p0 < Ls * NU; p0 += 64 * W) {
+                        const bool act = p0 + tid < Ls * NU;
+                        const int p = act ? p0 + tid : 0;
+                        const int k = qs * Ls + p / NU, j = p % NU;
+                        const float* const zp = seg_lds + SegL.ZL + ((size_t)k * NU + j) * SegLayout<M>::NXP;
+                        float* const lrp = it_lds + ((size_t)k * IT::NF + IT::LR) * NV + j;
+                        float lr = *lrp;
+#pragma unroll
+                        for (int c = 0; c < NX; c++) lr += zp[c] * lam[c];
+                        if (act) *lrp = lr;
+                    }
+                }
+                __syncthreads();  // the updated LR of every stage
+            }
             if (4 * wave < Sg) {
                 const float* const sl = seg_lds + SegL.SL;
                 float lam[NX];
@@ -1336,12 +1401,15 @@ __global__ __launch_bounds__(64 * W, (SEG && M::NX < 10 && W <= kRowparW2Max) ? 
 #pragma unroll
                     for (int qq = 0; qq < NU; qq++) du_all[qq] = 0.0f;
                     if (k < N) {
-                        // LR of the segment's end costate (input lane j: row j of Z_k . lam)
-                        const float* const zp = seg_lds + SegL.ZL + ((size_t)k * NU + (is_u ? r : 0)) * SegLayout<M>::NXP;
-                        float lr = rc[R::LR];
+                        if constexpr (!kLrPre) {
+                            // LR of the segment's end costate (input lane j: row j of Z_k . lam)
+                            const float* const zp =
+                                seg_lds + SegL.ZL + ((size_t)k * NU + (is_u ? r : 0)) * SegLayout<M>::NXP;
+                            float lr = rc[R::LR];
 #pragma unroll
-                        for (int c = 0; c < NX; c++) lr += zp[c] * lam[c];
-                        rc[R::LR] = is_u ? lr : rc[R::LR];
+                            for (int c = 0; c < NX; c++) lr += zp[c] * lam[c];
+                            rc[R::LR] = is_u ? lr : rc[R::LR];
+                        }
                         float w[NU];
                         sfor<0, NU>([&](auto qc) {
                             constexpr int qq = decltype(qc)::value;
@@ -1366,9 +1434,22 @@ __global__ __launch_bounds__(64 * W, (SEG && M::NX < 10 && W <= kRowparW2Max) ? 
                     dz = is_x ? ((k >= 1) ? dxs : 0.0f) : dz;
                     dz = valid ? dz : 0.0f;
                     *it_wr(k, IT::DZ, live && lv) = dz;
+                    if constexpr (kDinC) dterm(k, live, rc, dz);
                     if (k < N) dxs = dyn(rc, dz);
                 };
-                auto load = [&](int j, float (&v)[RS]) { ld_cfields(kof(j), v); };
+                auto load = [&](int j, float (&v)[RS]) {
+                    if constexpr (kDinC) {
+                        // phase D's record fields [Z, UB] with C's Jacobian rows (one contiguous range)
+                        static_assert(R::UB + 1 == R::GV && R::Z < R::GV, "D and C record fields contiguous");
+                        const int k = kof(j);
+                        ld_range<R::Z, R::GV + NGV, RS, QM>(tbase + (size_t)k * KS, v);
+                        v[R::LR] = it_rd(k, IT::LR);
+#pragma unroll
+                        for (int qq = 0; qq < NU; qq++) v[R::LM + qq] = it_rd(k, IT::LM + qq);
+                    } else {
+                        ld_cfields(kof(j), v);
+                    }
+                };
                 float ra[RS], rb[RS];
                 load(0, ra);
                 for (int j = 0;; j += 2) {
@@ -1540,29 +1621,16 @@ __global__ __launch_bounds__(64 * W, (SEG && M::NX < 10 && W <= kRowparW2Max) ? 
             RP_STAMP(5 + 4 * it);
         }
 
-        // phase D (stage-parallel): bound directions, fraction-to-boundary step bound, complementarity polynomial
-        float amax = 1e30f, s1 = 0.0f, s2 = 0.0f;
-        spar(std::integral_constant<int, R::Z>{}, std::integral_constant<int, R::UB + 1>{},
-             [&](int j, float (&rc)[RS], float dz) {
-            const int kr = j * ROWS + q;
-            const bool kv = kr <= N;
-            const int k = kv ? kr : N;
-            const bool valid = kv && ((is_u && k < N) || (is_x && k >= 1));
-            const bool bnd = valid && has_b;
-            const float z = rc[R::Z];
-            const float tl = rc[R::TL], tu = rc[R::TU], ll = rc[R::LL], lu = rc[R::LU];
-            const float rl = z - rc[R::LB] - tl, rr = rc[R::UB] - z - tu;
-            const float itl = frcp(tl), itu = frcp(tu);
-            const BoundDir d = bound_dir(dz, rl, rr, tl, tu, ll, lu, itl, itu, sigma_mu, sigma_mu);
-            if (kv) {
-                amax = step_bound_r(amax, tl, d.dtl);
-                amax = step_bound_r(amax, tu, d.dtu);
-                amax = step_bound_r(amax, ll, d.dll);
-                amax = step_bound_r(amax, lu, d.dlu);
-            }
-            s1 += bnd ? ll * d.dtl + tl * d.dll + lu * d.dtu + tu * d.dlu : 0.0f;
-            s2 += bnd ? d.dll * d.dtl + d.dlu * d.dtu : 0.0f;
-        });
+        // phase D (stage-parallel unless accumulated in phase C): bound directions, fraction-to-boundary step bound,
+        // complementarity polynomial, reduced over the block
+        if constexpr (!kDinC) {
+            spar(std::integral_constant<int, R::Z>{}, std::integral_constant<int, R::UB + 1>{},
+                 [&](int j, float (&rc)[RS], float dz) {
+                const int kr = j * ROWS + q;
+                const bool kv = kr <= N;
+                dterm(kv ? kr : N, kv, rc, dz);
+            });
+        }
         {
             float v[6] = {wave_min_rows(row_min16(lv ? amax : 1e30f)), wave_sum_rows(row_sum16(lv ? s1 : 0.0f)),
                           wave_sum_rows(row_sum16(lv ? s2 : 0.0f)), 0.0f, 0.0f, 0.0f};

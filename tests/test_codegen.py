@@ -200,7 +200,8 @@ AB_VARIANTS = [("sqp_rti_rowpar.hip", "-DNMPC_ROWPAR_MCOL"), ("sqp_rti_rowpar.hi
                ("sqp_rti_rowpar.hip", "-DNMPC_HYBRID"), ("nmpc_batch.cpp", "-DNMPC_HYBRID"),
                ("sqp_rti_team.hip", "-DNMPC_F32_FACTOR"), ("sqp_rti_rowpar.hip", "-DNMPC_P0_SERIAL"),
                ("sqp_rti_rowpar.hip", "-DNMPC_W4_BOUND2"), ("sqp_rti_rowpar.hip", "-DNMPC_P0_NO_OVERLAP"),
-               ("sqp_rti_rowpar.hip", "-DNMPC_SENS_FUSED")]
+               ("sqp_rti_rowpar.hip", "-DNMPC_SENS_FUSED"), ("sqp_rti_rowpar.hip", "-DNMPC_D_SEPARATE"),
+               ("sqp_rti_rowpar.hip", "-DNMPC_LR_IN_C")]
 
 
 @pytest.mark.parametrize("src,flag", AB_VARIANTS, ids=[f"{s.split('.')[0]}{f[2:].lower()}" for s, f in AB_VARIANTS])
